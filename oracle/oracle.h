@@ -1,0 +1,43 @@
+/* oracle.h -- CPU restatement of the dmdqn hot path (TEST INFRASTRUCTURE).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * link or load this code; the product path (dmdqn_amd) never does.
+ */
+#ifndef DMDQN_ORACLE_H
+#define DMDQN_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    uint32_t mt[624];
+    int32_t mti;
+} orc_mt;
+
+/* ---- random streams (oracle_rng.c) ---- */
+void orc_mt_init_genrand(orc_mt *s, uint32_t seed);
+void orc_mt_init_by_array(orc_mt *s, const uint32_t *key, int len);
+void orc_py_seed(orc_mt *s, uint64_t seed);
+void orc_np_seed(orc_mt *s, uint32_t seed);
+uint32_t orc_mt_u32(orc_mt *s);
+uint32_t orc_py_randbelow(orc_mt *s, uint32_t n);
+int orc_py_sample(orc_mt *s, uint32_t n, uint32_t k, int32_t *out);
+double orc_np_rand(orc_mt *s);
+uint32_t orc_np_randint(orc_mt *s, uint32_t hi);
+double orc_np_sum(const double *a, long n);
+void orc_zscore(const double *r, long n, float *out);
+void orc_act(orc_mt *s, int nagents, double eps, const int32_t *greedy, int32_t *out);
+
+/* ---- observation / reward (oracle_obs.c) ---- */
+void orc_neighbors(int R, int C, int32_t *nbr);
+void orc_local_state(int A, const int32_t *halt, const int32_t *phase,
+                     const int32_t *tspent, int mode, float *local);
+void orc_build_obs(int R, int C, const float *local, float *obs);
+void orc_reward(int A, const float *local, double *rew);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
