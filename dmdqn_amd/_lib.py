@@ -1,0 +1,69 @@
+"""ctypes binding of libdmdqn_hip.so (the C ABI declared in include/dmdqn.h).
+
+The product path calls the HIP library only; if the library is missing or a
+call fails, it raises -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdmdqn_hip.so")
+_LIB = None
+
+vp, i32, u32, u64, f64 = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64, C.c_double
+
+# name -> argtypes (all return int status)
+SIGNATURES = {
+    "dmdqn_mt_seed_np": [vp, vp, i32, vp],
+    "dmdqn_mt_seed_py": [vp, vp, i32, vp],
+    "dmdqn_mt_draw_u32": [vp, i32, i32, vp, vp],
+    "dmdqn_act": [vp, i32, i32, f64, i32, vp, vp, vp],
+    "dmdqn_observe": [i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp],
+    "dmdqn_replay_store": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "dmdqn_replay_sample": [vp, i32, i32, i32, i32, vp, vp],
+}
+
+
+class DmdqnError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load the HIP library (raises if it is absent: no fallback path)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise DmdqnError(f"{p} not found: build it with `python -m dmdqn_amd.build` "
+                         "(the HIP path has no CPU fallback)")
+    lib = C.CDLL(p)
+    lib.dmdqn_last_error.restype = C.c_char_p
+    lib.dmdqn_last_error.argtypes = []
+    lib.dmdqn_version.restype = C.c_int
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    _LIB = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise DmdqnError(f"{name} failed (rc={rc}): {lib.dmdqn_last_error().decode()}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_of(device=None):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,75 @@
+"""Build libdmdqn_hip.so (all HIP kernels + the C ABI) for gfx950 with hipcc.
+
+The library is built in-tree (dmdqn_amd/lib/) so it travels to the GPU box with
+the repository snapshot.  Usage:  python -m dmdqn_amd.build [--force]
+"""
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+OBJDIR = os.path.join(LIBDIR, "obj")
+LIBNAME = "libdmdqn_hip.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("DMDQN_ARCH", "gfx950")
+
+# Exact-arithmetic kernels (RNG, observe, sim, replay) must not contract a*b+c
+# into an fma: the oracle (gcc, -ffp-contract=off) computes the same IEEE
+# sequence.  The learn kernel is tolerance-checked and may contract.
+COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
+          "-Wno-unused-result", "-munsafe-fp-atomics"]
+PER_FILE = {
+    "learn.hip": ["-ffp-contract=fast"],
+}
+DEFAULT_FP = ["-ffp-contract=off"]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(
+        os.path.join(HERE, "..", "include", "*.h"))
+
+
+def _compile(src, force):
+    name = os.path.basename(src)
+    obj = os.path.join(OBJDIR, name + ".o")
+    newest = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest:
+        return obj, False
+    flags = COMMON + PER_FILE.get(name, DEFAULT_FP)
+    lang = ["-x", "hip"] if name.endswith(".hip") else []
+    cmd = [HIPCC] + flags + lang + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {name}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if r.stderr.strip():
+        sys.stderr.write(r.stderr)
+    return obj, True
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OBJDIR, exist_ok=True)
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        results = list(ex.map(lambda s: _compile(s, force), srcs))
+    so = os.path.join(LIBDIR, LIBNAME)
+    objs = [o for o, _ in results]
+    if force or any(ch for _, ch in results) or not os.path.exists(so):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", so] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print(f"built {so}")
+    return so
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,138 @@
+// common.hpp -- shared host/device helpers for the dmdqn HIP kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/dmdqn.h"
+
+namespace dmdqn {
+
+// ---------------------------------------------------------------- host side
+void set_error(const char *fmt, ...);
+
+#define DMDQN_REQUIRE(cond, ...)          \
+    do {                                  \
+        if (!(cond)) {                    \
+            ::dmdqn::set_error(__VA_ARGS__); \
+            return DMDQN_EINVAL;          \
+        }                                 \
+    } while (0)
+
+#define DMDQN_LAUNCH_CHECK(what)                                              \
+    do {                                                                      \
+        hipError_t e_ = hipGetLastError();                                    \
+        if (e_ != hipSuccess) {                                               \
+            ::dmdqn::set_error("%s: %s", what, hipGetErrorString(e_));        \
+            return DMDQN_EHIP;                                                \
+        }                                                                     \
+    } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------- MT19937
+// One stream = 624 state words + position.  Device kernels that consume a
+// stream run ONE wave (64 lanes) per stream: the state lives in LDS, the twist
+// is done cooperatively, and the (data-dependent) consumption loop is executed
+// wave-uniformly so every lane sees the same draw.
+constexpr int MT_N = 624;
+constexpr int MT_M = 397;
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t hi_word, uint32_t lo_word, uint32_t far) {
+    uint32_t y = (hi_word & 0x80000000u) | (lo_word & 0x7fffffffu);
+    return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// Cooperative twist of mt[624] in LDS by the 64 lanes of a one-wave block.
+// Sequential semantics (CPython _randommodule.c genrand_uint32) are kept by
+// splitting the index range where the recurrence reads freshly written words:
+//   [0,227) reads old mt[k+397]; [227,454) reads new mt[k-227] from [0,227);
+//   [454,623) reads new mt[k-227] from [227,396); 623 reads new mt[0], mt[396].
+__device__ inline void mt_twist_wave(uint32_t *mt) {
+    const int l = threadIdx.x;
+    uint32_t nv[4];
+    // phase 1
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        int k = c * 64 + l;
+        if (k < 227) nv[c] = mt_mix(mt[k], mt[k + 1], mt[k + MT_M]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        int k = c * 64 + l;
+        if (k < 227) mt[k] = nv[c];
+    }
+    __syncthreads();
+    // phase 2a: k in [227,454)
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        int k = 227 + c * 64 + l;
+        if (k < 454) nv[c] = mt_mix(mt[k], mt[k + 1], mt[k - 227]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        int k = 227 + c * 64 + l;
+        if (k < 454) mt[k] = nv[c];
+    }
+    __syncthreads();
+    // phase 2b: k in [454,623)
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        int k = 454 + c * 64 + l;
+        if (k < 623) nv[c] = mt_mix(mt[k], mt[k + 1], mt[k - 227]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        int k = 454 + c * 64 + l;
+        if (k < 623) mt[k] = nv[c];
+    }
+    __syncthreads();
+    if (l == 0) mt[623] = mt_mix(mt[623], mt[0], mt[MT_M - 1]);
+    __syncthreads();
+}
+
+// Wave-resident stream: raw state words in LDS plus a tempered copy of the
+// current block (tempered in parallel right after each twist) so the
+// sequential consumer does one LDS read per draw.
+struct MTWave {
+    uint32_t *mt;    // [624] LDS
+    uint32_t *out;   // [624] LDS, tempered outputs of the current block
+    int mti;         // wave-uniform position
+
+    __device__ void load(const uint32_t *g) {
+        for (int i = threadIdx.x; i < MT_N; i += 64) mt[i] = g[i];
+        mti = (int)g[MT_N];
+        __syncthreads();
+        for (int i = threadIdx.x; i < MT_N; i += 64) out[i] = mt_temper(mt[i]);
+        __syncthreads();
+    }
+    __device__ void store(uint32_t *g) const {
+        for (int i = threadIdx.x; i < MT_N; i += 64) g[i] = mt[i];
+        if (threadIdx.x == 0) g[MT_N] = (uint32_t)mti;
+    }
+    __device__ void refill() {
+        mt_twist_wave(mt);
+        for (int i = threadIdx.x; i < MT_N; i += 64) out[i] = mt_temper(mt[i]);
+        __syncthreads();
+        mti = 0;
+    }
+    // Wave-uniform: every lane calls it with the same control flow.
+    __device__ __forceinline__ uint32_t next() {
+        if (mti >= MT_N) refill();
+        return out[mti++];
+    }
+};
+
+}  // namespace dmdqn

@@ -1,0 +1,73 @@
+// replay.hip -- replay ring store (ReplayBuffer.add, src/agents/dqn_agent.py:31-57).
+//
+// Layout (per agent slot, capacity cap, ring position = total_adds % cap):
+//   ring_s, ring_n : int8  [NA][cap][96]   s and s' rows (89 used, 7 zero pad)
+//   ring_a         : uint8 [NA][cap]
+//   ring_r         : f64   [NA][cap]       Python-float reward, kept in f64 so
+//                                          the batch z-score is numpy-exact
+//   ring_d         : uint8 [NA][cap]
+// Observations of this env are small integers (queue counts <= 23, one-hot,
+// time spent, -1 padding), so int8 storage is exact; any value that is not an
+// integer in [-128,127] sets *err = DMDQN_ERANGE instead of being rounded.
+#include "common.hpp"
+
+namespace dmdqn {
+
+__device__ __forceinline__ int8_t to_i8(float v, int32_t *err) {
+    float r = rintf(v);
+    if (!(r == v) || r < -128.0f || r > 127.0f) {
+        atomicExch(err, DMDQN_ERANGE);
+        return 0;
+    }
+    return (int8_t)(int)r;
+}
+
+// One thread per (agent, 4-byte group): 24 groups of 4 int8 per row.
+__global__ void k_replay_store(int NA, int cap, int slot, const float *obs_s, const float *obs_n,
+                               const int32_t *act, const double *rew, const uint8_t *done,
+                               int8_t *ring_s, int8_t *ring_n, uint8_t *ring_a, double *ring_r,
+                               uint8_t *ring_d, int32_t *err) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int agent = t / 24, grp = t - agent * 24;
+    if (agent >= NA) return;
+    const size_t row = ((size_t)agent * cap + slot);
+    char4 cs, cn;
+    int8_t bs[4], bn[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int i = grp * 4 + q;
+        bs[q] = i < DMDQN_OBS_DIM ? to_i8(obs_s[(size_t)agent * DMDQN_OBS_DIM + i], err) : 0;
+        bn[q] = i < DMDQN_OBS_DIM ? to_i8(obs_n[(size_t)agent * DMDQN_OBS_DIM + i], err) : 0;
+    }
+    cs = make_char4(bs[0], bs[1], bs[2], bs[3]);
+    cn = make_char4(bn[0], bn[1], bn[2], bn[3]);
+    reinterpret_cast<char4 *>(ring_s + row * DMDQN_ROW_BYTES)[grp] = cs;
+    reinterpret_cast<char4 *>(ring_n + row * DMDQN_ROW_BYTES)[grp] = cn;
+    if (grp == 0) {
+        ring_a[row] = (uint8_t)act[agent];
+        ring_r[row] = rew[agent];
+        ring_d[row] = done[agent] ? 1 : 0;
+    }
+}
+
+}  // namespace dmdqn
+
+using namespace dmdqn;
+
+extern "C" int dmdqn_replay_store(int NA, int cap, int slot, const float *obs_s,
+                                  const float *obs_n, const int32_t *act, const double *rew,
+                                  const uint8_t *done, int8_t *ring_s, int8_t *ring_n,
+                                  uint8_t *ring_a, double *ring_r, uint8_t *ring_d,
+                                  int32_t *err, void *stream) {
+    DMDQN_REQUIRE(NA > 0 && cap > 0 && slot >= 0 && slot < cap,
+                  "dmdqn_replay_store: NA=%d cap=%d slot=%d", NA, cap, slot);
+    DMDQN_REQUIRE(obs_s && obs_n && act && rew && done && ring_s && ring_n && ring_a && ring_r &&
+                      ring_d && err,
+                  "dmdqn_replay_store: null pointer");
+    const int threads = NA * 24;
+    hipLaunchKernelGGL(k_replay_store, dim3((threads + 255) / 256), dim3(256), 0,
+                       as_stream(stream), NA, cap, slot, obs_s, obs_n, act, rew, done, ring_s,
+                       ring_n, ring_a, ring_r, ring_d, err);
+    DMDQN_LAUNCH_CHECK("k_replay_store");
+    return DMDQN_OK;
+}

@@ -1,0 +1,132 @@
+"""Thin torch-facing wrappers over the C ABI (device tensors in, device tensors out).
+
+PyTorch is used only for device memory and the current HIP stream; every op
+below is one (or a few) launches of a hand-written gfx950 kernel in
+libdmdqn_hip.so, on torch's current stream.
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_of
+
+MT_WORDS = 625
+OBS_DIM = 89
+LOCAL_DIM = 17
+ROW_BYTES = 96
+
+
+def _check(t, dtype, shape=None, name="tensor"):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} shape {tuple(t.shape)} != {tuple(shape)}")
+
+
+# ------------------------------------------------------------------ streams
+def seed_streams(seeds, kind, device="cuda"):
+    """Device MT19937 streams, one per env.  kind 'np' (numpy RandomState.seed)
+    or 'py' (CPython random.seed).  Returns uint32-as-int32 [E, 625]."""
+    seeds = torch.as_tensor(seeds, dtype=torch.int64).to(device).contiguous()
+    E = seeds.numel()
+    st = torch.empty((E, MT_WORDS), dtype=torch.int32, device=device)
+    fn = "dmdqn_mt_seed_np" if kind == "np" else "dmdqn_mt_seed_py"
+    call(fn, ptr(st), ptr(seeds), E, stream_of(device))
+    return st
+
+
+def draw_u32(state, count):
+    E = state.shape[0]
+    out = torch.empty((E, count), dtype=torch.int32, device=state.device)
+    call("dmdqn_mt_draw_u32", ptr(state), E, count, ptr(out), stream_of(state.device))
+    return out
+
+
+# ------------------------------------------------------------------ act
+def act(np_state, A, eps=1.0, n_actions=4, greedy=None, out=None):
+    E = np_state.shape[0]
+    _check(np_state, torch.int32, (E, MT_WORDS), "np_state")
+    if out is None:
+        out = torch.empty((E, A), dtype=torch.int32, device=np_state.device)
+    if greedy is not None:
+        _check(greedy, torch.int32, (E, A), "greedy")
+    call("dmdqn_act", ptr(np_state), E, A, float(eps), n_actions, ptr(greedy), ptr(out),
+         stream_of(np_state.device))
+    return out
+
+
+# ------------------------------------------------------------------ observe
+def observe(R, C, halt, phase, tspent, mode, prev_local=None, want_obs=True):
+    E = halt.shape[0]
+    A = R * C
+    _check(halt, torch.int32, (E, A, 12), "halt")
+    _check(phase, torch.int32, (E, A), "phase")
+    _check(tspent, torch.int32, (E, A), "tspent")
+    dev = halt.device
+    local = torch.empty((E, A, LOCAL_DIM), dtype=torch.float32, device=dev)
+    obs = torch.empty((E, A, OBS_DIM), dtype=torch.float32, device=dev) if want_obs else None
+    reward = None
+    if prev_local is not None:
+        _check(prev_local, torch.float32, (E, A, LOCAL_DIM), "prev_local")
+        reward = torch.empty((E, A), dtype=torch.float64, device=dev)
+    call("dmdqn_observe", R, C, E, ptr(halt), ptr(phase), ptr(tspent), int(mode), ptr(local),
+         ptr(obs), ptr(prev_local), ptr(reward), stream_of(dev))
+    return local, obs, reward
+
+
+# ------------------------------------------------------------------ replay
+class ReplayRing:
+    """Device replay rings for NA agents (ReplayBuffer, dqn_agent.py:27-89).
+
+    Each agent keeps the last `cap` transitions; deque position p (0 = oldest)
+    lives in ring slot (start + p) % cap.  All agents add in lockstep, so one
+    host-side counter describes every ring."""
+
+    def __init__(self, NA, cap, device="cuda"):
+        self.NA, self.cap = NA, cap
+        z = dict(device=device)
+        self.s = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
+        self.n = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
+        self.a = torch.zeros((NA, cap), dtype=torch.uint8, **z)
+        self.r = torch.zeros((NA, cap), dtype=torch.float64, **z)
+        self.d = torch.zeros((NA, cap), dtype=torch.uint8, **z)
+        self.err = torch.zeros(1, dtype=torch.int32, **z)
+        self.total = 0
+
+    def __len__(self):
+        return min(self.total, self.cap)
+
+    @property
+    def start(self):
+        return 0 if self.total <= self.cap else self.total % self.cap
+
+    def store(self, obs_s, obs_n, act, rew, done):
+        NA = self.NA
+        _check(obs_s, torch.float32, (NA, OBS_DIM), "obs_s")
+        _check(obs_n, torch.float32, (NA, OBS_DIM), "obs_n")
+        _check(act, torch.int32, (NA,), "act")
+        _check(rew, torch.float64, (NA,), "rew")
+        _check(done, torch.uint8, (NA,), "done")
+        slot = self.total % self.cap
+        call("dmdqn_replay_store", NA, self.cap, slot, ptr(obs_s), ptr(obs_n), ptr(act), ptr(rew),
+             ptr(done), ptr(self.s), ptr(self.n), ptr(self.a), ptr(self.r), ptr(self.d),
+             ptr(self.err), stream_of(obs_s.device))
+        self.total += 1
+
+    def check(self):
+        """Raise if a stored value was not exactly representable (syncs)."""
+        if int(self.err.item()) != 0:
+            raise _lib.DmdqnError("replay_store: observation value not representable in int8")
+
+
+def replay_sample(py_state, A, n, k=128, out=None):
+    E = py_state.shape[0]
+    _check(py_state, torch.int32, (E, MT_WORDS), "py_state")
+    if out is None:
+        out = torch.empty((E * A, k), dtype=torch.int32, device=py_state.device)
+    call("dmdqn_replay_sample", ptr(py_state), E, A, int(n), int(k), ptr(out),
+         stream_of(py_state.device))
+    return out

@@ -1,0 +1,103 @@
+/* dmdqn.h -- C ABI of the MI355X-native dmdqn hot path (libdmdqn_hip.so).
+ *
+ * Every entry point takes plain device pointers + sizes and a hipStream_t
+ * (passed as void*; NULL = default stream), launches asynchronously on that
+ * stream and returns 0 on success or a negative DMDQN_E* code.  Argument
+ * errors are detected on the host before any launch; the message is then
+ * available from dmdqn_last_error().  No torch types cross this boundary.
+ *
+ * Units: E envs (replicas) per process, A agents (junctions, row-major J_r_c)
+ * per env, NA = E*A agent slots.  One "agent-env step" = one agent in one env
+ * completing one iteration of the reference loop (src/scripts/train.py:207-310).
+ *
+ * Which reference interface each entry point replaces is cited per function.
+ * The reference itself has no FFI (it is pure Python over TraCI/Keras); the
+ * ctypes binding a maintainer would add is shown in INTEGRATION.md.
+ */
+#ifndef DMDQN_H
+#define DMDQN_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMDQN_OK 0
+#define DMDQN_EINVAL -1   /* bad argument (shape / size / null pointer)        */
+#define DMDQN_EHIP -2     /* HIP runtime error at launch                       */
+#define DMDQN_ERANGE -3   /* value not representable in the chosen storage    */
+
+/* Number of 32-bit words of one MT19937 stream on the device: 624 state words
+ * followed by the position word (mti). */
+#define DMDQN_MT_WORDS 625
+/* Observation / local-state sizes (order_lanes.py:497, :554). */
+#define DMDQN_OBS_DIM 89
+#define DMDQN_LOCAL_DIM 17
+/* Replay row stride in bytes for int8 observation storage (89 padded). */
+#define DMDQN_ROW_BYTES 96
+
+const char *dmdqn_last_error(void);
+int dmdqn_version(void);
+
+/* ------------------------------------------------------------------ streams
+ * Seed E MT19937 streams on the device.
+ *  _np: numpy legacy RandomState.seed(int) (init_genrand); replaces the global
+ *       np.random stream drawn at src/agents/dqn_agent.py:263-265.
+ *  _py: CPython random.seed(int) (init_by_array of the 32-bit words); replaces
+ *       the global `random` stream drawn at src/agents/dqn_agent.py:63.
+ * state: uint32 [E][DMDQN_MT_WORDS];  seeds: uint64 [E] (device memory). */
+int dmdqn_mt_seed_np(uint32_t *state, const uint64_t *seeds, int E, void *stream);
+int dmdqn_mt_seed_py(uint32_t *state, const uint64_t *seeds, int E, void *stream);
+
+/* Draw `count` raw tempered uint32 outputs per stream (test hook). out [E][count]. */
+int dmdqn_mt_draw_u32(uint32_t *state, int E, int count, uint32_t *out, void *stream);
+
+/* ------------------------------------------------------------------ act
+ * Replaces DQNAgent.select_action (src/agents/dqn_agent.py:246-274) for all
+ * agents of all envs: per env, agents in junction order draw rand() then, if
+ * rand() < eps, randint(0, n_actions) from the env's numpy stream; otherwise
+ * take greedy[e*A+j] (argmax of the online Q, see dmdqn_q_argmax).
+ * greedy may be NULL only when eps >= 1.  actions: int32 [E*A]. */
+int dmdqn_act(uint32_t *np_state, int E, int A, double eps, int n_actions,
+              const int32_t *greedy, int32_t *actions, void *stream);
+
+/* ------------------------------------------------------------------ observe
+ * Replaces order_lanes.get_own_state (:430-499), build_state_vector (:502-555)
+ * and the reward lines of train.py (:159-165, :254).
+ *   halt   int32 [E][A][12]  halting vehicles per incoming lane (n,s,e,w x lane)
+ *   phase  int32 [E][A]      current TL phase index
+ *   tspent int32 [E][A]      seconds since the phase started
+ *   mode   0 = reference (traci.junction.getType absent: [0,0,0,0], -1.0)
+ *          1 = intended (PHASE_ENCODING one-hot, time spent)
+ * Outputs (any may be NULL): local f32 [E][A][17], obs f32 [E][A][89].
+ * reward f64 [E][A] is computed from prev_local (the PRE-step state, A-3);
+ * pass prev_local = NULL to skip it. */
+int dmdqn_observe(int R, int C, int E, const int32_t *halt, const int32_t *phase,
+                  const int32_t *tspent, int mode, float *local, float *obs,
+                  const float *prev_local, double *reward, void *stream);
+
+/* ------------------------------------------------------------------ replay
+ * Replaces ReplayBuffer.add (src/agents/dqn_agent.py:31-57): one transition
+ * per agent into ring slot `slot` (capacity `cap`).  Observations are stored
+ * as int8 rows of DMDQN_ROW_BYTES (exact for this env's integer features; a
+ * non-representable value sets *err to DMDQN_ERANGE).  done: uint8 [NA].
+ * ring_s / ring_n int8 [NA][cap][96]; ring_a uint8 [NA][cap];
+ * ring_r f64 [NA][cap]; ring_d uint8 [NA][cap]; err int32 [1] (device). */
+int dmdqn_replay_store(int NA, int cap, int slot, const float *obs_s,
+                       const float *obs_n, const int32_t *act, const double *rew,
+                       const uint8_t *done, int8_t *ring_s, int8_t *ring_n,
+                       uint8_t *ring_a, double *ring_r, uint8_t *ring_d,
+                       int32_t *err, void *stream);
+
+/* Replaces random.sample(self.buffer, k) (dqn_agent.py:63): per env, agents
+ * j = 0..A-1 in order draw k deque positions (0 = oldest) from a deque of
+ * length n with CPython's algorithm on the env's `random` stream.
+ * idx: int32 [E*A][k]. */
+int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int k,
+                        int32_t *idx, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
