@@ -1,0 +1,384 @@
+// sim.hip -- vectorised grid microsimulation replacing SUMO/TraCI (one block per env).
+//
+// What it replaces (src/scripts/train.py:225-236 and the TraCI reads of
+// src/experimental/order_lanes.py:449-482):
+//   traci.trafficlight.setPhase(j, ACTION_MAP[a])   -> phase = 3a, timer restart
+//   traci.simulationStep() x K                       -> K one-second substeps
+//   traci.lane.getLastStepHaltingNumber(lane)        -> halt[a][12] (v < 0.1 m/s)
+//   getPhase / getNextSwitch / getPhaseDuration      -> phase, tspent
+//   getMinExpectedNumber() == 0 or t >= MAX_SIM_TIME -> done
+// The car-following model is IDM over per-lane vehicle rings (a NEW simulator,
+// not SUMO's Krauss: parity is against the C restatement in oracle/oracle_sim.c,
+// bit-exact, which needs -ffp-contract=off and the fixed operation order below).
+//
+// One substep (time t -> t+1), each pass data-parallel over lanes, passes
+// separated by block barriers:
+//   TL    phase advance when t - start >= duration (12-phase program of
+//         grid_3x3.net.xml:893-906, actuation ignored)
+//   A     front vehicle of each lane: route, target lane, IDM vs the target
+//         lane's last vehicle (green) or the stop line (red/yellow); request
+//   B     each target lane grants at most one request (feeder priority rotates
+//         with t) if it has room
+//   C     every lane advances its vehicles front-to-back (IDM, no overlap);
+//         granted fronts leave, arrivals are removed
+//   D     target lanes append the vehicle they granted
+//   E     origin queues insert one departed vehicle per edge if there is room
+#include "common.hpp"
+#include "sim.hpp"
+
+namespace dmdqn {
+
+__device__ __forceinline__ int last_slot(int head, int cnt, int cap) {
+    int s = head + cnt - 1;
+    return s >= cap ? s - cap : s;
+}
+
+struct EnvView {
+    const dmdqn_sim &S;
+    int e, A, X, NL, cap;
+    float *x, *v;
+    int32_t *dst, *head, *cnt, *req, *gfrom;
+    float *fx, *fv;
+    int32_t *phase, *ts, *qptr, *stats;
+    const int32_t *q_off;
+    const uint16_t *q_ids, *vdst;
+
+    __device__ EnvView(const dmdqn_sim &s, int env) : S(s), e(env) {
+        A = s.R * s.C;
+        X = 2 * s.R + 2 * s.C;
+        NL = 3 * (4 * A + X);
+        cap = s.cap_lane;
+        size_t ls = (size_t)env * NL;
+        x = s.x + ls * cap;
+        v = s.v + ls * cap;
+        dst = s.dst + ls * cap;
+        head = s.head + ls;
+        cnt = s.cnt + ls;
+        req = s.req + ls;
+        gfrom = s.gfrom + ls;
+        fx = s.fx + ls;
+        fv = s.fv + ls;
+        phase = s.tl_phase + (size_t)env * A;
+        ts = s.tl_ts + (size_t)env * A;
+        qptr = s.qptr + (size_t)env * 4 * A;
+        q_off = s.q_off + (size_t)env * (4 * A + 1);
+        q_ids = s.q_ids + (size_t)env * s.nveh;
+        vdst = s.vdst + (size_t)env * s.nveh;
+        stats = s.stats + (size_t)env * 4;
+    }
+};
+
+// ---------------------------------------------------------------- substep
+__device__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
+    const dmdqn_sim &S = V.S;
+    const int R = S.R, C = S.C, A = V.A, NL = V.NL, cap = V.cap;
+    const int tid = threadIdx.x, nt = blockDim.x;
+
+    // ---- TL: natural phase advance (fixed durations)
+    for (int a = tid; a < A; a += nt) {
+        int p = V.phase[a];
+        if (t - V.ts[a] >= kPhaseDur[p]) {
+            V.phase[a] = (p + 1) % 12;
+            V.ts[a] = t;
+        }
+    }
+    __syncthreads();
+
+    // ---- A: front vehicles decide
+    for (int l = tid; l < NL; l += nt) {
+        V.req[l] = -1;
+        V.gfrom[l] = -1;
+        int n = V.cnt[l];
+        if (n == 0) continue;
+        const int e = l / 3, kf = l - 3 * e;
+        const int h0 = V.head[l];
+        const size_t base = (size_t)l * cap;
+        const float x0 = V.x[base + h0], v0 = V.v[base + h0];
+        const int d0 = V.dst[base + h0];
+        const float len = lane_length(e, A, R, C, P);
+        float acc, vn, xn;
+        if (e >= 4 * A || d0 == e) {  // exit edge or destination edge: free road
+            acc = idm_free(v0, P);
+            vn = clamp_speed(v0 + acc, P);
+            xn = x0 + vn;
+            V.req[l] = kArrive;
+        } else {
+            const int aj = e >> 2, d = e & 3, h = opp(d);
+            const int o = route_out(aj, h, d0, R, C, S.exit_ao);
+            const int m = movement(h, o);
+            const int e2 = next_edge(aj, o, R, C, S.exit_id);
+            const int k2 = lane_for(e2, kf, d0, V.cnt, A, R, C, S.exit_ao);
+            const int tl = e2 * 3 + k2;
+            const bool green = (kGreen[V.phase[aj]] >> (d * 4 + m)) & 1;
+            if (green) {
+                int nc = V.cnt[tl];
+                if (nc > 0) {
+                    int ls = last_slot(V.head[tl], nc, cap);
+                    float xl = V.x[(size_t)tl * cap + ls], vl = V.v[(size_t)tl * cap + ls];
+                    float gap = (len - x0) + (xl - P.length);
+                    acc = idm_acc(v0, gap, v0 - vl, P);
+                } else {
+                    acc = idm_free(v0, P);
+                }
+            } else {
+                float gap = (len - x0) + P.min_gap;
+                acc = idm_acc(v0, gap, v0, P);
+            }
+            vn = clamp_speed(v0 + acc, P);
+            xn = x0 + vn;
+            if (xn > len) {
+                if (green) {
+                    V.req[l] = tl;
+                } else {
+                    xn = len;
+                    vn = 0.0f;
+                }
+            }
+        }
+        V.fx[l] = xn;
+        V.fv[l] = vn;
+    }
+    __syncthreads();
+
+    // ---- B: target lanes grant one request
+    for (int tl = tid; tl < NL; tl += nt) {
+        int fl[5];
+        if (!feeders(tl / 3, A, R, C, S.exit_ao, fl)) continue;
+        const int start = t % 5;
+        for (int i = 0; i < 5; i++) {
+            int f = fl[(start + i) % 5];
+            if (V.req[f] != tl) continue;
+            int nc = V.cnt[tl];
+            bool room = nc < cap;
+            if (room && nc > 0) {
+                int ls = last_slot(V.head[tl], nc, cap);
+                room = (V.x[(size_t)tl * cap + ls] - P.length) >= P.min_gap;
+            }
+            if (room) V.gfrom[tl] = f;
+            break;  // only the highest-priority requester is considered
+        }
+    }
+    __syncthreads();
+
+    // ---- C: advance every lane; fronts leave (granted) or arrive
+    for (int l = tid; l < NL; l += nt) {
+        int n = V.cnt[l];
+        if (n == 0) continue;
+        const int e = l / 3;
+        const float len = lane_length(e, A, R, C, P);
+        const size_t base = (size_t)l * cap;
+        int hd = V.head[l];
+        // front
+        float lead_x_old = V.x[base + hd], lead_v_old = V.v[base + hd];
+        float lead_x_new = V.fx[l];
+        float fvn = V.fv[l];
+        const int rq = V.req[l];
+        bool pop = false;
+        if (rq == kArrive) {
+            pop = lead_x_new >= len;
+            if (pop) atomicAdd(&V.stats[1], 1);
+        } else if (rq >= 0) {
+            // granted? the target lane recorded the source lane in gfrom
+            pop = V.gfrom[rq] == l;
+            if (!pop) {
+                lead_x_new = len;
+                fvn = 0.0f;
+            }
+        }
+        if (!pop) {
+            V.x[base + hd] = lead_x_new;
+            V.v[base + hd] = fvn;
+        }
+        int s = hd;
+        for (int i = 1; i < n; i++) {
+            s = (s + 1 == cap) ? 0 : s + 1;
+            const float xi = V.x[base + s], vi = V.v[base + s];
+            const float gap = (lead_x_old - P.length) - xi;
+            const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
+            float vn = clamp_speed(vi + acc, P);
+            float xn = xi + vn;
+            const float lim = lead_x_new - P.length;
+            if (xn > lim) {
+                if (lim < xi) {
+                    xn = xi;
+                    vn = 0.0f;
+                } else {
+                    xn = lim;
+                    vn = lim - xi;
+                }
+            }
+            V.x[base + s] = xn;
+            V.v[base + s] = vn;
+            lead_x_old = xi;
+            lead_v_old = vi;
+            lead_x_new = xn;
+        }
+        if (pop) {
+            V.head[l] = (hd + 1 == cap) ? 0 : hd + 1;
+            V.cnt[l] = n - 1;
+        }
+    }
+    __syncthreads();
+
+    // ---- D: append granted vehicles
+    for (int tl = tid; tl < NL; tl += nt) {
+        const int f = V.gfrom[tl];
+        if (f < 0) continue;
+        const int e2 = tl / 3;
+        (void)e2;
+        const float over = V.fx[f] - lane_length(f / 3, A, R, C, P);
+        const float vin = V.fv[f];
+        // the source lane already popped its front; read its (old) destination
+        // from the slot it vacated
+        const int fh = V.head[f] == 0 ? cap - 1 : V.head[f] - 1;
+        const int dv = V.dst[(size_t)f * cap + fh];
+        int nc = V.cnt[tl];
+        float xe = over;
+        if (nc > 0) {
+            int ls = last_slot(V.head[tl], nc, cap);
+            float lim = V.x[(size_t)tl * cap + ls] - P.length - P.min_gap;
+            if (lim < xe) xe = lim;
+        }
+        if (xe < 0.0f) xe = 0.0f;
+        int slot = V.head[tl] + nc;
+        if (slot >= cap) slot -= cap;
+        V.x[(size_t)tl * cap + slot] = xe;
+        V.v[(size_t)tl * cap + slot] = vin;
+        V.dst[(size_t)tl * cap + slot] = dv;
+        V.cnt[tl] = nc + 1;
+    }
+    __syncthreads();
+
+    // ---- E: insertion from the origin queues (vehicles with depart <= t)
+    for (int e = tid; e < 4 * A; e += nt) {
+        int p = V.qptr[e];
+        if (p >= V.q_off[e + 1]) continue;
+        const int id = V.q_ids[p];
+        if ((long long)id * S.period_ms > (long long)t * 1000) continue;
+        const int d0 = V.vdst[id];
+        const int aj = e >> 2, d = e & 3, h = opp(d);
+        const int o = route_out(aj, h, d0, R, C, S.exit_ao);
+        const int m = movement(h, o);
+        const int k = lane_for_move(m, e, V.cnt);
+        const int l = e * 3 + k;
+        const int nc = V.cnt[l];
+        if (nc >= cap) continue;
+        if (nc > 0) {
+            int ls = last_slot(V.head[l], nc, cap);
+            if (V.x[(size_t)l * cap + ls] < 2.0f * P.length + P.min_gap) continue;
+        }
+        int slot = V.head[l] + nc;
+        if (slot >= cap) slot -= cap;
+        V.x[(size_t)l * cap + slot] = P.length;
+        V.v[(size_t)l * cap + slot] = 0.0f;
+        V.dst[(size_t)l * cap + slot] = d0;
+        V.cnt[l] = nc + 1;
+        V.qptr[e] = p + 1;
+        atomicAdd(&V.stats[0], 1);
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, const int32_t *actions,
+                                                  int stride, int t0, int K, int max_time,
+                                                  int32_t *halt, int32_t *phase_out,
+                                                  int32_t *tspent, uint8_t *done) {
+    EnvView V(S, blockIdx.x);
+    const int A = V.A;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (actions) {
+        for (int a = tid; a < A; a += nt) {
+            V.phase[a] = stride * actions[(size_t)blockIdx.x * A + a];
+            V.ts[a] = t0;
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < K; k++) substep(V, P, t0 + k);
+    const int t = t0 + K;
+    // halting counts on the observed (incoming) lanes + bookkeeping
+    __shared__ int s_running, s_pending;
+    if (tid == 0) { s_running = 0; s_pending = 0; }
+    __syncthreads();
+    int run = 0, pend = 0;
+    for (int l = tid; l < V.NL; l += nt) {
+        const int n = V.cnt[l];
+        run += n;
+        if (l < 12 * A) {
+            int h = 0, s = V.head[l];
+            const size_t base = (size_t)l * V.cap;
+            for (int i = 0; i < n; i++) {
+                h += V.v[base + s] < P.halt_speed ? 1 : 0;
+                s = (s + 1 == V.cap) ? 0 : s + 1;
+            }
+            halt[(size_t)blockIdx.x * 12 * A + l] = h;
+        }
+    }
+    for (int e = tid; e < 4 * A; e += nt) pend += V.q_off[e + 1] - V.qptr[e];
+    atomicAdd(&s_running, run);
+    atomicAdd(&s_pending, pend);
+    for (int a = tid; a < A; a += nt) {
+        phase_out[(size_t)blockIdx.x * A + a] = V.phase[a];
+        tspent[(size_t)blockIdx.x * A + a] = t - V.ts[a];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        V.stats[2] = s_running;
+        V.stats[3] = s_pending;
+        done[blockIdx.x] = (t >= max_time || (s_running + s_pending) == 0) ? 1 : 0;
+    }
+}
+
+__global__ void k_sim_reset(dmdqn_sim S) {
+    EnvView V(S, blockIdx.x);
+    for (int l = threadIdx.x; l < V.NL; l += blockDim.x) {
+        V.head[l] = 0;
+        V.cnt[l] = 0;
+        V.req[l] = -1;
+        V.gfrom[l] = -1;
+    }
+    for (int a = threadIdx.x; a < V.A; a += blockDim.x) {
+        V.phase[a] = 0;
+        V.ts[a] = 0;
+    }
+    for (int e = threadIdx.x; e < 4 * V.A; e += blockDim.x) V.qptr[e] = V.q_off[e];
+    if (threadIdx.x < 4) V.stats[threadIdx.x] = 0;
+}
+
+}  // namespace dmdqn
+
+using namespace dmdqn;
+
+static int check_sim(const dmdqn_sim *s) {
+    DMDQN_REQUIRE(s, "dmdqn_sim: null");
+    DMDQN_REQUIRE(s->R >= 1 && s->C >= 1 && s->R <= 10 && s->C <= 10, "dmdqn_sim: grid %dx%d",
+                  s->R, s->C);
+    DMDQN_REQUIRE(s->E >= 1 && s->cap_lane >= 2 && s->cap_lane <= 64, "dmdqn_sim: E/cap_lane");
+    DMDQN_REQUIRE(s->nveh >= 0 && s->nveh <= 65535 && s->period_ms > 0, "dmdqn_sim: demand");
+    DMDQN_REQUIRE(s->x && s->v && s->dst && s->head && s->cnt && s->req && s->gfrom && s->fx &&
+                      s->fv && s->tl_phase && s->tl_ts && s->qptr && s->q_off && s->exit_id &&
+                      s->exit_ao && s->stats && (s->nveh == 0 || (s->q_ids && s->vdst)),
+                  "dmdqn_sim: null array");
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_sim_reset(const dmdqn_sim *sim, void *stream) {
+    int rc = check_sim(sim);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_sim_reset, dim3(sim->E), dim3(256), 0, as_stream(stream), *sim);
+    DMDQN_LAUNCH_CHECK("k_sim_reset");
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *actions,
+                              int action_stride, int t0, int K, int max_time, int32_t *halt,
+                              int32_t *phase, int32_t *tspent, uint8_t *done, void *stream) {
+    int rc = check_sim(sim);
+    if (rc) return rc;
+    DMDQN_REQUIRE(idm && halt && phase && tspent && done, "dmdqn_sim_step: null output");
+    DMDQN_REQUIRE(K >= 0 && t0 >= 0 && action_stride >= 0, "dmdqn_sim_step: K/t0");
+    DMDQN_REQUIRE(action_stride * 3 < 12, "dmdqn_sim_step: action_stride*3 must be < 12");
+    hipLaunchKernelGGL(k_sim_step, dim3(sim->E), dim3(256), 0, as_stream(stream), *sim, *idm,
+                       actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+    DMDQN_LAUNCH_CHECK("k_sim_step");
+    return DMDQN_OK;
+}

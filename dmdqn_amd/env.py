@@ -1,0 +1,214 @@
+"""Vectorised traffic environment on the GPU (replaces SUMO/TraCI + order_lanes).
+
+`TrafficEnv` keeps E independent replicas of an R x C signalised grid resident
+in HBM and steps them all with one simulator launch plus one observe launch
+per RL step.  It mirrors two reference surfaces:
+
+* the batched loop body of src/scripts/train.py:207-270 -- `reset()` /
+  `step(actions[E, A])` return device tensors (obs [E,A,89] f32, reward [E,A]
+  f64, done [E] bool);
+* the class API of src/agents/sumo_env.py:SumoTrafficEnvironment -- reset /
+  step over {junction_id: ...} dicts for E = 1 (`reset_dict`, `step_dict`),
+  get_controlled_intersection_ids / get_state_size / get_action_size /
+  close_sumo.
+
+Semantics follow train.py (89-dim N,S,E,W observation, reward on the PRE-step
+state, setPhase every RL step with ACTION_MAP {0:0,1:3,2:6,3:9}, K = 10
+one-second substeps, done at t >= 2400), not sumo_env.py's 74-dim variant.
+"""
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_of
+from . import kernels as K
+from .scenario import Grid, demand_tables
+
+SIGNAL_MODES = {"reference": 0, "intended": 1}
+
+
+@dataclass
+class IDMParams:
+    """SUMO passenger-car defaults + grid_3x3 geometry."""
+    length: float = 5.0
+    min_gap: float = 2.5
+    accel: float = 2.6
+    decel: float = 4.5
+    tau: float = 1.0
+    vmax: float = 13.89
+    halt_speed: float = 0.1
+    len_inner: float = 172.8
+    len_outer: float = 86.4
+
+    def c_struct(self):
+        f = np.float32
+        two_sqrt_ab = f(2.0) * np.sqrt(f(self.accel) * f(self.decel), dtype=np.float32)
+        return CIdm(f(self.length), f(self.min_gap), f(self.accel), f(self.decel), f(self.tau),
+                    f(self.vmax), f(two_sqrt_ab), f(self.halt_speed), f(self.len_inner),
+                    f(self.len_outer))
+
+
+@dataclass
+class EnvConfig:
+    rows: int = 4
+    cols: int = 4
+    num_envs: int = 1024
+    seed: int = 0                # env e uses seed + env_offset + e
+    env_offset: int = 0          # global index of this process's first env
+    step_duration: int = 10      # STEP_DURATION (train.py:56), 1 s substeps
+    max_sim_time: int = 2400     # MAX_SIM_TIME (train.py:58)
+    action_stride: int = 3       # ACTION_MAP {a: 3a} (train.py:57)
+    signal_features: str = "reference"  # A-5: "reference" (padding) | "intended"
+    cap_lane: int = 24           # vehicle slots per lane (172.8 m / 7.5 m + 1)
+    end_ms: int = 2_500_000      # last departure (trips_p06.trips.xml:7-9)
+    period_ms: Optional[int] = None
+    idm: IDMParams = field(default_factory=IDMParams)
+
+    @property
+    def n_agents(self):
+        return self.rows * self.cols
+
+
+class CSim(C.Structure):
+    _fields_ = [("R", C.c_int32), ("C", C.c_int32), ("E", C.c_int32), ("cap_lane", C.c_int32),
+                ("period_ms", C.c_int32), ("nveh", C.c_int32)] + [
+        (n, C.c_void_p) for n in ["x", "v", "dst", "head", "cnt", "req", "gfrom", "fx", "fv",
+                                  "tl_phase", "tl_ts", "qptr", "q_off", "q_ids", "vdst",
+                                  "exit_id", "exit_ao", "stats"]]
+
+
+class CIdm(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ["length", "min_gap", "accel", "decel", "tau", "vmax",
+                                         "two_sqrt_ab", "halt_speed", "len_inner", "len_outer"]]
+
+
+_lib.SIGNATURES.update({
+    "dmdqn_sim_reset": [C.POINTER(CSim), C.c_void_p],
+    "dmdqn_sim_step": [C.POINTER(CSim), C.POINTER(CIdm), C.c_void_p, C.c_int, C.c_int, C.c_int,
+                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+})
+
+
+class TrafficEnv:
+    """E replicas of the grid on one device.  All state lives in device memory."""
+
+    def __init__(self, cfg: EnvConfig = None, device="cuda"):
+        self.cfg = cfg = cfg or EnvConfig()
+        if cfg.signal_features not in SIGNAL_MODES:
+            raise ValueError(f"signal_features must be one of {list(SIGNAL_MODES)}")
+        _lib.load()
+        self.device = torch.device(device)
+        self.grid = g = Grid(cfg.rows, cfg.cols)
+        self.R, self.C, self.A, self.E = cfg.rows, cfg.cols, g.A, cfg.num_envs
+        E, A, NL, cap = self.E, self.A, g.NL, cfg.cap_lane
+        self.seeds = np.arange(cfg.num_envs, dtype=np.int64) + cfg.seed + cfg.env_offset
+        q_ids, q_off, vdst, nveh, period = demand_tables(g, self.seeds, cfg.end_ms, cfg.period_ms)
+        self.nveh, self.period_ms = nveh, period
+        dev = self.device
+        z32 = lambda *s: torch.zeros(s, dtype=torch.int32, device=dev)  # noqa: E731
+        self.t_x = torch.zeros((E, NL, cap), dtype=torch.float32, device=dev)
+        self.t_v = torch.zeros((E, NL, cap), dtype=torch.float32, device=dev)
+        self.t_dst = z32(E, NL, cap)
+        self.t_head, self.t_cnt, self.t_req, self.t_gfrom = z32(E, NL), z32(E, NL), z32(E, NL), z32(E, NL)
+        self.t_fx = torch.zeros((E, NL), dtype=torch.float32, device=dev)
+        self.t_fv = torch.zeros((E, NL), dtype=torch.float32, device=dev)
+        self.t_phase_state, self.t_ts = z32(E, A), z32(E, A)
+        self.t_qptr = z32(E, 4 * A)
+        self.t_q_off = torch.from_numpy(q_off).to(dev)
+        self.t_q_ids = torch.from_numpy(q_ids.view(np.int16)).to(dev)
+        self.t_vdst = torch.from_numpy(vdst.view(np.int16)).to(dev)
+        self.t_exit_id = torch.from_numpy(g.exit_id.reshape(-1).copy()).to(dev)
+        self.t_exit_ao = torch.from_numpy(g.exit_ao.reshape(-1).copy()).to(dev)
+        self.t_stats = z32(E, 4)
+        self.csim = CSim(cfg.rows, cfg.cols, E, cap, period, nveh, *[
+            t.data_ptr() for t in [self.t_x, self.t_v, self.t_dst, self.t_head, self.t_cnt,
+                                   self.t_req, self.t_gfrom, self.t_fx, self.t_fv,
+                                   self.t_phase_state, self.t_ts, self.t_qptr, self.t_q_off,
+                                   self.t_q_ids, self.t_vdst, self.t_exit_id, self.t_exit_ao,
+                                   self.t_stats]])
+        self.cidm = cfg.idm.c_struct()
+        # observation buffers
+        self.halt = z32(E, A, 12)
+        self.phase = z32(E, A)
+        self.tspent = z32(E, A)
+        self.done_u8 = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self.mode = SIGNAL_MODES[cfg.signal_features]
+        self.local = None
+        self.obs = None
+        self.t = 0
+        self.episode = 0
+
+    # ------------------------------------------------------------ batched API
+    def reset(self):
+        """traci.load (train.py:190) for every replica; returns obs [E,A,89]."""
+        call("dmdqn_sim_reset", C.byref(self.csim), stream_of(self.device))
+        self.t = 0
+        self.halt.zero_()
+        self.phase.zero_()
+        self.tspent.zero_()
+        self.local, self.obs, _ = K.observe(self.R, self.C, self.halt, self.phase, self.tspent,
+                                            self.mode)
+        return self.obs
+
+    def step(self, actions):
+        """One RL step for all replicas (train.py:225-270).
+        actions int32 [E,A] on the device.  Returns (obs', reward, done, info):
+        reward [E,A] f64 is computed from the PRE-step local state (A-3)."""
+        if self.local is None:
+            raise RuntimeError("call reset() first")
+        if actions.dtype != torch.int32 or tuple(actions.shape) != (self.E, self.A):
+            raise ValueError(f"actions must be int32 [{self.E},{self.A}]")
+        cfg = self.cfg
+        call("dmdqn_sim_step", C.byref(self.csim), C.byref(self.cidm), ptr(actions),
+             cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time, ptr(self.halt),
+             ptr(self.phase), ptr(self.tspent), ptr(self.done_u8), stream_of(self.device))
+        self.t += cfg.step_duration
+        prev = self.local
+        self.local, self.obs, reward = K.observe(self.R, self.C, self.halt, self.phase,
+                                                 self.tspent, self.mode, prev_local=prev)
+        # every replica shares the clock and the demand horizon, so `done` is
+        # uniform across replicas; the host knows it without a device sync
+        done = self.t >= cfg.max_sim_time
+        info = {"simulation_time": float(self.t), "done_flags": self.done_u8}
+        return self.obs, reward, done, info
+
+    def stats(self):
+        """[E,4] inserted, arrived, running, pending (syncs)."""
+        return self.t_stats.cpu().numpy()
+
+    # ------------------------------------------------------------ reference class API
+    def get_controlled_intersection_ids(self):
+        return list(self.grid.junction_ids)
+
+    def get_state_size(self):
+        return K.OBS_DIM
+
+    def get_action_size(self, intersection_id=None):
+        return 4
+
+    def close_sumo(self):
+        pass
+
+    def reset_dict(self):
+        """SumoTrafficEnvironment.reset (sumo_env.py:420) for E = 1."""
+        obs = self.reset()[0].cpu().numpy()
+        return {j: obs[a] for a, j in enumerate(self.grid.junction_ids)}
+
+    def step_dict(self, actions):
+        """SumoTrafficEnvironment.step (sumo_env.py:434) for E = 1, train.py semantics."""
+        if self.E != 1:
+            raise ValueError("step_dict is the single-replica API (num_envs == 1)")
+        a = torch.tensor([[int(actions[j]) for j in self.grid.junction_ids]], dtype=torch.int32,
+                         device=self.device)
+        obs, rew, done, info = self.step(a)
+        obs, rew = obs[0].cpu().numpy(), rew[0].cpu().numpy()
+        ids = self.grid.junction_ids
+        info = {"simulation_time": float(self.t)}
+        if done:
+            info["termination_reason"] = "max_time_reached"
+        return ({j: obs[a] for a, j in enumerate(ids)}, {j: float(rew[a]) for a, j in enumerate(ids)},
+                bool(done), info)

@@ -97,6 +97,58 @@ int dmdqn_replay_store(int NA, int cap, int slot, const float *obs_s,
 int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int k,
                         int32_t *idx, void *stream);
 
+/* ------------------------------------------------------------------ simulator
+ * Vectorised grid microsimulation that replaces SUMO behind train.py:225-236
+ * (traci.trafficlight.setPhase x A, simulationStep x K, getTime,
+ * getMinExpectedNumber) and the lane reads of order_lanes.py:449-482
+ * (getLastStepHaltingNumber, getPhase, getNextSwitch, getPhaseDuration).
+ *
+ * Network: R x C grid of junctions J_r_c (row-major index a = r*C + c).
+ * Edges: 4*A incoming approaches (edge id a*4+d, d = 0 n, 1 s, 2 e, 3 w: the
+ * side the vehicle comes FROM) then X = 2R+2C exit edges (id 4A+x).  Each
+ * edge has 3 lanes (lane id = edge*3 + k); NL = 3*(4A+X).  Per lane a ring of
+ * cap_lane vehicle slots (front = head).  All arrays are device memory; the
+ * layout is [E][...] with the per-env block contiguous. */
+typedef struct dmdqn_sim {
+    int32_t R, C, E, cap_lane;   /* grid, envs, slots per lane                 */
+    int32_t period_ms, nveh;     /* demand: vehicle i departs at i*period_ms   */
+    float *x, *v;                /* [E][NL][cap_lane] front position, speed     */
+    int32_t *dst;                /* [E][NL][cap_lane] destination edge id       */
+    int32_t *head, *cnt;         /* [E][NL] ring head / occupancy              */
+    int32_t *req, *gfrom;        /* [E][NL] scratch: requested lane, granted src */
+    float *fx, *fv;              /* [E][NL] scratch: front vehicle tentative    */
+    int32_t *tl_phase, *tl_ts;   /* [E][A] TL phase index, phase start time     */
+    int32_t *qptr;               /* [E][4A] next vehicle of each origin queue   */
+    const int32_t *q_off;        /* [E][4A+1] origin-queue offsets into q_ids   */
+    const uint16_t *q_ids;       /* [E][nveh] vehicle ids sorted (origin, id)  */
+    const uint16_t *vdst;        /* [E][nveh] destination edge of vehicle i    */
+    const int32_t *exit_id;      /* [A*4] exit id of (a, out-dir) or -1        */
+    const int32_t *exit_ao;      /* [X][2] (a, out-dir) of exit x              */
+    int32_t *stats;              /* [E][4] inserted, arrived, running, pending */
+} dmdqn_sim;
+
+/* Car-following / geometry constants (SUMO passenger defaults + grid_3x3
+ * geometry: grid_3x3.net.xml:652-891). */
+typedef struct dmdqn_idm {
+    float length, min_gap, accel, decel, tau, vmax, two_sqrt_ab, halt_speed;
+    float len_inner, len_outer;  /* J->J lanes 172.8 m; END->J and J->END 86.4 m */
+} dmdqn_idm;
+
+/* Reset every env to t = 0: empty lanes, all TLs in phase 0 (started at 0),
+ * origin queues rewound (replaces traci.load, train.py:190). */
+int dmdqn_sim_reset(const dmdqn_sim *sim, void *stream);
+
+/* One RL step for every env (train.py:225-236): if actions != NULL set
+ * phase = action_stride*action (ACTION_MAP {0:0,1:3,2:6,3:9}) with the phase
+ * timer restarted at t0, then run K one-second substeps from time t0.
+ * Outputs after the last substep (time t0+K):
+ *   halt   int32 [E][A][12] vehicles with v < halt_speed per incoming lane
+ *   phase  int32 [E][A], tspent int32 [E][A] (= t - phase start)
+ *   done   uint8 [E] = (t0+K >= max_time) || no vehicle running or pending. */
+int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *actions,
+                   int action_stride, int t0, int K, int max_time, int32_t *halt,
+                   int32_t *phase, int32_t *tspent, uint8_t *done, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

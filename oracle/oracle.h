@@ -37,6 +37,22 @@ void orc_local_state(int A, const int32_t *halt, const int32_t *phase,
 void orc_build_obs(int R, int C, const float *local, float *obs);
 void orc_reward(int A, const float *local, double *rew);
 
+/* ---- grid microsimulation (oracle_sim.c) ---- */
+typedef struct {
+    float length, min_gap, accel, decel, tau, vmax, two_sqrt_ab, halt_speed;
+    float len_inner, len_outer;
+} orc_idm;
+typedef struct orc_env orc_env;
+orc_env *orc_env_create(int R, int C, int cap, uint64_t seed, long end_ms, int period_ms,
+                        const orc_idm *P);
+void orc_env_free(orc_env *g);
+void orc_env_reset(orc_env *g);
+void orc_env_step(orc_env *g, const int32_t *actions, int stride, int t0, int K, int max_time,
+                  int32_t *halt, int32_t *phase, int32_t *tspent, uint8_t *done);
+int orc_env_info(const orc_env *g, int32_t *out);
+void orc_env_lanes(const orc_env *g, float *x, float *v, int32_t *dst, int32_t *head, int32_t *cnt);
+void orc_env_demand(const orc_env *g, uint16_t *q_ids, int32_t *q_off, uint16_t *vdst);
+
 #ifdef __cplusplus
 }
 #endif

@@ -151,3 +151,84 @@ def reward(local):
     out = np.zeros(local.shape[0], dtype=np.float64)
     lib().orc_reward(local.shape[0], local, out)
     return out
+
+
+# ---------------------------------------------------------------- simulator
+class CIdmO(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ["length", "min_gap", "accel", "decel", "tau", "vmax",
+                                         "two_sqrt_ab", "halt_speed", "len_inner", "len_outer"]]
+
+
+def idm_default():
+    f = np.float32
+    return CIdmO(f(5.0), f(2.5), f(2.6), f(4.5), f(1.0), f(13.89),
+                 f(2.0) * np.sqrt(f(2.6) * f(4.5), dtype=np.float32), f(0.1), f(172.8), f(86.4))
+
+
+def _declare_env(L):
+    L.orc_env_create.restype = C.c_void_p
+    L.orc_env_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_long, C.c_int,
+                                 C.POINTER(CIdmO)]
+    L.orc_env_free.argtypes = [C.c_void_p]
+    L.orc_env_reset.argtypes = [C.c_void_p]
+    L.orc_env_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                               _i32, _i32, _i32, _u8]
+    L.orc_env_info.argtypes = [C.c_void_p, _i32]
+    L.orc_env_lanes.argtypes = [C.c_void_p, _f32, _f32, _i32, _i32, _i32]
+    L.orc_env_demand.argtypes = [C.c_void_p, _u16, _i32, _u16]
+
+
+class OracleEnv:
+    """One replica of the grid microsimulation on the CPU (oracle_sim.c)."""
+
+    def __init__(self, R, Cc, seed, cap=24, end_ms=2_500_000, period_ms=0, idm=None):
+        L = lib()
+        if not hasattr(L, "_env_declared"):
+            _declare_env(L)
+            L._env_declared = True
+        self.R, self.C, self.A, self.cap = R, Cc, R * Cc, cap
+        self.idm = idm or idm_default()
+        self.h = L.orc_env_create(R, Cc, cap, seed, end_ms, period_ms or 0, C.byref(self.idm))
+        info = self.info()
+        self.NL, self.nveh = int(info[0]), int(info[1])
+
+    def __del__(self):
+        try:
+            lib().orc_env_free(self.h)
+        except Exception:
+            pass
+
+    def info(self):
+        out = np.zeros(8, dtype=np.int32)
+        lib().orc_env_info(self.h, out)
+        return out
+
+    def reset(self):
+        lib().orc_env_reset(self.h)
+
+    def step(self, actions, stride, t0, K, max_time):
+        halt = np.zeros(self.A * 12, dtype=np.int32)
+        ph = np.zeros(self.A, dtype=np.int32)
+        ts = np.zeros(self.A, dtype=np.int32)
+        done = np.zeros(1, dtype=np.uint8)
+        a = None
+        if actions is not None:
+            a = np.ascontiguousarray(actions, dtype=np.int32)
+        lib().orc_env_step(self.h, None if a is None else a.ctypes.data, stride, t0, K, max_time,
+                           halt, ph, ts, done)
+        return halt.reshape(self.A, 12), ph, ts, bool(done[0])
+
+    def lanes(self):
+        ns = self.NL * self.cap
+        x, v = np.zeros(ns, np.float32), np.zeros(ns, np.float32)
+        d = np.zeros(ns, np.int32)
+        hd, cn = np.zeros(self.NL, np.int32), np.zeros(self.NL, np.int32)
+        lib().orc_env_lanes(self.h, x, v, d, hd, cn)
+        return x.reshape(self.NL, self.cap), v.reshape(self.NL, self.cap), d.reshape(self.NL, self.cap), hd, cn
+
+    def demand(self):
+        q = np.zeros(self.nveh, np.uint16)
+        off = np.zeros(4 * self.A + 1, np.int32)
+        vd = np.zeros(self.nveh, np.uint16)
+        lib().orc_env_demand(self.h, q, off, vd)
+        return q, off, vd

@@ -1,0 +1,94 @@
+"""GPU parity of the HIP microsimulation + observe vs the C oracle (bit-exact),
+through the C ABI (TrafficEnv -> dmdqn_sim_step / dmdqn_observe)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import oracle as O  # noqa: E402
+from dmdqn_amd.env import EnvConfig, TrafficEnv  # noqa: E402
+
+
+def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_at=()):
+    cfg = EnvConfig(rows=R, cols=C, num_envs=E, seed=seed, signal_features=mode)
+    env = TrafficEnv(cfg)
+    obs = env.reset()
+    refs = [O.OracleEnv(R, C, seed + e) for e in range(E)]
+    m = 1 if mode == "intended" else 0
+    A = R * C
+    prev_local = [O.local_state(np.zeros((A, 12)), np.zeros(A), np.zeros(A), m) for _ in range(E)]
+    np.testing.assert_array_equal(obs.cpu().numpy()[0], O.build_obs(R, C, prev_local[0]))
+    rng = np.random.RandomState(seed)
+    t = 0
+    for step in range(steps):
+        acts = rng.randint(0, 4, size=(E, A)).astype(np.int32)
+        obs, rew, done, info = env.step(torch.from_numpy(acts).cuda())
+        if step % check_every and step not in full_state_at and step != steps - 1:
+            for e in range(E):
+                halt, ph, ts, _ = refs[e].step(acts[e], 3, t, 10, 2400)
+                prev_local[e] = O.local_state(halt, ph, ts, m)
+            t += 10
+            continue
+        halt_g = env.halt.cpu().numpy()
+        ph_g, ts_g = env.phase.cpu().numpy(), env.tspent.cpu().numpy()
+        obs_g, rew_g = obs.cpu().numpy(), rew.cpu().numpy()
+        done_g = info["done_flags"].cpu().numpy()
+        for e in range(E):
+            halt, ph, ts, dn = refs[e].step(acts[e], 3, t, 10, 2400)
+            np.testing.assert_array_equal(halt_g[e], halt, err_msg=f"halt env {e} step {step}")
+            np.testing.assert_array_equal(ph_g[e], ph)
+            np.testing.assert_array_equal(ts_g[e], ts)
+            assert bool(done_g[e]) == dn
+            L = O.local_state(halt, ph, ts, m)
+            np.testing.assert_array_equal(obs_g[e], O.build_obs(R, C, L))
+            np.testing.assert_array_equal(rew_g[e], O.reward(prev_local[e]))
+            prev_local[e] = L
+        t += 10
+        if step in full_state_at or step == steps - 1:
+            X = env.t_x.cpu().numpy()
+            Vv = env.t_v.cpu().numpy()
+            D = env.t_dst.cpu().numpy()
+            H = env.t_head.cpu().numpy()
+            N = env.t_cnt.cpu().numpy()
+            for e in range(E):
+                x, v, d, hd, cn = refs[e].lanes()
+                np.testing.assert_array_equal(N[e], cn)
+                np.testing.assert_array_equal(H[e], hd)
+                for l in np.nonzero(cn)[0]:
+                    idx = [(hd[l] + i) % refs[e].cap for i in range(cn[l])]
+                    np.testing.assert_array_equal(X[e, l, idx], x[l, idx], err_msg=f"x lane {l}")
+                    np.testing.assert_array_equal(Vv[e, l, idx], v[l, idx])
+                    np.testing.assert_array_equal(D[e, l, idx], d[l, idx])
+            st = env.stats()
+            for e in range(E):
+                np.testing.assert_array_equal(st[e], refs[e].info()[4:8])
+    return env
+
+
+@pytest.mark.parametrize("grid", [(1, 1), (2, 2), (3, 3), (4, 4), (2, 3)])
+def test_sim_matches_oracle(grid):
+    R, C = grid
+    _run(R, C, E=6, steps=80, full_state_at=(10, 40))
+
+
+def test_sim_8x8_matches_oracle():
+    _run(8, 8, E=3, steps=40, check_every=5, full_state_at=(20,))
+
+
+def test_sim_intended_mode_full_episode_and_reset():
+    env = _run(2, 2, E=4, steps=240, mode="intended", check_every=20)
+    assert env.t == 2400
+    obs = env.reset()
+    assert env.t == 0 and float(obs[:, :, :12].abs().sum()) == 0.0
+    assert (env.stats() == 0).all()
+
+
+def test_dict_api_single_replica():
+    env = TrafficEnv(EnvConfig(rows=3, cols=3, num_envs=1, seed=7))
+    obs = env.reset_dict()
+    assert list(obs) == [f"J_{r}_{c}" for r in range(3) for c in range(3)]
+    assert all(o.shape == (89,) and o.dtype == np.float32 for o in obs.values())
+    nobs, rew, done, info = env.step_dict({j: 1 for j in obs})
+    assert set(rew) == set(obs) and not done and info["simulation_time"] == 10.0
+    assert env.get_state_size() == 89 and env.get_action_size() == 4
