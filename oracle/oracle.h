@@ -53,6 +53,14 @@ int orc_env_info(const orc_env *g, int32_t *out);
 void orc_env_lanes(const orc_env *g, float *x, float *v, int32_t *dst, int32_t *head, int32_t *cnt);
 void orc_env_demand(const orc_env *g, uint16_t *q_ids, int32_t *q_off, uint16_t *vdst);
 
+/* ---- learn step (oracle_learn.c) ---- */
+long orc_qnet_nparams(int H1, int H2, int NA);
+void orc_qnet_forward(const float *p, int H1, int H2, int NA, const float *x, int B, float *q,
+                      float *z1c, float *z2c);
+float orc_learn(float *p, const float *target, float *m, float *v, int H1, int H2, int NA,
+                int B, const float *S, const int32_t *A, const float *Rn, const float *S2,
+                const float *Dn, const float *hyper, float *grad_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -232,3 +232,75 @@ class OracleEnv:
         vd = np.zeros(self.nveh, np.uint16)
         lib().orc_env_demand(self.h, q, off, vd)
         return q, off, vd
+
+
+# ---------------------------------------------------------------- learn
+def _declare_learn(L):
+    L.orc_qnet_nparams.restype = C.c_long
+    L.orc_qnet_nparams.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.orc_qnet_forward.argtypes = [_f32, C.c_int, C.c_int, C.c_int, _f32, C.c_int, _f32,
+                                   C.c_void_p, C.c_void_p]
+    L.orc_learn.restype = C.c_float
+    L.orc_learn.argtypes = [_f32, _f32, _f32, _f32, C.c_int, C.c_int, C.c_int, C.c_int, _f32, _i32,
+                            _f32, _f32, _f32, _f32, C.c_void_p]
+
+
+def _L():
+    L = lib()
+    if not hasattr(L, "_learn_declared"):
+        _declare_learn(L)
+        L._learn_declared = True
+    return L
+
+
+def qnet_nparams(H1=128, H2=128, NA=4):
+    return int(_L().orc_qnet_nparams(H1, H2, NA))
+
+
+def qnet_forward(p, x, H1=128, H2=128, NA=4):
+    p = np.ascontiguousarray(p, np.float32)
+    x = np.ascontiguousarray(x, np.float32)
+    q = np.zeros((x.shape[0], NA), np.float32)
+    _L().orc_qnet_forward(p, H1, H2, NA, x, x.shape[0], q, None, None)
+    return q
+
+
+def keras_adam_consts(t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
+    """Keras-3 Adam constants for step t (1-based) computed in float32 ops."""
+    f = np.float32
+    b1p = np.power(f(b1), f(t), dtype=np.float32)
+    b2p = np.power(f(b2), f(t), dtype=np.float32)
+    alpha = f(f(lr) * np.sqrt(f(1) - b2p, dtype=np.float32)) / f(f(1) - b1p)
+    return f(alpha), f(1 - b1), f(1 - b2), f(eps)
+
+
+def learn(p, target, m, v, S, A, Rn, S2, Dn, t, gamma=0.99, lr=1e-3, H1=128, H2=128, NA=4,
+          want_grad=False):
+    """In-place Keras-semantics learn step on float32 numpy arrays; returns loss (and grad)."""
+    alpha, c1, c2, eps = keras_adam_consts(t, lr)
+    hyper = np.array([np.float32(gamma), alpha, c1, c2, eps], np.float32)
+    grad = np.zeros(p.size, np.float32) if want_grad else None
+    B = S.shape[0]
+    loss = _L().orc_learn(p, np.ascontiguousarray(target, np.float32), m, v, H1, H2, NA, B,
+                          np.ascontiguousarray(S, np.float32), np.ascontiguousarray(A, np.int32),
+                          np.ascontiguousarray(Rn, np.float32), np.ascontiguousarray(S2, np.float32),
+                          np.ascontiguousarray(Dn, np.float32), hyper,
+                          None if grad is None else grad.ctypes.data)
+    return (loss, grad) if want_grad else loss
+
+
+def keras_init(rng, H1=128, H2=128, NA=4):
+    """HeNormal (truncated, stddev sqrt(2/fan_in)/0.8796) hidden kernels,
+    GlorotUniform output kernel, zero biases (dqn_agent.py:160-181)."""
+    def he(fi, fo):
+        std = np.sqrt(2.0 / fi) / 0.87962566103423978
+        w = rng.normal(0, std, size=(fi, fo))
+        bad = np.abs(w) > 2 * std
+        while bad.any():
+            w[bad] = rng.normal(0, std, size=bad.sum())
+            bad = np.abs(w) > 2 * std
+        return w
+    lim = np.sqrt(6.0 / (H2 + NA))
+    parts = [he(89, H1), np.zeros(H1), he(H1, H2), np.zeros(H2),
+             rng.uniform(-lim, lim, size=(H2, NA)), np.zeros(NA)]
+    return np.concatenate([x.reshape(-1) for x in parts]).astype(np.float32)

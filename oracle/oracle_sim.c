@@ -171,7 +171,7 @@ static void make_demand(orc_env *g, uint64_t seed, long end_ms) {
     int *origin = (int *)malloc(sizeof(int) * N);
     g->q_ids = (uint16_t *)malloc(sizeof(uint16_t) * (N ? N : 1));
     g->vdst = (uint16_t *)malloc(sizeof(uint16_t) * (N ? N : 1));
-    g->q_off = (int *)calloc(no + 1, sizeof(int));
+    g->q_off = (int *)calloc((size_t)(no > 0 ? no + 1 : 1), sizeof(int));
     for (int i = 0; i < N; i++) {
         uint64_t z = splitmix64(seed ^ ((uint64_t)i * 0xD1B54A32D192ED03ull));
         int o = pick(ocum, no, z % ocum[no - 1]);
@@ -186,7 +186,7 @@ static void make_demand(orc_env *g, uint64_t seed, long end_ms) {
         g->q_off[o + 1]++;
     }
     for (int e = 0; e < no; e++) g->q_off[e + 1] += g->q_off[e];
-    int *fill = (int *)calloc(no, sizeof(int));
+    int *fill = (int *)calloc((size_t)(no > 0 ? no : 1), sizeof(int));
     for (int i = 0; i < N; i++) { /* stable: ids ascending within an origin */
         int o = origin[i];
         g->q_ids[g->q_off[o] + fill[o]++] = (uint16_t)i;
