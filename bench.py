@@ -1,0 +1,242 @@
+#!/usr/bin/env python
+"""bench.py -- agent-env steps/s of the full dmdqn RL loop on MI355X.
+
+Metric (BASELINE.json): agent-env steps/sec (whole node), 16-intersection x 1024
+envs.  One "step" is one iteration of the reference loop body
+(src/scripts/train.py:207-310) for every agent of every env replica:
+act -> setPhase + 10 one-second substeps -> observe/reward -> remember ->
+replay (sample + fused Double-DQN learn with Adam).  Inputs are synthetic
+(4x4 grid + randomTrips-style demand generated on the host, random-init
+Keras-style weights) and resident in HBM before the timed region.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run, one rank per GPU, each with its own env shard
+(env ids offset by rank), no data-path collectives ("weak" scaling).
+The replay rings are first filled for batch_size-1 untimed steps so that the
+learn step is active in every warm-up and timed step (train.py learns only
+once a buffer holds batch_size transitions, dqn_agent.py:333).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+REPLAY_ROW_BYTES = 721  # canonical fp32 transition: 2*89*4 + 4 (a) + 4 (r) + 1 (d)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def learn_bytes_per_agent(P, batch=128):
+    """Algorithmic HBM bytes of one agent's learn:
+    replay gather batch*721 + Adam/target traffic 28*P (read w, m, v, w_target;
+    write w, m, v; 4 B each)."""
+    return batch * REPLAY_ROW_BYTES + 28 * P
+
+
+def cpu_baseline(rows, cols, budget_s=15.0, max_steps=200, seed=0):
+    """The C oracle (oracle/, a restatement of the reference semantics) running
+    the same loop for ONE env of the same grid, 1 thread, learn active.
+    Returns (agent-env steps/s, sample description)."""
+    import oracle as O
+    A = rows * cols
+    env = O.OracleEnv(rows, cols, seed)
+    nps, pys = O.np_stream(seed), O.py_stream(seed)
+    rng = np.random.RandomState(seed)
+    P = O.qnet_nparams()
+    params = [O.keras_init(rng) for _ in range(A)]
+    target = [p.copy() for p in params]
+    m = [np.zeros(P, np.float32) for _ in range(A)]
+    v = [np.zeros(P, np.float32) for _ in range(A)]
+    cap, B = 10000, 128
+    S = np.zeros((A, cap, 89), np.float32)
+    S2 = np.zeros((A, cap, 89), np.float32)
+    Aa = np.zeros((A, cap), np.int32)
+    Rr = np.zeros((A, cap), np.float64)
+    Dd = np.zeros((A, cap), np.float32)
+    L = O.local_state(np.zeros((A, 12)), np.zeros(A), np.zeros(A), 0)
+    obs = O.build_obs(rows, cols, L)
+    t, n, learn_steps = 0, 0, 0
+
+    def one_step(learn):
+        nonlocal t, n, L, obs, learn_steps
+        acts = O.act(nps, A, 1.0)
+        halt, ph, ts, done = env.step(acts, 3, t, 10, 2400)
+        t += 10
+        L2 = O.local_state(halt, ph, ts, 0)
+        obs2 = O.build_obs(rows, cols, L2)
+        rew = O.reward(L)
+        slot = n % cap
+        S[:, slot], S2[:, slot], Aa[:, slot], Rr[:, slot], Dd[:, slot] = obs, obs2, acts, rew, done
+        n += 1
+        size = min(n, cap)
+        if learn and size >= B:
+            learn_steps += 1
+            start = 0 if n <= cap else n % cap
+            for j in range(A):
+                idx = (start + O.py_sample(pys, size, B)) % cap
+                O.learn(params[j], target[j], m[j], v[j], S[j, idx], Aa[j, idx],
+                        O.zscore(Rr[j, idx]), S2[j, idx], Dd[j, idx], learn_steps)
+            if learn_steps % 500 == 0:
+                for j in range(A):
+                    target[j][:] = params[j]
+        L, obs = L2, obs2
+        if done:
+            env.reset()
+            t = 0
+
+    for _ in range(B - 1):  # replay fill, untimed (learn inactive, as in the reference)
+        one_step(False)
+    steps = 0
+    t0 = time.perf_counter()
+    while steps < max_steps and (time.perf_counter() - t0) < budget_s:
+        one_step(True)
+        steps += 1
+    el = time.perf_counter() - t0
+    sample = (f"1 env x {A} agents ({rows}x{cols}), {steps} RL steps with learn active after a "
+              f"{B - 1}-step untimed replay fill; C oracle (oracle/), 1 thread, {el:.1f} s")
+    return steps * A / el, sample
+
+
+def read_traffic(workload_key):
+    """Per-launch HBM bytes of the learn kernel from the committed PMC pass
+    (profiles/learn_pmc.json, written by tools/pmc_learn.py), or None."""
+    p = os.path.join(ROOT, "profiles", "learn_pmc.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--envs", type=int, default=1024, help="env replicas per GPU")
+    ap.add_argument("--rows", type=int, default=4)
+    ap.add_argument("--cols", type=int, default=4)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp16"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from dmdqn_amd.agent import AgentConfig
+    from dmdqn_amd.env import EnvConfig
+    from dmdqn_amd.trainer import Trainer
+
+    env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
+                        env_offset=rank * args.envs)
+    agent_cfg = AgentConfig(precision=args.precision, seed=1000 + rank)
+    tr = Trainer(env_cfg, agent_cfg, device=dev)
+    E, A = tr.env.E, tr.env.A
+    NA = E * A
+    for _ in range(agent_cfg.batch_size - 1):  # replay fill (no learn yet)
+        tr.step()
+    for _ in range(args.warmup):
+        tr.step()
+    assert tr.agent.learn_launches > 0 or args.warmup == 0
+
+    # HIP events bracketing each learn launch, on the stream it runs on
+    starts, ends = [], []
+
+    def hook(before):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        (starts if before else ends).append(ev)
+
+    learn_before = tr.agent.learn_launches
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    tr.agent.learn_hook = hook
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    tr.agent.learn_hook = None
+    n_learn = tr.agent.learn_launches - learn_before
+    assert n_learn == args.steps, "learn must run in every timed step"
+    learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    el_max = el
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+
+    if rank == 0:
+        value = args.steps * NA * world / el_max
+        P = tr.agent.P
+        bpl = NA * learn_bytes_per_agent(P)
+        avg_learn_s = float(np.mean(learn_ms)) / 1e3
+        achieved = bpl / avg_learn_s / 1e9
+        wl = f"{args.rows}x{args.cols}x{args.envs}"
+        traffic = read_traffic(f"{wl}_{args.precision}")
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cv, sample = cpu_baseline(args.rows, args.cols, args.cpu_budget)
+            cpu = {"value": round(cv, 2), "unit": "agent-env steps/s", "cores": 1,
+                   "kind": "port", "sample": sample}
+        out = {
+            "metric": "agent-env steps/sec (whole node), 16-intersection x 1024 envs",
+            "value": round(value, 1),
+            "unit": "agent-env steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.precision == "fp32" else "f16 (f32 accumulate, f32 master)",
+            "data": "synthetic (4x4 grid, randomTrips-style demand, Keras-style random init)",
+            "config": {
+                "workload": f"C3: {args.rows}x{args.cols} grid ({A} agents) x {args.envs} envs/GPU, "
+                            "full RL step (act, 10 IDM substeps, observe, remember, sample, "
+                            "Double-DQN learn + Adam), H=128, batch 128, replay 10000",
+                "envs_per_gpu": args.envs, "agents_per_env": A, "global_envs": args.envs * world,
+                "replay_prefill_steps": agent_cfg.batch_size - 1,
+                "parallelism": f"env-shard x{world} (no collectives)",
+                "precision": args.precision,
+            },
+            "roofline": {
+                "kernel": "k_learn (fused gather + 3x fwd + bwd + Adam, MFMA)",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "bytes_per_launch": bpl,
+                "avg_launch_ms": round(avg_learn_s * 1e3, 4),
+                "learn_share_of_step": round(avg_learn_s / (el_max / args.steps), 3),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

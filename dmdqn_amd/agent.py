@@ -1,0 +1,243 @@
+"""Batched Double-DQN agents on the GPU (replaces src/agents/dqn_agent.py).
+
+`BatchedDQN` holds NA = E*A independent agents (one per junction per env
+replica): online / target Q-networks, Keras-3 Adam slots, replay rings and the
+per-env random streams, all resident in HBM.  One call of each method acts,
+stores or learns for every agent:
+
+  act(obs)                         DQNAgent.select_action  (dqn_agent.py:246-274)
+  remember(s, a, r, s', done)      DQNAgent.remember       (:312-326)
+  replay()                         DQNAgent.replay / learn (:328-380, :428-434)
+  update_target_network()          (:382-387)
+
+Draw-order contract (bit-exact with the reference when E = 1 and the global
+streams are seeded with random.seed(s) / np.random.seed(s)): per env, agents
+in junction order draw from that env's numpy stream for act and from its
+CPython `random` stream for replay sampling.
+"""
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_of
+from . import kernels as K
+
+D_IN = 89
+N_ACTIONS = 4
+
+
+class CLearn(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ["NA", "cap", "start", "batch", "hidden", "precision",
+                                         "sync_target", "P"]] + [
+        (n, C.c_void_p) for n in ["ring_s", "ring_n", "ring_a", "ring_d", "ring_r", "idx",
+                                  "params", "adam_m", "adam_v", "target", "loss"]] + [
+        (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]]
+
+
+_lib.SIGNATURES.update({
+    "dmdqn_learn": [C.POINTER(CLearn), C.c_void_p],
+    "dmdqn_q_argmax": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                       C.c_void_p],
+})
+
+PRECISIONS = {"fp32": 0, "fp16": 1}
+
+
+def n_params(hidden, n_actions=N_ACTIONS):
+    H = hidden
+    return D_IN * H + H + H * H + H + H * n_actions + n_actions
+
+
+def keras_adam_consts(t, lr, b1=0.9, b2=0.999, eps=1e-7):
+    """keras/src/optimizers/adam.py update_step constants for local step t (f32 ops)."""
+    f = np.float32
+    b1p = np.power(f(b1), f(t), dtype=np.float32)
+    b2p = np.power(f(b2), f(t), dtype=np.float32)
+    alpha = f(f(lr) * np.sqrt(f(1) - b2p, dtype=np.float32)) / f(f(1) - b1p)
+    return float(alpha), float(f(1 - b1)), float(f(1 - b2)), float(f(eps))
+
+
+def keras_initial_weights(rng, hidden, n_agents):
+    """HeNormal (truncated at 2 sigma, stddev sqrt(2/fan_in)/0.8796) for the ReLU
+    layers, GlorotUniform for the output layer, zero biases (dqn_agent.py:160-181).
+    TF's RNG stream is not reproducible here, so initial weights are an input."""
+    H = hidden
+
+    def he(fi, fo):
+        std = np.sqrt(2.0 / fi) / 0.87962566103423978
+        w = rng.normal(0, std, size=(n_agents, fi, fo))
+        bad = np.abs(w) > 2 * std
+        while bad.any():
+            w[bad] = rng.normal(0, std, size=int(bad.sum()))
+            bad = np.abs(w) > 2 * std
+        return w.reshape(n_agents, -1)
+
+    lim = np.sqrt(6.0 / (H + N_ACTIONS))
+    parts = [he(D_IN, H), np.zeros((n_agents, H)), he(H, H), np.zeros((n_agents, H)),
+             rng.uniform(-lim, lim, size=(n_agents, H * N_ACTIONS)), np.zeros((n_agents, N_ACTIONS))]
+    return np.concatenate(parts, axis=1).astype(np.float32)
+
+
+@dataclass
+class AgentConfig:
+    """Keys of config/agent_config.yaml; defaults are the values train.py uses
+    (train.py:110-121), not the YAML file's (A-17)."""
+    learning_rate: float = 0.001
+    gamma: float = 0.99
+    epsilon_start: float = 1.0
+    epsilon_min: float = 0.01
+    epsilon_decay_steps: int = 200000
+    replay_buffer_size: int = 10000
+    batch_size: int = 128
+    target_update_frequency: int = 500
+    nn_layers: List[int] = field(default_factory=lambda: [128, 128])
+    # build-only knobs (additive)
+    precision: str = "fp32"          # "fp32" | "fp16" (mixed, the reference's policy)
+    count_env_steps: bool = False    # True fixes A-1 (epsilon decays); False = reference
+    seed: int = 0
+
+    @classmethod
+    def from_dict(cls, d):
+        known = {k: v for k, v in d.items() if k in cls.__dataclass_fields__}
+        return cls(**known)
+
+
+class BatchedDQN:
+    """E*A independent DQN agents (agent index = env * A + junction)."""
+
+    def __init__(self, num_envs, n_agents, cfg: AgentConfig = None, device="cuda",
+                 env_seeds=None, init_weights=None):
+        self.cfg = cfg = cfg or AgentConfig()
+        _lib.load()
+        H = cfg.nn_layers[0]
+        if len(cfg.nn_layers) != 2 or cfg.nn_layers[1] != H or H not in (64, 128):
+            raise ValueError("the fused learn kernel supports nn_layers [64,64] or [128,128]")
+        if cfg.batch_size != 128:
+            raise ValueError("the fused learn kernel is built for batch_size 128")
+        if cfg.precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {list(PRECISIONS)}")
+        self.device = dev = torch.device(device)
+        self.E, self.A = num_envs, n_agents
+        self.NA = NA = num_envs * n_agents
+        self.H, self.P = H, n_params(H)
+        if init_weights is None:
+            init_weights = keras_initial_weights(np.random.RandomState(cfg.seed), H, NA)
+        w = torch.as_tensor(np.asarray(init_weights, dtype=np.float32).reshape(NA, self.P))
+        self.params = w.to(dev).contiguous()
+        self.target = self.params.clone()
+        self.adam_m = torch.zeros_like(self.params)
+        self.adam_v = torch.zeros_like(self.params)
+        self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev)
+        seeds = np.arange(num_envs, dtype=np.int64) + cfg.seed if env_seeds is None else np.asarray(env_seeds)
+        self.np_state = K.seed_streams(seeds, "np", dev)
+        self.py_state = K.seed_streams(seeds, "py", dev)
+        self.idx = torch.empty((NA, cfg.batch_size), dtype=torch.int32, device=dev)
+        self.loss = torch.zeros(NA, dtype=torch.float32, device=dev)
+        self.actions = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
+        self.greedy = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
+        self.global_step_count = 0
+        self.learn_step_counter = 0
+        self.epsilon = cfg.epsilon_start
+        self.learn_launches = 0
+        self.learn_hook = None  # optional callable(before: bool), e.g. HIP event timing
+
+    # -------------------------------------------------------------- act
+    def current_epsilon(self):
+        """dqn_agent.py:258-261 (global_step_count never moves on the reference
+        training path, so epsilon stays 1.0 -- A-1)."""
+        g = self.global_step_count
+        if g < 8000:
+            self.epsilon = 1.0
+        elif self.epsilon > self.cfg.epsilon_min:
+            self.epsilon = max(0.01, 1.0 * float(np.exp(-(g - 8000) / 16000)))
+        return self.epsilon
+
+    def act(self, obs):
+        """obs f32 [E, A, 89] -> actions int32 [E, A] (device)."""
+        eps = self.current_epsilon()
+        greedy = None
+        if eps < 1.0:
+            call("dmdqn_q_argmax", ptr(self.params), self.NA, self.P, self.H,
+                 ptr(obs.reshape(self.NA, D_IN)), ptr(self.greedy), None, stream_of(self.device))
+            greedy = self.greedy
+        return K.act(self.np_state, self.A, eps=eps, n_actions=N_ACTIONS, greedy=greedy,
+                     out=self.actions)
+
+    # -------------------------------------------------------------- replay
+    def remember(self, obs, actions, rewards, next_obs, done):
+        """One transition per agent (ReplayBuffer.add).  obs/next_obs [E,A,89] f32,
+        actions [E,A] int32, rewards [E,A] f64, done: bool or uint8 [E]."""
+        NA = self.NA
+        if isinstance(done, (bool, np.bool_, int)):
+            d = torch.full((NA,), int(bool(done)), dtype=torch.uint8, device=self.device)
+        else:
+            d = done.to(torch.uint8).reshape(self.E, 1).expand(self.E, self.A).reshape(NA).contiguous()
+        self.ring.store(obs.reshape(NA, D_IN), next_obs.reshape(NA, D_IN),
+                        actions.reshape(NA), rewards.reshape(NA), d)
+        if self.cfg.count_env_steps:
+            self.global_step_count += 1
+
+    def replay(self):
+        """DQNAgent.replay for every agent: returns the loss tensor [NA] (device),
+        or None while the buffers hold fewer than batch_size transitions."""
+        return self.learn()
+
+    def learn(self):
+        n = len(self.ring)
+        if n < self.cfg.batch_size:
+            return None
+        cfg = self.cfg
+        K.replay_sample(self.py_state, self.A, n, cfg.batch_size, out=self.idx)
+        self.learn_step_counter += 1
+        alpha, c1, c2, eps = keras_adam_consts(self.learn_step_counter, cfg.learning_rate)
+        sync = self.learn_step_counter % cfg.target_update_frequency == 0
+        a = CLearn(self.NA, self.ring.cap, self.ring.start, cfg.batch_size, self.H,
+                   PRECISIONS[cfg.precision], int(sync), self.P,
+                   *[t.data_ptr() for t in [self.ring.s, self.ring.n, self.ring.a, self.ring.d,
+                                            self.ring.r, self.idx, self.params, self.adam_m,
+                                            self.adam_v, self.target, self.loss]],
+                   np.float32(cfg.gamma), alpha, c1, c2, eps)
+        if self.learn_hook:
+            self.learn_hook(True)
+        call("dmdqn_learn", C.byref(a), stream_of(self.device))
+        if self.learn_hook:
+            self.learn_hook(False)
+        self.learn_launches += 1
+        return self.loss
+
+    def update_target_network(self):
+        self.target.copy_(self.params)
+
+    # -------------------------------------------------------------- weights
+    def get_weights(self, agent):
+        """Keras get_weights() order for one agent: [W1, b1, W2, b2, W3, b3]."""
+        p = self.params[agent].cpu().numpy()
+        H = self.H
+        shapes = [(D_IN, H), (H,), (H, H), (H,), (H, N_ACTIONS), (N_ACTIONS,)]
+        out, o = [], 0
+        for sh in shapes:
+            n = int(np.prod(sh))
+            out.append(p[o:o + n].reshape(sh).copy())
+            o += n
+        return out
+
+    def set_weights(self, agent, weights):
+        flat = np.concatenate([np.asarray(w, np.float32).reshape(-1) for w in weights])
+        self.params[agent].copy_(torch.from_numpy(flat))
+        self.target[agent].copy_(self.params[agent])
+
+    def state_dict(self):
+        return {"params": self.params.cpu(), "target": self.target.cpu(),
+                "adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(),
+                "learn_step_counter": self.learn_step_counter,
+                "global_step_count": self.global_step_count}
+
+    def load_state_dict(self, sd):
+        for k in ["params", "target", "adam_m", "adam_v"]:
+            getattr(self, k).copy_(sd[k].to(self.device))
+        self.learn_step_counter = int(sd["learn_step_counter"])
+        self.global_step_count = int(sd["global_step_count"])

@@ -149,6 +149,35 @@ int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *ac
                    int action_stride, int t0, int K, int max_time, int32_t *halt,
                    int32_t *phase, int32_t *tspent, uint8_t *done, void *stream);
 
+/* ------------------------------------------------------------------ learn
+ * Replaces DQNAgent.learn (src/agents/dqn_agent.py:328-380) + the target sync
+ * (:376-377, :382-387) for NA independent agents in ONE launch (one workgroup
+ * per agent): replay gather (ReplayBuffer.sample :64-84, z-scored rewards),
+ * Double-DQN target, MSE loss, backward and Keras-3 Adam, fused.
+ * Parameters use the Keras get_weights() layout per agent:
+ *   W1[89][H] b1[H] W2[H][H] b2[H] W3[H][4] b3[4]   (P floats, row stride P).
+ * precision: 0 = fp32 MFMA (exact f32 products), 1 = fp16 MFMA with fp32
+ * accumulation and fp32 master weights (the reference's mixed_float16). */
+typedef struct dmdqn_learn_args {
+    int32_t NA, cap, start, batch, hidden, precision, sync_target, P;
+    const int8_t *ring_s, *ring_n;   /* [NA][cap][96]                        */
+    const uint8_t *ring_a, *ring_d;  /* [NA][cap]                            */
+    const double *ring_r;            /* [NA][cap]                            */
+    const int32_t *idx;              /* [NA][batch] deque positions          */
+    float *params, *adam_m, *adam_v; /* [NA][P] online weights + Adam slots  */
+    float *target;                   /* [NA][P] target network               */
+    float *loss;                     /* [NA] MSE loss of this learn (or NULL) */
+    float gamma, alpha, c1, c2, eps; /* alpha = lr*sqrt(1-b2^t)/(1-b1^t),
+                                        c1 = 1-b1, c2 = 1-b2 (float32)       */
+} dmdqn_learn_args;
+
+int dmdqn_learn(const dmdqn_learn_args *args, void *stream);
+
+/* Greedy actions argmax_a Q_online(obs) for NA agents (dqn_agent.py:268-273);
+ * obs f32 [NA][89]; out int32 [NA].  Used by dmdqn_act when eps < 1. */
+int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, const float *obs,
+                   int32_t *out, float *q_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

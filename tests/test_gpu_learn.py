@@ -1,0 +1,103 @@
+"""GPU parity of the fused learn kernel (dmdqn_learn) vs the C oracle restatement
+of DQNAgent.learn (Keras semantics), through the C ABI.
+
+Tolerances (stated): fp32 path -- loss rtol 1e-5; weights after each Adam
+step: >= 99.99 % within 1e-6 + 1e-5|w| and ALL within 1e-5 absolute (1 % of one
+Adam step at lr 1e-3; Adam's update m/(sqrt(v)+eps) amplifies the last-bit
+summation-order differences of gradients whose magnitude is near eps);
+Adam m / v rtol 1e-4 scaled by the largest gradient.  Replay indices and the
+z-scored rewards feeding the kernel are bit-exact (tested separately)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import oracle as O  # noqa: E402
+from dmdqn_amd import kernels as K  # noqa: E402
+from dmdqn_amd.agent import AgentConfig, BatchedDQN  # noqa: E402
+
+DEV = "cuda"
+
+
+def _fill(agent, T, rng):
+    E, A = agent.E, agent.A
+    for t in range(T):
+        s = torch.from_numpy(rng.randint(-1, 24, size=(E, A, 89)).astype(np.float32)).to(DEV)
+        n = torch.from_numpy(rng.randint(-1, 24, size=(E, A, 89)).astype(np.float32)).to(DEV)
+        a = torch.from_numpy(rng.randint(0, 4, size=(E, A)).astype(np.int32)).to(DEV)
+        loc = rng.randint(0, 40, size=(E, A))
+        glob = rng.randint(0, 400, size=(E, 1))
+        r = 0.3 * (-1.0 * loc) + 0.7 * (-1.0 * glob)
+        agent.remember(s, a, torch.from_numpy(r).to(DEV), n, (t % 60) == 59)
+    agent.ring.check()
+
+
+def _host_batch(agent, ag, idx):
+    ring = agent.ring
+    slots = (ring.start + idx) % ring.cap
+    S = ring.s[ag].cpu().numpy()[slots, :89].astype(np.float32)
+    S2 = ring.n[ag].cpu().numpy()[slots, :89].astype(np.float32)
+    A = ring.a[ag].cpu().numpy()[slots].astype(np.int32)
+    r = ring.r[ag].cpu().numpy()[slots]
+    D = ring.d[ag].cpu().numpy()[slots].astype(np.float32)
+    return S, A, O.zscore(r), S2, D
+
+
+@pytest.mark.parametrize("hidden", [128, 64])
+def test_learn_fp32_matches_oracle(hidden):
+    E, A = 2, 5
+    cfg = AgentConfig(replay_buffer_size=300, nn_layers=[hidden, hidden], target_update_frequency=3,
+                      seed=3)
+    ag = BatchedDQN(E, A, cfg)
+    rng = np.random.RandomState(0)
+    _fill(ag, 330, rng)  # wraps the ring (start != 0)
+    assert ag.ring.start == 30
+    P = ag.P
+    p_h = ag.params.cpu().numpy().copy()
+    t_h = ag.target.cpu().numpy().copy()
+    m_h = np.zeros_like(p_h)
+    v_h = np.zeros_like(p_h)
+    for step in range(1, 5):
+        loss = ag.learn()
+        assert loss is not None
+        idx = ag.idx.cpu().numpy()
+        losses = []
+        for j in range(ag.NA):
+            S, Aa, Rn, S2, D = _host_batch(ag, j, idx[j])
+            losses.append(O.learn(p_h[j], t_h[j], m_h[j], v_h[j], S, Aa, Rn, S2, D, step,
+                                  H1=hidden, H2=hidden))
+        if step % 3 == 0:
+            t_h = p_h.copy()
+        p_g = ag.params.cpu().numpy()
+        np.testing.assert_allclose(loss.cpu().numpy(), np.array(losses), rtol=1e-5)
+        close = np.abs(p_g - p_h) <= 1e-6 + 1e-5 * np.abs(p_h)
+        assert close.mean() >= 0.9999, f"params step {step}: {close.size - close.sum()} off"
+        np.testing.assert_allclose(p_g, p_h, rtol=0, atol=1e-5, err_msg=f"params step {step}")
+        gs = np.sqrt(np.abs(v_h).max() / 1e-3)
+        np.testing.assert_allclose(ag.adam_m.cpu().numpy(), m_h, rtol=1e-4, atol=1e-6 * gs)
+        np.testing.assert_allclose(ag.adam_v.cpu().numpy(), v_h, rtol=1e-4, atol=1e-8 * gs * gs)
+        np.testing.assert_allclose(ag.target.cpu().numpy(), t_h, rtol=0, atol=1e-5)
+        # keep the oracle on the GPU trajectory so errors do not compound
+        p_h = p_g.copy()
+        m_h = ag.adam_m.cpu().numpy().copy()
+        v_h = ag.adam_v.cpu().numpy().copy()
+        t_h = ag.target.cpu().numpy().copy()
+
+
+def test_learn_gate_and_q_argmax():
+    ag = BatchedDQN(1, 3, AgentConfig(replay_buffer_size=500))
+    rng = np.random.RandomState(1)
+    _fill(ag, 127, rng)
+    assert ag.learn() is None  # dqn_agent.py:333-335
+    _fill(ag, 1, rng)
+    assert ag.learn() is not None
+    obs = torch.from_numpy(rng.randint(-1, 24, size=(1, 3, 89)).astype(np.float32)).to(DEV)
+    from dmdqn_amd._lib import call, ptr, stream_of
+    qd = torch.empty((3, 4), dtype=torch.float32, device=DEV)
+    call("dmdqn_q_argmax", ptr(ag.params), 3, ag.P, ag.H, ptr(obs), ptr(ag.greedy), ptr(qd),
+         stream_of())
+    q_ref = np.stack([O.qnet_forward(ag.params[j].cpu().numpy(), obs[0, j:j + 1].cpu().numpy())[0]
+                      for j in range(3)])
+    np.testing.assert_allclose(qd.cpu().numpy(), q_ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(ag.greedy.cpu().numpy().reshape(-1), q_ref.argmax(1))
