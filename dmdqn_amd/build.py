@@ -24,6 +24,7 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
           "-Wno-unused-result", "-munsafe-fp-atomics"]
 PER_FILE = {
     "learn.hip": ["-ffp-contract=fast"],
+    "learn_f16.hip": ["-ffp-contract=fast"],
 }
 DEFAULT_FP = ["-ffp-contract=off"]
 

@@ -101,3 +101,88 @@ def test_learn_gate_and_q_argmax():
                       for j in range(3)])
     np.testing.assert_allclose(qd.cpu().numpy(), q_ref, rtol=1e-5, atol=1e-5)
     np.testing.assert_array_equal(ag.greedy.cpu().numpy().reshape(-1), q_ref.argmax(1))
+
+
+# ---------------------------------------------------------------------------
+# fp16 (mixed_float16) path
+def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e-3):
+    """numpy restatement of the kernel's rounding points: f16 operands, f32
+    accumulation, f16 activations / Q / activation-gradients, f32 Adam."""
+    f16, f32 = np.float16, np.float32
+
+    def split(w):
+        sizes = [89 * H, H, H * H, H, H * 4, 4]
+        out, o = [], 0
+        for s in sizes:
+            out.append(w[o:o + s])
+            o += s
+        W1, b1, W2, b2, W3, b3 = out
+        return (W1.reshape(89, H).astype(f16).astype(f32), b1, W2.reshape(H, H).astype(f16).astype(f32),
+                b2, W3.reshape(H, 4).astype(f16).astype(f32), b3)
+
+    def fwd(ws, X):
+        W1, b1, W2, b2, W3, b3 = ws
+        h1 = np.maximum(X @ W1 + b1, 0).astype(f16).astype(f32)
+        h2 = np.maximum(h1 @ W2 + b2, 0).astype(f16).astype(f32)
+        q = (h2 @ W3 + b3).astype(f16).astype(f32)
+        return h1, h2, q
+
+    wo, wt = split(p), split(tgt)
+    _, _, q2 = fwd(wo, S2)
+    _, _, qt = fwd(wt, S2)
+    a_star = q2.argmax(1)
+    y = Rn + f32(gamma) * (1.0 - D) * qt[np.arange(128), a_star]
+    h1, h2, q = fwd(wo, S)
+    pred = q[np.arange(128), Aa]
+    dq = (2.0 * (pred - y) / 128).astype(f32)
+    loss = np.mean((y - pred) ** 2)
+    dq16 = dq.astype(f16).astype(f32)
+    DQ = np.zeros((128, 4), f32)
+    DQ[np.arange(128), Aa] = dq16
+    W1, b1, W2, b2, W3, b3 = wo
+    gW3 = h2.T @ DQ
+    gb3 = DQ.sum(0)
+    dz2 = np.where(h2 > 0, (dq16[:, None] * W3[:, Aa].T), 0).astype(f16).astype(f32)
+    gb2 = dz2.sum(0)
+    gW2 = h1.T @ dz2
+    dz1 = np.where(h1 > 0, dz2 @ W2.T, 0).astype(f16).astype(f32)
+    gb1 = dz1.sum(0)
+    gW1 = S.T @ dz1
+    g = np.concatenate([gW1.ravel(), gb1, gW2.ravel(), gb2, gW3.ravel(), gb3]).astype(f32)
+    alpha, c1, c2, eps = O.keras_adam_consts(t, lr)
+    m2 = m + (g - m) * c1
+    v2 = v + (g * g - v) * c2
+    p2 = p - (m2 * alpha) / (np.sqrt(v2) + eps)
+    return loss, g, p2, m2, v2
+
+
+def test_learn_fp16_matches_mixed_emulation_and_fp32_oracle():
+    E, A = 2, 4
+    cfg = AgentConfig(replay_buffer_size=300, target_update_frequency=2, seed=5, precision="fp16")
+    ag = BatchedDQN(E, A, cfg)
+    rng = np.random.RandomState(2)
+    _fill(ag, 200, rng)
+    p0 = ag.params.cpu().numpy().copy()
+    t0 = ag.target.cpu().numpy().copy()
+    loss = ag.learn().cpu().numpy()
+    idx = ag.idx.cpu().numpy()
+    m_g = ag.adam_m.cpu().numpy()
+    p_g = ag.params.cpu().numpy()
+    for j in range(ag.NA):
+        S, Aa, Rn, S2, D = _host_batch(ag, j, idx[j])
+        zero = np.zeros_like(p0[j])
+        l_e, g_e, p_e, m_e, v_e = _mixed_emulation(p0[j], t0[j], zero, zero.copy(), S, Aa, Rn, S2, D, 1)
+        # tight: same rounding points (f16 ulp flips from accumulation order only)
+        np.testing.assert_allclose(loss[j], l_e, rtol=2e-3)
+        gs = np.abs(g_e).max()
+        close = np.abs(m_g[j] / np.float32(0.1) - g_e) <= 2e-3 * gs + 1e-2 * np.abs(g_e)
+        assert close.mean() > 0.999, f"agent {j}: {np.sum(~close)} gradient entries off"
+        # stated tolerance vs the fp32 oracle (SURVEY 8c: rtol 2e-2 on the loss)
+        p1, m1, v1 = p0[j].copy(), zero.copy(), zero.copy()
+        l32 = O.learn(p1, t0[j], m1, v1, S, Aa, Rn, S2, D, 1)
+        np.testing.assert_allclose(loss[j], l32, rtol=2e-2)
+        dw_g, dw_o = p_g[j] - p0[j], p1 - p0[j]
+        assert np.corrcoef(dw_g, dw_o)[0, 1] > 0.97
+    # second learn triggers the target sync (frequency 2)
+    ag.learn()
+    np.testing.assert_array_equal(ag.target.cpu().numpy(), ag.params.cpu().numpy())
