@@ -186,7 +186,8 @@ def main():
 
     if rank == 0:
         value = args.steps * NA * world / el_max
-        P = tr.agent.P
+        from dmdqn_amd.agent import n_params_keras
+        P = n_params_keras(tr.agent.H)  # the reference's 28,548 parameters
         bpl = NA * learn_bytes_per_agent(P)
         avg_learn_s = float(np.mean(learn_ms)) / 1e3
         achieved = bpl / avg_learn_s / 1e9

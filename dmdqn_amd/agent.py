@@ -47,9 +47,57 @@ _lib.SIGNATURES.update({
 PRECISIONS = {"fp32": 0, "fp16": 1}
 
 
-def n_params(hidden, n_actions=N_ACTIONS):
+D_PAD = 96  # layer-1 fan-in padded for 32-byte MFMA fragments (qnet_layout.hpp)
+
+
+def n_params_keras(hidden, n_actions=N_ACTIONS):
+    """Parameters of the reference Keras model (dqn_agent.py:153-184)."""
     H = hidden
     return D_IN * H + H + H * H + H + H * n_actions + n_actions
+
+
+def n_params(hidden, n_actions=N_ACTIONS):
+    """Floats per agent in the device layout (qnet_layout.hpp):
+    W1T[H][96] | W2T[H][H] | W3T[4][H] | b1[H] | b2[H] | b3[4]."""
+    H = hidden
+    return H * D_PAD + H * H + n_actions * H + 2 * H + n_actions
+
+
+def keras_to_kernel(flat, hidden):
+    """[..., P_keras] Keras get_weights order -> [..., P_kernel] device layout."""
+    H = hidden
+    flat = np.asarray(flat, dtype=np.float32)
+    lead = flat.shape[:-1]
+    o = 0
+    W1 = flat[..., o:o + D_IN * H].reshape(lead + (D_IN, H)); o += D_IN * H
+    b1 = flat[..., o:o + H]; o += H
+    W2 = flat[..., o:o + H * H].reshape(lead + (H, H)); o += H * H
+    b2 = flat[..., o:o + H]; o += H
+    W3 = flat[..., o:o + H * N_ACTIONS].reshape(lead + (H, N_ACTIONS)); o += H * N_ACTIONS
+    b3 = flat[..., o:o + N_ACTIONS]
+    W1T = np.zeros(lead + (H, D_PAD), np.float32)
+    W1T[..., :D_IN] = np.swapaxes(W1, -1, -2)
+    parts = [W1T.reshape(lead + (-1,)), np.swapaxes(W2, -1, -2).reshape(lead + (-1,)),
+             np.swapaxes(W3, -1, -2).reshape(lead + (-1,)), b1, b2, b3]
+    return np.concatenate(parts, axis=-1)
+
+
+def kernel_to_keras(flat, hidden):
+    """Inverse of keras_to_kernel (drops the zero feature padding)."""
+    H = hidden
+    flat = np.asarray(flat, dtype=np.float32)
+    lead = flat.shape[:-1]
+    o = 0
+    W1T = flat[..., o:o + H * D_PAD].reshape(lead + (H, D_PAD)); o += H * D_PAD
+    W2T = flat[..., o:o + H * H].reshape(lead + (H, H)); o += H * H
+    W3T = flat[..., o:o + N_ACTIONS * H].reshape(lead + (N_ACTIONS, H)); o += N_ACTIONS * H
+    b1 = flat[..., o:o + H]; o += H
+    b2 = flat[..., o:o + H]; o += H
+    b3 = flat[..., o:o + N_ACTIONS]
+    parts = [np.swapaxes(W1T[..., :D_IN], -1, -2).reshape(lead + (-1,)), b1,
+             np.swapaxes(W2T, -1, -2).reshape(lead + (-1,)), b2,
+             np.swapaxes(W3T, -1, -2).reshape(lead + (-1,)), b3]
+    return np.concatenate(parts, axis=-1)
 
 
 def keras_adam_consts(t, lr, b1=0.9, b2=0.999, eps=1e-7):
@@ -126,7 +174,10 @@ class BatchedDQN:
         self.H, self.P = H, n_params(H)
         if init_weights is None:
             init_weights = keras_initial_weights(np.random.RandomState(cfg.seed), H, NA)
-        w = torch.as_tensor(np.asarray(init_weights, dtype=np.float32).reshape(NA, self.P))
+        init = np.asarray(init_weights, dtype=np.float32).reshape(NA, -1)
+        if init.shape[1] == n_params_keras(H):
+            init = keras_to_kernel(init, H)
+        w = torch.as_tensor(init.reshape(NA, self.P))
         self.params = w.to(dev).contiguous()
         self.target = self.params.clone()
         self.adam_m = torch.zeros_like(self.params)
@@ -213,9 +264,13 @@ class BatchedDQN:
         self.target.copy_(self.params)
 
     # -------------------------------------------------------------- weights
+    def keras_params(self, which="params"):
+        """[NA, P_keras] copy of params / target / adam_m / adam_v in Keras order."""
+        return kernel_to_keras(getattr(self, which).cpu().numpy(), self.H)
+
     def get_weights(self, agent):
         """Keras get_weights() order for one agent: [W1, b1, W2, b2, W3, b3]."""
-        p = self.params[agent].cpu().numpy()
+        p = kernel_to_keras(self.params[agent].cpu().numpy(), self.H)
         H = self.H
         shapes = [(D_IN, H), (H,), (H, H), (H,), (H, N_ACTIONS), (N_ACTIONS,)]
         out, o = [], 0
@@ -227,7 +282,7 @@ class BatchedDQN:
 
     def set_weights(self, agent, weights):
         flat = np.concatenate([np.asarray(w, np.float32).reshape(-1) for w in weights])
-        self.params[agent].copy_(torch.from_numpy(flat))
+        self.params[agent].copy_(torch.from_numpy(keras_to_kernel(flat, self.H)))
         self.target[agent].copy_(self.params[agent])
 
     def state_dict(self):

@@ -15,6 +15,7 @@
 #include <math.h>
 
 #include "common.hpp"
+#include "qnet_layout.hpp"
 
 namespace dmdqn {
 
@@ -30,10 +31,8 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 }
 
 template <int H>
-struct Lay {
-    static constexpr int P = D_ * H + H + H * H + H + H * NACT + NACT;
-    static constexpr int oW1 = 0, ob1 = D_ * H, oW2 = ob1 + H, ob2 = oW2 + H * H;
-    static constexpr int oW3 = ob2 + H, ob3 = oW3 + H * NACT;
+struct Lay : QL<H> {
+    using QL<H>::P;
     // LDS byte offsets
     static constexpr int X_OFF = 0;
     static constexpr int H1_OFF = B_ * DP * 2;
@@ -55,9 +54,9 @@ struct Scratch {
 };
 
 // Y[b][n] = act(X[b][:] . W[:][n] + bias[n]) for the wave's 16-column tile.
-// X rows come from LDS (f16 or f32), W from global memory (Keras [K][N]).
-template <int H, int K, typename TX, bool RELU, int NOUT>
-__device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *W, const float *bias,
+// X rows come from LDS (f16 or f32), W^T [N][KS] from global memory.
+template <int H, int K, typename TX, bool RELU, int KS>
+__device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *WT, const float *bias,
                                            float *Y, int ldy, int n0, int nvalid) {
     const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
     f32x4 acc[8];
@@ -66,7 +65,7 @@ __device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *W,
     const int n = n0 + lr;
     for (int k0 = 0; k0 < K; k0 += 4) {
         const int kk = k0 + lk;
-        const float bv = (kk < K && lr < nvalid) ? W[(size_t)kk * NOUT + n] : 0.0f;
+        const float bv = (kk < K && lr < nvalid) ? WT[(size_t)n * KS + kk] : 0.0f;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const float av = (float)X[(16 * t + lr) * ldx + kk];
@@ -93,19 +92,19 @@ __device__ void forward(const float *P, const _Float16 *X, float *H1, float *H2,
     const int w = threadIdx.x >> 6;
     constexpr int NT = H / 16;  // column tiles per layer
     for (int nt = w; nt < NT; nt += 8)
-        dense_tile<H, D_, _Float16, true, H>(X, DP, P + L::oW1, P + L::ob1, H1, H, 16 * nt, 16);
+        dense_tile<H, D_, _Float16, true, QN_DP>(X, DP, P + L::oW1T, P + L::ob1, H1, H, 16 * nt, 16);
     __syncthreads();
     for (int nt = w; nt < NT; nt += 8)
-        dense_tile<H, H, float, true, H>(H1, H, P + L::oW2, P + L::ob2, H2, H, 16 * nt, 16);
+        dense_tile<H, H, float, true, H>(H1, H, P + L::oW2T, P + L::ob2, H2, H, 16 * nt, 16);
     __syncthreads();
     // output layer: 4 columns; wave w computes batch tile w (K = H)
     {
         const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        const float *W3 = P + L::oW3;
+        const float *W3T = P + L::oW3T;
         for (int k0 = 0; k0 < H; k0 += 4) {
             const int kk = k0 + lk;
-            const float bv = lr < NACT ? W3[kk * NACT + lr] : 0.0f;
+            const float bv = lr < NACT ? W3T[lr * H + kk] : 0.0f;
             const float av = H2[(16 * w + lr) * H + kk];
             acc = mfma4(av, bv, acc);
         }
@@ -275,11 +274,11 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     __syncthreads();
     // dZ2 = dq * W3[:, a] masked by ReLU; overwrite H2 in place
     {
-        const float *W3 = Wp + L::oW3;
+        const float *W3T = Wp + L::oW3T;
         for (int e = tid; e < B_ * H; e += 512) {
             int b = e / H, k = e - b * H;
             float h = H2[e];
-            H2[e] = h > 0.0f ? S.dq[b] * W3[k * NACT + S.act[b]] : 0.0f;
+            H2[e] = h > 0.0f ? S.dq[b] * W3T[S.act[b] * H + k] : 0.0f;
         }
     }
     __syncthreads();
@@ -312,14 +311,14 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     f32x4 d1[NT];
     {
         const int lr = l & 15, lk = l >> 4;
-        const float *W2 = Wp + L::oW2;
+        const float *W2T = Wp + L::oW2T;
 #pragma unroll
         for (int t = 0; t < NT; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int k0 = 0; k0 < H; k0 += 4) {
             const int k = k0 + lk;
             const float av = H2[(16 * w + lr) * H + k];
 #pragma unroll
-            for (int t = 0; t < NT; t++) d1[t] = mfma4(av, W2[(size_t)(16 * t + lr) * H + k], d1[t]);
+            for (int t = 0; t < NT; t++) d1[t] = mfma4(av, W2T[(size_t)k * H + 16 * t + lr], d1[t]);
         }
     }
     __syncthreads();  // everyone done reading H1 (dW2) and old W2 (dH1)
@@ -342,7 +341,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
             for (int t = 0; t < NT; t++)
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    size_t i = L::oW2 + (size_t)(16 * jt + 4 * lk + j) * H + 16 * t + lr;
+                    size_t i = L::oW2T + (size_t)(16 * t + lr) * H + 16 * jt + 4 * lk + j;
                     adam_el(Wp, Mp, Vp, Tp, i, g2[q][t][j], AK, sync);
                 }
     }
@@ -373,7 +372,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     int i = 16 * t + 4 * lk + j;
-                    if (i < D_) adam_el(Wp, Mp, Vp, Tp, L::oW1 + (size_t)i * H + 16 * jt + lr,
+                    if (i < D_) adam_el(Wp, Mp, Vp, Tp, L::oW1T + (size_t)(16 * jt + lr) * QN_DP + i,
                                         g1[t][j], AK, sync);
                 }
         }
@@ -383,7 +382,8 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
         adam_el(Wp, Mp, Vp, Tp, L::ob1 + tid, gb1, AK, sync);
         adam_el(Wp, Mp, Vp, Tp, L::ob2 + tid, gb2, AK, sync);
     }
-    for (int e = tid; e < H * NACT; e += 512) adam_el(Wp, Mp, Vp, Tp, L::oW3 + e, g3, AK, sync);
+    for (int e = tid; e < H * NACT; e += 512)
+        adam_el(Wp, Mp, Vp, Tp, L::oW3T + (size_t)(e & 3) * H + (e >> 2), g3, AK, sync);
     if (tid < NACT) adam_el(Wp, Mp, Vp, Tp, L::ob3 + tid, gb3, AK, sync);
 }
 
@@ -399,21 +399,21 @@ __global__ void __launch_bounds__(256) k_q_argmax(const float *params, int P, co
     __syncthreads();
     for (int j = tid; j < H; j += blockDim.x) {
         float s = 0.0f;
-        for (int i = 0; i < D_; i++) s += x[i] * Wp[L::oW1 + i * H + j];
+        for (int i = 0; i < D_; i++) s += x[i] * Wp[L::oW1T + j * QN_DP + i];
         s += Wp[L::ob1 + j];
         h1[j] = s > 0.0f ? s : 0.0f;
     }
     __syncthreads();
     for (int k = tid; k < H; k += blockDim.x) {
         float s = 0.0f;
-        for (int j = 0; j < H; j++) s += h1[j] * Wp[L::oW2 + j * H + k];
+        for (int j = 0; j < H; j++) s += h1[j] * Wp[L::oW2T + k * H + j];
         s += Wp[L::ob2 + k];
         h2[k] = s > 0.0f ? s : 0.0f;
     }
     __syncthreads();
     if (tid < NACT) {
         float s = 0.0f;
-        for (int k = 0; k < H; k++) s += h2[k] * Wp[L::oW3 + k * NACT + tid];
+        for (int k = 0; k < H; k++) s += h2[k] * Wp[L::oW3T + tid * H + k];
         q[tid] = s + Wp[L::ob3 + tid];
     }
     __syncthreads();

@@ -1,26 +1,33 @@
 // learn_f16.hip -- fused Double-DQN learn step, mixed precision (the reference's
 // tf.keras mixed_float16 policy, train.py:61): f16 operands on the MFMA
 // (v_mfma_f32_16x16x32_f16, f32 accumulate), f32 master weights + Adam slots.
-// One workgroup (8 waves) per agent, everything between the replay gather and
-// the Adam update stays in LDS.
+//
+// One workgroup (8 waves) per agent, TWO workgroups per CU: 74 KB of LDS and
+// <= 128 VGPRs, so one agent's HBM phases (weight fragments, replay gather,
+// Adam read-modify-write) overlap the other agent's MFMA phases.
+//
+// Weights never pass through LDS: each wave owns 16 output neurons and reads
+// their fan-in rows (transposed layout, qnet_layout.hpp) straight from HBM
+// into MFMA A-fragments (32 contiguous bytes per lane, converted f32 -> f16).
+// LDS holds only activations:   R1 = H1 / dZ1 (f16 [128][128])
+//                               R2 = X / H2 / dZ2 (f16 [128][128])
+//                               DQ (f16 [128][16]) + per-row scratch
 //
 // GEMM orientation (C[M][N] = sum_k A[M][k] B[k][N], 16x16x32 fragments):
-//   forward  Z^T[n][b] = W^T[n][k] . X[b][k]   A: W^T image rows, B: X rows
-//            -> each lane holds 4 consecutive neurons of one batch row, stored
-//               as one 8-byte write into the [b][n] activation image
-//   dW3      C[k][a] = H2^T . DQ               (batch reduction: transposed reads)
-//   dW2      C[j][k] = H1^T . dZ2              (transposed reads)
-//   dH1^T    C[j][b] = W2 . dZ2^T              A: transposed read of W2^T image
-//   dW1      C[i][j] = X^T . dZ1               (transposed reads)
-// Gradient tiles come out in Keras [in][out] order: Adam runs straight from
-// the accumulators with 64-byte contiguous row segments per 16 lanes.
-//
-// LDS (bytes): X f16[128][96] | W1T f16[128][96] | W2T f16[128][128] |
-//   W3T f16[16][128] | H1 f16[128][128] | H2 f16[128][128] | biases f32 |
-//   DQ f16[128][16] | scratch        = 162,976 B (1 workgroup / CU)
+//   forward  Z^T[n][b] = W^T[n][k] . X[b][k]   -> lane holds 4 consecutive
+//            neurons of one batch row: one 8-byte store into the [b][n] image
+//   dW3      C[k][a] = H2^T . DQ       (batch reductions use ds_read_b64_tr_b16)
+//   dW2      C[j][k] = H1^T . dZ2
+//   dH1^T    C[j][b] = W2[j][k] . dZ2^T
+//   dW1      C[i][j] = X^T . dZ1
+//   bias grads: the same MFMAs with an all-ones operand (column sums).
+// Gradient tiles C[in][out] hold 4 consecutive fan-in values per lane, which
+// is 16 contiguous bytes of the transposed parameter layout: Adam is one
+// float4 read-modify-write of w, m, v per lane straight from the accumulators.
 #include <math.h>
 
 #include "common.hpp"
+#include "qnet_layout.hpp"
 
 namespace dmdqn {
 namespace f16k {
@@ -31,23 +38,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short v4s __attribute__((vector_size(8)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
-constexpr int B_ = 128, D_ = 89, DP = 96, H = 128, NACT = 4;
-constexpr int P = D_ * H + H + H * H + H + H * NACT + NACT;
-constexpr int oW1 = 0, ob1 = D_ * H, oW2 = ob1 + H, ob2 = oW2 + H * H, oW3 = ob2 + H,
-              ob3 = oW3 + H * NACT;
+constexpr int B_ = 128, D_ = QN_D, DP = QN_DP, H = 128, NACT = QN_NA;
+using L = QL<H>;
 
 // LDS byte offsets
-constexpr int X_OFF = 0;
-constexpr int W1T_OFF = X_OFF + B_ * DP * 2;
-constexpr int W2T_OFF = W1T_OFF + H * DP * 2;
-constexpr int W3T_OFF = W2T_OFF + H * H * 2;
-constexpr int H1_OFF = W3T_OFF + 16 * H * 2;
-constexpr int H2_OFF = H1_OFF + B_ * H * 2;
-constexpr int BIAS_OFF = H2_OFF + B_ * H * 2;       // b1[128] b2[128] b3[8] f32
-constexpr int DQ_OFF = BIAS_OFF + (2 * H + 8) * 4;  // f16 [128][16]
+constexpr int R1_OFF = 0;
+constexpr int R2_OFF = R1_OFF + B_ * H * 2;
+constexpr int DQ_OFF = R2_OFF + B_ * H * 2;
 constexpr int SC_OFF = DQ_OFF + B_ * 16 * 2;
 constexpr int LDS_BYTES = SC_OFF + 6272;
-static_assert(LDS_BYTES <= 163840, "LDS budget");
+static_assert(LDS_BYTES <= 81920, "two workgroups per CU");
 
 __device__ __forceinline__ f32x4 mfma(half8 a, half8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -76,143 +76,166 @@ __device__ __forceinline__ half8 frag_tr(const _Float16 *img, int ld, int r0, in
     return r;
 }
 
+// A-fragment of a transposed f32 weight matrix WT[N][ld] straight from HBM:
+// WT[n0 + (l&15)][k0 + 8(l>>4) + e] -> f16.  nvalid masks padded rows.
+__device__ __forceinline__ half8 wfrag(const float *WT, int ld, int n0, int k0, int nvalid = 16) {
+    const int l = threadIdx.x & 63, lr = l & 15;
+    half8 r;
+    if (lr < nvalid) {
+        const float4 *p = reinterpret_cast<const float4 *>(WT + (size_t)(n0 + lr) * ld + k0 + 8 * (l >> 4));
+        float4 x = p[0], y = p[1];
+        r[0] = (_Float16)x.x; r[1] = (_Float16)x.y; r[2] = (_Float16)x.z; r[3] = (_Float16)x.w;
+        r[4] = (_Float16)y.x; r[5] = (_Float16)y.y; r[6] = (_Float16)y.z; r[7] = (_Float16)y.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; e++) r[e] = (_Float16)0.0f;
+    }
+    return r;
+}
+
+__device__ __forceinline__ half8 ones8() {
+    half8 r;
+#pragma unroll
+    for (int e = 0; e < 8; e++) r[e] = (_Float16)1.0f;
+    return r;
+}
+
 struct Scratch {
-    float *z3;    // [128][4]
+    float *z3;  // [128][4]
     float *rn, *y, *dq, *dn;
     int *act, *slot;
     double *r64, *red;
 };
 
-// Forward of one 128-row batch: H1/H2 f16 images (post-ReLU), Q -> z3 (f32).
-__device__ void forward(const _Float16 *X, const _Float16 *W1T, const _Float16 *W2T,
-                        const _Float16 *W3T, const float *bias, _Float16 *H1, _Float16 *H2,
-                        float *z3) {
+// Forward of one 128-row batch X (in R2).  Leaves H1 in R1 and H2 in R2 (X is
+// overwritten by H2), Q in qout[128][4] (f32 of the f16 output, as Keras'
+// mixed policy emits f16 from the last Dense).
+__device__ void forward(const float *Wg, _Float16 *R1, _Float16 *R2, float *qout) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
-    const int n0 = 16 * w;  // this wave's 16 neurons
-    // layer 1: K = 96 (3 k-steps)
+    const int n0 = 16 * w;
+    const int n = n0 + 4 * lg;
+    // layer 1: K = 96 (3 k-steps); A from HBM, B = X rows
     {
+        half8 a0 = wfrag(Wg + L::oW1T, DP, n0, 0);
+        half8 a1 = wfrag(Wg + L::oW1T, DP, n0, 32);
+        half8 a2 = wfrag(Wg + L::oW1T, DP, n0, 64);
+        const float4 bb = *reinterpret_cast<const float4 *>(Wg + L::ob1 + n);
         f32x4 acc[8];
 #pragma unroll
-        for (int t = 0; t < 8; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k0 = 0; k0 < DP; k0 += 32) {
-            half8 a = frag_row(W1T, DP, n0, k0);
-#pragma unroll
-            for (int t = 0; t < 8; t++) acc[t] = mfma(a, frag_row(X, DP, 16 * t, k0), acc[t]);
+        for (int t = 0; t < 8; t++) {
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+            c = mfma(a0, frag_row(R2, DP, 16 * t, 0), c);
+            c = mfma(a1, frag_row(R2, DP, 16 * t, 32), c);
+            acc[t] = mfma(a2, frag_row(R2, DP, 16 * t, 64), c);
         }
-        const int n = n0 + 4 * lg;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             half4v hv;
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                float z = acc[t][e] + bias[n + e];
-                hv[e] = (_Float16)(z > 0.0f ? z : 0.0f);
-            }
-            *reinterpret_cast<half4v *>(H1 + (16 * t + lr) * H + n) = hv;
+            hv[0] = (_Float16)fmaxf(acc[t][0] + bb.x, 0.0f);
+            hv[1] = (_Float16)fmaxf(acc[t][1] + bb.y, 0.0f);
+            hv[2] = (_Float16)fmaxf(acc[t][2] + bb.z, 0.0f);
+            hv[3] = (_Float16)fmaxf(acc[t][3] + bb.w, 0.0f);
+            *reinterpret_cast<half4v *>(R1 + (16 * t + lr) * H + n) = hv;
         }
     }
     __syncthreads();
-    // layer 2: K = 128 (4 k-steps)
+    // layer 2: K = 128; B = H1 rows (R1) ; output H2 -> R2 (X is dead)
     {
+        const float *W2T = Wg + L::oW2T;
+        half8 a[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) a[s] = wfrag(W2T, H, n0, 32 * s);
+        const float4 bb = *reinterpret_cast<const float4 *>(Wg + L::ob2 + n);
         f32x4 acc[8];
 #pragma unroll
-        for (int t = 0; t < 8; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < 8; t++) {
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k0 = 0; k0 < H; k0 += 32) {
-            half8 a = frag_row(W2T, H, n0, k0);
-#pragma unroll
-            for (int t = 0; t < 8; t++) acc[t] = mfma(a, frag_row(H1, H, 16 * t, k0), acc[t]);
+            for (int s = 0; s < 4; s++) c = mfma(a[s], frag_row(R1, H, 16 * t, 32 * s), c);
+            acc[t] = c;
         }
-        const int n = n0 + 4 * lg;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             half4v hv;
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                float z = acc[t][e] + bias[H + n + e];
-                hv[e] = (_Float16)(z > 0.0f ? z : 0.0f);
-            }
-            *reinterpret_cast<half4v *>(H2 + (16 * t + lr) * H + n) = hv;
+            hv[0] = (_Float16)fmaxf(acc[t][0] + bb.x, 0.0f);
+            hv[1] = (_Float16)fmaxf(acc[t][1] + bb.y, 0.0f);
+            hv[2] = (_Float16)fmaxf(acc[t][2] + bb.z, 0.0f);
+            hv[3] = (_Float16)fmaxf(acc[t][3] + bb.w, 0.0f);
+            *reinterpret_cast<half4v *>(R2 + (16 * t + lr) * H + n) = hv;
         }
     }
     __syncthreads();
-    // layer 3: Q^T[a][b], wave w -> batch tile w
+    // layer 3: Q^T[a][b] = W3T[a][k] . H2[b][k]; wave w -> batch tile w
     {
+        const float *W3T = Wg + L::oW3T;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k0 = 0; k0 < H; k0 += 32) acc = mfma(frag_row(W3T, H, 0, k0), frag_row(H2, H, 16 * w, k0), acc);
+        for (int s = 0; s < 4; s++)
+            acc = mfma(wfrag(W3T, H, 0, 32 * s, NACT), frag_row(R2, H, 16 * w, 32 * s), acc);
         if (lg == 0) {
-            // (keras mixed_float16: the last Dense also outputs f16)
-#pragma unroll
-            for (int e = 0; e < 4; e++)
-                z3[(16 * w + lr) * NACT + e] = (float)(_Float16)(acc[e] + bias[2 * H + e]);
+            const float4 bb = *reinterpret_cast<const float4 *>(Wg + L::ob3);
+            float4 q;
+            q.x = (float)(_Float16)(acc[0] + bb.x);
+            q.y = (float)(_Float16)(acc[1] + bb.y);
+            q.z = (float)(_Float16)(acc[2] + bb.z);
+            q.w = (float)(_Float16)(acc[3] + bb.w);
+            *reinterpret_cast<float4 *>(qout + (16 * w + lr) * NACT) = q;
         }
     }
     __syncthreads();
 }
 
-// Stage one network (fp32, Keras layout in global memory) into the f16 LDS
-// images W1T[n][k], W2T[n][j], W3T[a][k] and the f32 biases.
-__device__ void stage(const float *Wg, _Float16 *W1T, _Float16 *W2T, _Float16 *W3T, float *bias) {
-    const int tid = threadIdx.x;
-    // lanes of a wave: 16 consecutive k-quads x 4 neurons -> 8-byte LDS writes
-    for (int t = tid; t < H * (DP / 4); t += 512) {   // W1T: 128 n x 24 k-quads
-        int n = t / (DP / 4), kq = t - n * (DP / 4);
-        half4v hv;
+struct AdamC {
+    float alpha, c1, c2, eps;
+    bool sync;
+};
+
+// Keras-3 Adam on 4 consecutive parameters (one 16-byte lane access each).
+__device__ __forceinline__ void adam4(float *W, float *M, float *V, float *T, size_t i, f32x4 g,
+                                      const AdamC &k) {
+    float4 w = *reinterpret_cast<float4 *>(W + i);
+    float4 m = *reinterpret_cast<float4 *>(M + i);
+    float4 v = *reinterpret_cast<float4 *>(V + i);
+    float *pw = &w.x, *pm = &m.x, *pv = &v.x;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            int k = 4 * kq + c;
-            hv[c] = k < D_ ? (_Float16)Wg[oW1 + k * H + n] : (_Float16)0.0f;
-        }
-        *reinterpret_cast<half4v *>(W1T + n * DP + 4 * kq) = hv;
+    for (int e = 0; e < 4; e++) {
+        float ge = g[e];
+        pm[e] = pm[e] + (ge - pm[e]) * k.c1;
+        pv[e] = pv[e] + (ge * ge - pv[e]) * k.c2;
+        pw[e] = pw[e] - (pm[e] * k.alpha) / (sqrtf(pv[e]) + k.eps);
     }
-    for (int t = tid; t < H * (H / 4); t += 512) {    // W2T: 128 n x 32 j-quads
-        int n = t / (H / 4), jq = t - n * (H / 4);
-        half4v hv;
-#pragma unroll
-        for (int c = 0; c < 4; c++) hv[c] = (_Float16)Wg[oW2 + (4 * jq + c) * H + n];
-        *reinterpret_cast<half4v *>(W2T + n * H + 4 * jq) = hv;
-    }
-    for (int t = tid; t < 16 * H; t += 512) {         // W3T: 16 a (4 used) x 128 k
-        int a = t / H, k = t - a * H;
-        W3T[t] = a < NACT ? (_Float16)Wg[oW3 + k * NACT + a] : (_Float16)0.0f;
-    }
-    for (int t = tid; t < 2 * H + 8; t += 512)
-        bias[t] = t < H ? Wg[ob1 + t] : t < 2 * H ? Wg[ob2 + t - H] : (t < 2 * H + NACT ? Wg[ob3 + t - 2 * H] : 0.0f);
-    __syncthreads();
+    *reinterpret_cast<float4 *>(W + i) = w;
+    *reinterpret_cast<float4 *>(M + i) = m;
+    *reinterpret_cast<float4 *>(V + i) = v;
+    if (k.sync) *reinterpret_cast<float4 *>(T + i) = w;
 }
 
-__device__ __forceinline__ void adam_el(float *w, float *m, float *v, float *tgt, size_t i, float g,
-                                        float alpha, float c1, float c2, float eps, bool sync) {
-    float mi = m[i], vi = v[i], wi = w[i];
-    mi = mi + (g - mi) * c1;
-    vi = vi + (g * g - vi) * c2;
-    wi = wi - (mi * alpha) / (sqrtf(vi) + eps);
-    m[i] = mi;
-    v[i] = vi;
-    w[i] = wi;
-    if (sync) tgt[i] = wi;
+__device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, size_t i, float g,
+                                      const AdamC &k) {
+    float m = M[i], v = V[i], w = W[i];
+    m = m + (g - m) * k.c1;
+    v = v + (g * g - v) * k.c2;
+    w = w - (m * k.alpha) / (sqrtf(v) + k.eps);
+    M[i] = m;
+    V[i] = v;
+    W[i] = w;
+    if (k.sync) T[i] = w;
 }
 
-__global__ void __launch_bounds__(512) k_learn_f16(dmdqn_learn_args a) {
+__global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    _Float16 *X = (_Float16 *)(smem + X_OFF), *W1T = (_Float16 *)(smem + W1T_OFF);
-    _Float16 *W2T = (_Float16 *)(smem + W2T_OFF), *W3T = (_Float16 *)(smem + W3T_OFF);
-    _Float16 *H1 = (_Float16 *)(smem + H1_OFF), *H2 = (_Float16 *)(smem + H2_OFF);
-    float *bias = (float *)(smem + BIAS_OFF);
+    _Float16 *R1 = (_Float16 *)(smem + R1_OFF), *R2 = (_Float16 *)(smem + R2_OFF);
     _Float16 *DQ = (_Float16 *)(smem + DQ_OFF);
     char *sc = smem + SC_OFF;
-    Scratch S{(float *)sc,         (float *)(sc + 2048), (float *)(sc + 2560),
+    Scratch S{(float *)sc,          (float *)(sc + 2048), (float *)(sc + 2560),
               (float *)(sc + 3072), (float *)(sc + 3584), (int *)(sc + 4096),
               (int *)(sc + 4608),   (double *)(sc + 5120), (double *)(sc + 6144)};
     const int agent = blockIdx.x;
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
-    const size_t Pz = (size_t)P;
+    const size_t Pz = (size_t)L::P;
     float *Wp = a.params + agent * Pz, *Mp = a.adam_m + agent * Pz, *Vp = a.adam_v + agent * Pz;
     float *Tp = a.target + agent * Pz;
-    const bool sync = a.sync_target != 0;
-    const float alpha = a.alpha, c1 = a.c1, c2 = a.c2, eps = a.eps;
+    const AdamC AK{a.alpha, a.c1, a.c2, a.eps, a.sync_target != 0};
 
     // ---- batch metadata + reward z-score (numpy pairwise order, f64)
     if (tid < B_) {
@@ -259,6 +282,7 @@ __global__ void __launch_bounds__(512) k_learn_f16(dmdqn_learn_args a) {
     __syncthreads();
     if (tid < B_) S.rn[tid] = (float)__ddiv_rn(__dsub_rn(S.r64[tid], S.red[8]), S.red[9]);
 
+    // replay rows (int8) -> X f16 [128][96] in R2
     auto gather = [&](const int8_t *ring) {
         for (int t = tid; t < B_ * (DP / 4); t += 512) {
             int b = t / (DP / 4), q = t - b * (DP / 4);
@@ -269,41 +293,45 @@ __global__ void __launch_bounds__(512) k_learn_f16(dmdqn_learn_args a) {
             hv[1] = (_Float16)(float)c.y;
             hv[2] = (_Float16)(float)c.z;
             hv[3] = (_Float16)(float)c.w;
-            *reinterpret_cast<half4v *>(X + b * DP + 4 * q) = hv;
+            *reinterpret_cast<half4v *>(R2 + b * DP + 4 * q) = hv;
         }
+        __syncthreads();
     };
 
-    // ---- target(S') then online(S') -> a*, y
+    // ---- target(S') -> z3 ; online(S') -> Q in R1 (free during layer 3) ; y
     gather(a.ring_n);
-    stage(a.target + agent * Pz, W1T, W2T, W3T, bias);
-    forward(X, W1T, W2T, W3T, bias, H1, H2, S.z3);
-    stage(Wp, W1T, W2T, W3T, bias);
-    float *qo = (float *)H1;  // H1 is free while layer 3 runs
-    forward(X, W1T, W2T, W3T, bias, H1, H2, qo);
+    forward(a.target + agent * Pz, R1, R2, S.z3);
+    gather(a.ring_n);
+    float *qo = (float *)R1;
+    forward(Wp, R1, R2, qo);
     if (tid < B_) {
+        const float4 q = *reinterpret_cast<const float4 *>(qo + tid * NACT);
         int best = 0;
-        for (int k = 1; k < NACT; k++)
-            if (qo[tid * NACT + k] > qo[tid * NACT + best]) best = k;
+        float bq = q.x;
+        if (q.y > bq) { best = 1; bq = q.y; }
+        if (q.z > bq) { best = 2; bq = q.z; }
+        if (q.w > bq) { best = 3; }
         float tq = S.z3[tid * NACT + best];
         float gd = a.gamma * (1.0f - S.dn[tid]);
         S.y[tid] = S.rn[tid] + gd * tq;
     }
     __syncthreads();
-    // ---- online(S) with activations kept; q, loss, dq
+    // ---- online(S), activations kept: H1 in R1, H2 in R2 ; q, loss, DQ
     gather(a.ring_s);
-    __syncthreads();
-    forward(X, W1T, W2T, W3T, bias, H1, H2, S.z3);
+    forward(Wp, R1, R2, S.z3);
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];
         float diff = q - S.y[tid];
         float dq = 2.0f * diff / (float)B_;
-        S.dq[tid] = dq;
         lsum = diff * diff;
-        half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        half8 z;
+#pragma unroll
+        for (int e = 0; e < 8; e++) z[e] = (_Float16)0.0f;
         *reinterpret_cast<half8 *>(DQ + tid * 16) = z;
         *reinterpret_cast<half8 *>(DQ + tid * 16 + 8) = z;
         DQ[tid * 16 + S.act[tid]] = (_Float16)dq;
+        S.dq[tid] = (float)(_Float16)dq;
     }
     if (w < 2) {
         for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
@@ -312,112 +340,116 @@ __global__ void __launch_bounds__(512) k_learn_f16(dmdqn_learn_args a) {
     __syncthreads();
     if (tid == 0 && a.loss) a.loss[agent] = (float)(S.red[10] + S.red[11]) / (float)B_;
 
-    // ---- dW3[k][a] = H2^T . DQ  (wave w: k-tile w) ; db3
+    const half8 ones = ones8();
+    // ---- dW3[k][a] = H2^T . DQ (wave w: k-tile w) ; db3 (wave 0)
     {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f}, gb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int b0 = 0; b0 < B_; b0 += 32)
-            acc = mfma(frag_tr(H2, H, b0, 16 * w), frag_tr(DQ, 16, b0, 0), acc);
+        for (int b0 = 0; b0 < B_; b0 += 32) {
+            half8 dqf = frag_tr(DQ, 16, b0, 0);
+            acc = mfma(frag_tr(R2, H, b0, 16 * w), dqf, acc);
+            gb = mfma(ones, dqf, gb);  // every wave (no MFMA under divergent control)
+        }
         if (lr < NACT) {
-#pragma unroll
-            for (int e = 0; e < 4; e++)
-                adam_el(Wp, Mp, Vp, Tp, oW3 + (size_t)(16 * w + 4 * lg + e) * NACT + lr, acc[e],
-                        alpha, c1, c2, eps, sync);
+            // rows k = 16w + 4lg + e (consecutive), column a: W3T[a][k..k+3]
+            adam4(Wp, Mp, Vp, Tp, L::oW3T + (size_t)lr * H + 16 * w + 4 * lg, acc, AK);
+            if (w == 0 && lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob3 + lr, gb[0], AK);
         }
     }
-    if (tid < NACT) {
-        float s = 0.0f;
-        for (int b = 0; b < B_; b++) s += (float)DQ[b * 16 + tid];
-        adam_el(Wp, Mp, Vp, Tp, ob3 + tid, s, alpha, c1, c2, eps, sync);
+    __syncthreads();  // dW3 read H2; dZ2 overwrites it
+    // ---- dZ2 = dq * W3[:, a] (ReLU mask), in place over H2 (8 columns per task)
+    for (int t = tid; t < B_ * (H / 8); t += 512) {
+        const int b = t >> 4, k8 = (t & 15) * 8, ac = S.act[b];
+        half8 *p = reinterpret_cast<half8 *>(R2 + b * H + k8);
+        half8 h = *p, o;
+        const float4 *w3 = reinterpret_cast<const float4 *>(Wp + L::oW3T + (size_t)ac * H + k8);
+        const float4 u = w3[0], v = w3[1];
+        const float wv[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        const float dq = S.dq[b];
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+            o[e] = (float)h[e] > 0.0f ? (_Float16)(dq * (float)(_Float16)wv[e]) : (_Float16)0.0f;
+        *p = o;
     }
     __syncthreads();
-    // ---- dZ2 = dq * W3[:, a] (ReLU mask), in place over H2
-    for (int e = tid; e < B_ * H; e += 512) {
-        int b = e >> 7, k = e & (H - 1);
-        float h = (float)H2[e];
-        float g = (float)DQ[b * 16 + S.act[b]] * (float)W3T[S.act[b] * H + k];
-        H2[e] = (_Float16)(h > 0.0f ? g : 0.0f);
-    }
-    __syncthreads();
-    float gb2 = 0.0f;
-    if (tid < H) {
-        for (int b = 0; b < B_; b++) gb2 += (float)H2[b * H + tid];
-    }
-    // ---- dW2[j][k] = H1^T . dZ2   (wave w: j-tile w, 8 k-tiles)
-    f32x4 g2[8];
+    // ---- dH1 A-fragments (OLD W2: W2[j][k] = W2T[k][j]) before Adam touches W2.
+    // Wave w reads and later updates exactly the columns j of its own tile.
+    half8 aw2[4];
+    {
+        const float *W2T = Wp + L::oW2T;
 #pragma unroll
-    for (int t = 0; t < 8; t++) g2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < 4; s++)
 #pragma unroll
-    for (int b0 = 0; b0 < B_; b0 += 32) {
-        half8 av = frag_tr(H1, H, b0, 16 * w);
-#pragma unroll
-        for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr(H2, H, b0, 16 * t), g2[t]);
+            for (int e = 0; e < 8; e++)
+                aw2[s][e] = (_Float16)W2T[(size_t)(32 * s + 8 * lg + e) * H + 16 * w + lr];
     }
-    // ---- dH1^T[j][b] = W2[j][k] . dZ2^T  (A: transposed read of the W2T image)
+    // ---- dW2[j][k] = H1^T . dZ2 (wave w: j-tile w, 8 k-tiles) ; db2 (k-tile w)
+    {
+        f32x4 g2[8], gb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 8; t++) g2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b0 = 0; b0 < B_; b0 += 32) {
+            const half8 av = frag_tr(R1, H, b0, 16 * w);
+            gb = mfma(ones, frag_tr(R2, H, b0, 16 * w), gb);
+#pragma unroll
+            for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr(R2, H, b0, 16 * t), g2[t]);
+        }
+        // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3]
+#pragma unroll
+        for (int t = 0; t < 8; t++)
+            adam4(Wp, Mp, Vp, Tp, L::oW2T + (size_t)(16 * t + lr) * H + 16 * w + 4 * lg, g2[t], AK);
+        if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob2 + 16 * w + lr, gb[0], AK);
+    }
+    // ---- dH1^T[j][b] = W2[j][k] . dZ2^T  (wave w: j-tile w, 8 b-tiles)
     f32x4 d1[8];
 #pragma unroll
-    for (int t = 0; t < 8; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 8; t++) {
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k0 = 0; k0 < H; k0 += 32) {
-        half8 av = frag_tr(W2T, H, k0, 16 * w);
-#pragma unroll
-        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(H2, H, 16 * t, k0), d1[t]);
+        for (int s = 0; s < 4; s++) c = mfma(aw2[s], frag_row(R2, H, 16 * t, 32 * s), c);
+        d1[t] = c;
     }
-    __syncthreads();  // all reads of H1 (dW2) done
-    // dZ1 = dH1 masked by ReLU(H1): lane holds neurons j..j+3 of batch row b
+    __syncthreads();  // all reads of H1 (dW2) and dZ2 (dW2, dH1) done
+    // dZ1 = dH1 masked by ReLU(H1) -> R1 in place (lane: neurons j..j+3 of row b)
     {
         const int j = 16 * w + 4 * lg;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
-            half4v *p = reinterpret_cast<half4v *>(H1 + (16 * t + lr) * H + j);
+            half4v *p = reinterpret_cast<half4v *>(R1 + (16 * t + lr) * H + j);
             half4v h = *p, o;
 #pragma unroll
             for (int e = 0; e < 4; e++) o[e] = (float)h[e] > 0.0f ? (_Float16)d1[t][e] : (_Float16)0.0f;
             *p = o;
         }
     }
-    // Adam on W2 (rows j = 16w + 4lg + e, cols k = 16t + lr) and b2
-#pragma unroll
-    for (int t = 0; t < 8; t++)
-#pragma unroll
-        for (int e = 0; e < 4; e++)
-            adam_el(Wp, Mp, Vp, Tp, oW2 + (size_t)(16 * w + 4 * lg + e) * H + 16 * t + lr, g2[t][e],
-                    alpha, c1, c2, eps, sync);
-    if (tid < H) adam_el(Wp, Mp, Vp, Tp, ob2 + tid, gb2, alpha, c1, c2, eps, sync);
-    __syncthreads();
-    // ---- db1 ; dW1[i][j] = X^T . dZ1  (wave w: j-tile w, 6 i-tiles)
-    if (tid < H) {
-        float s = 0.0f;
-        for (int b = 0; b < B_; b++) s += (float)H1[b * H + tid];
-        adam_el(Wp, Mp, Vp, Tp, ob1 + tid, s, alpha, c1, c2, eps, sync);
-    }
+    gather(a.ring_s);  // X again (R2 is free), ends with a barrier
+    // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
     {
-        f32x4 g1[6];
+        f32x4 g1[6], gb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < 6; t++) g1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
-            half8 bv = frag_tr(H1, H, b0, 16 * w);
+            const half8 bv = frag_tr(R1, H, b0, 16 * w);
+            gb = mfma(ones, bv, gb);
 #pragma unroll
-            for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr(X, DP, b0, 16 * t), bv, g1[t]);
+            for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr(R2, DP, b0, 16 * t), bv, g1[t]);
         }
+        // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; padded
+        // features 89..95 have zero weight and zero gradient and stay zero
 #pragma unroll
         for (int t = 0; t < 6; t++)
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                int i = 16 * t + 4 * lg + e;
-                if (i < D_)
-                    adam_el(Wp, Mp, Vp, Tp, oW1 + (size_t)i * H + 16 * w + lr, g1[t][e], alpha, c1,
-                            c2, eps, sync);
-            }
+            adam4(Wp, Mp, Vp, Tp, L::oW1T + (size_t)(16 * w + lr) * DP + 16 * t + 4 * lg, g1[t], AK);
+        if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob1 + 16 * w + lr, gb[0], AK);
     }
 }
 
 }  // namespace f16k
 
 int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s) {
-    DMDQN_REQUIRE(a->hidden == 128 && a->P == f16k::P,
-                  "dmdqn_learn: precision 1 (fp16) needs hidden=128 (P=%d)", f16k::P);
+    DMDQN_REQUIRE(a->hidden == 128 && a->P == f16k::L::P,
+                  "dmdqn_learn: precision 1 (fp16) needs hidden=128 (P=%d)", f16k::L::P);
     hipLaunchKernelGGL(f16k::k_learn_f16, dim3(a->NA), dim3(512), 0, s, *a);
     DMDQN_LAUNCH_CHECK("k_learn_f16");
     return DMDQN_OK;

@@ -1,0 +1,45 @@
+"""Host-side agent logic (no GPU): parameter layout conversion, Keras Adam
+constants, epsilon schedule, config keys."""
+import numpy as np
+import yaml
+
+from conftest import ROOT
+from dmdqn_amd.agent import (AgentConfig, keras_adam_consts, keras_to_kernel, kernel_to_keras,
+                             n_params, n_params_keras)
+
+
+def test_param_counts():
+    assert n_params_keras(128) == 28548  # P = 28,548 for [128,128]
+    assert n_params_keras(256) == 89860
+    assert n_params(128) == 29444 and n_params(128) % 4 == 0
+
+
+def test_layout_roundtrip():
+    rng = np.random.RandomState(0)
+    for H in (64, 128):
+        k = rng.normal(size=(3, n_params_keras(H))).astype(np.float32)
+        kk = keras_to_kernel(k, H)
+        assert kk.shape == (3, n_params(H))
+        np.testing.assert_array_equal(kernel_to_keras(kk, H), k)
+        # feature padding of W1T is zero
+        W1T = kk[:, :H * 96].reshape(3, H, 96)
+        assert (W1T[:, :, 89:] == 0).all()
+        np.testing.assert_array_equal(W1T[:, :, :89], np.swapaxes(k[:, :89 * H].reshape(3, 89, H), 1, 2))
+
+
+def test_keras_adam_constants():
+    a, c1, c2, eps = keras_adam_consts(1, 1e-3)
+    np.testing.assert_allclose(a, 1e-3 * np.sqrt(1 - 0.999) / (1 - 0.9), rtol=1e-4)
+    assert np.float32(c1) == np.float32(0.1) and np.float32(eps) == np.float32(1e-7)
+
+
+def test_config_keys_match_reference_yaml():
+    # config/agent_config.yaml keys stay intact
+    ref = {"learning_rate", "gamma", "epsilon_start", "epsilon_min", "epsilon_decay_steps",
+           "replay_buffer_size", "batch_size", "target_update_frequency", "nn_layers"}
+    assert ref <= set(AgentConfig.__dataclass_fields__)
+    with open(f"{ROOT}/config/agent_config.yaml") as f:
+        y = yaml.safe_load(f)
+    assert ref <= set(y)
+    cfg = AgentConfig.from_dict(y)
+    assert cfg.nn_layers == y["nn_layers"]
