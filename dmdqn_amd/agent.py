@@ -158,7 +158,7 @@ class BatchedDQN:
     """E*A independent DQN agents (agent index = env * A + junction)."""
 
     def __init__(self, num_envs, n_agents, cfg: AgentConfig = None, device="cuda",
-                 env_seeds=None, init_weights=None):
+                 env_seeds=None, init_weights=None, streams=None):
         self.cfg = cfg = cfg or AgentConfig()
         _lib.load()
         H = cfg.nn_layers[0]
@@ -183,9 +183,15 @@ class BatchedDQN:
         self.adam_m = torch.zeros_like(self.params)
         self.adam_v = torch.zeros_like(self.params)
         self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev)
-        seeds = np.arange(num_envs, dtype=np.int64) + cfg.seed if env_seeds is None else np.asarray(env_seeds)
-        self.np_state = K.seed_streams(seeds, "np", dev)
-        self.py_state = K.seed_streams(seeds, "py", dev)
+        if streams is not None:
+            # shared (np_state, py_state) device streams, e.g. the process-global
+            # ones behind the per-agent DQNAgent surface
+            self.np_state, self.py_state = streams
+        else:
+            seeds = (np.arange(num_envs, dtype=np.int64) + cfg.seed if env_seeds is None
+                     else np.asarray(env_seeds))
+            self.np_state = K.seed_streams(seeds, "np", dev)
+            self.py_state = K.seed_streams(seeds, "py", dev)
         self.idx = torch.empty((NA, cfg.batch_size), dtype=torch.int32, device=dev)
         self.loss = torch.zeros(NA, dtype=torch.float32, device=dev)
         self.actions = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)

@@ -1,0 +1,52 @@
+"""Drop-in surfaces on the GPU: per-agent DQNAgent draw order vs the oracle
+streams, the reference-shaped train loop, and __graft_entry__.smoke()."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import oracle as O  # noqa: E402
+
+
+def test_dqnagent_draw_order_matches_global_streams():
+    from src.agents import dqn_agent
+    from src.env.traffic_env import EnvConfig, TrafficEnv
+    dqn_agent.seed(1234)
+    env = TrafficEnv(EnvConfig(rows=2, cols=2, num_envs=1, seed=3))
+    ids = env.get_controlled_intersection_ids()
+    cfg = {"nn_layers": [128, 128], "batch_size": 128, "replay_buffer_size": 500}
+    agents = {j: dqn_agent.DQNAgent(89, 4, j, cfg) for j in ids}
+    nps, pys = O.np_stream(1234), O.py_stream(1234)
+    state = env.reset_dict()
+    for step in range(130):
+        acts = {j: agents[j].select_action(state[j][None]) for j in ids}
+        np.testing.assert_array_equal([acts[j] for j in ids], O.act(nps, 4, 1.0))
+        nstate, rew, done, _ = env.step_dict(acts)
+        for j in ids:
+            agents[j].remember(state[j][None], acts[j], rew[j], nstate[j][None], done)
+            loss = agents[j].replay()
+            if step < 127:
+                assert loss == 0
+            else:
+                n = len(agents[j].replay_buffer)
+                exp = O.py_sample(pys, n, 128)
+                np.testing.assert_array_equal(agents[j]._core.idx.cpu().numpy()[0], exp)
+                assert loss > 0
+        state = nstate
+    b = agents[ids[0]].replay_buffer.sample(128)
+    assert b[0].shape == (128, 89) and b[2].dtype == torch.float32
+
+
+def test_train_loop_one_episode(tmp_path):
+    from src.scripts import train
+    m = tmp_path / "m.jsonl"
+    agents = train.train_agents(episodes=1, rows=2, cols=2, seed=0, metrics=str(m))
+    assert all(a.learn_step_counter == 240 - 127 for a in agents.values())
+    lines = m.read_text().strip().splitlines()
+    assert len(lines) == 240
+
+
+def test_graft_smoke():
+    import __graft_entry__
+    __graft_entry__.smoke()
