@@ -122,7 +122,9 @@ def main():
     ap.add_argument("--envs", type=int, default=1024, help="env replicas per GPU")
     ap.add_argument("--rows", type=int, default=4)
     ap.add_argument("--cols", type=int, default=4)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp16"])
+    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
+                    help="fp16 = the reference's mixed_float16 policy (f16 MFMA operands, "
+                         "f32 accumulate, f32 master weights + Adam); fp32 = strict path")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
@@ -209,7 +211,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.precision == "fp32" else "f16 (f32 accumulate, f32 master)",
+            "dtype": ("f32" if args.precision == "fp32" else
+                      "f16 (mixed_float16 as the reference: f16 MFMA operands, f32 accumulate, "
+                      "f32 master weights + Adam)"),
             "data": "synthetic (4x4 grid, randomTrips-style demand, Keras-style random init)",
             "config": {
                 "workload": f"C3: {args.rows}x{args.cols} grid ({A} agents) x {args.envs} envs/GPU, "
