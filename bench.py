@@ -131,14 +131,11 @@ def main():
 
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from dmdqn_amd import dist as D
+    rank, world, local = D.world()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    D.init(backend="nccl", device=dev)  # RCCL; only barrier + timing max use it
 
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.env import EnvConfig
@@ -165,8 +162,7 @@ def main():
         (starts if before else ends).append(ev)
 
     learn_before = tr.agent.learn_launches
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     torch.cuda.synchronize(dev)
     tr.agent.learn_hook = hook
     t0 = time.perf_counter()
@@ -174,17 +170,12 @@ def main():
         tr.step()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     tr.agent.learn_hook = None
     n_learn = tr.agent.learn_launches - learn_before
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    el_max = el
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el_max = float(t.item())
+    el_max = D.max_over_ranks(el, device=dev)
 
     if rank == 0:
         value = args.steps * NA * world / el_max
