@@ -127,15 +127,20 @@ def main():
                          "f32 accumulate, f32 master weights + Adam); fp32 = strict path")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, default) or gloo; only barrier + timing use it")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     from dmdqn_amd import dist as D
     rank, world, local = D.world()
+    # DMDQN_DEVICE_OVERRIDE pins every rank to one device (launch rehearsal on a
+    # 1-GPU box with --dist-backend gloo); normally rank r uses cuda:LOCAL_RANK
+    local = int(os.environ.get("DMDQN_DEVICE_OVERRIDE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    D.init(backend="nccl", device=dev)  # RCCL; only barrier + timing max use it
+    D.init(backend=args.dist_backend, device=dev)  # only barrier + timing max use it
 
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.env import EnvConfig

@@ -34,8 +34,9 @@ class CLearn(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ["NA", "cap", "start", "batch", "hidden", "precision",
                                          "sync_target", "P"]] + [
         (n, C.c_void_p) for n in ["ring_s", "ring_n", "ring_a", "ring_d", "ring_r", "idx",
-                                  "params", "adam_m", "adam_v", "target", "loss"]] + [
-        (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]]
+                                  "params", "adam_m", "adam_v", "target", "target_h",
+                                  "loss"]] + [
+        (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]] + [("stamps", C.c_void_p)]
 
 
 _lib.SIGNATURES.update({
@@ -180,6 +181,12 @@ class BatchedDQN:
         w = torch.as_tensor(init.reshape(NA, self.P))
         self.params = w.to(dev).contiguous()
         self.target = self.params.clone()
+        # fp16 path: the target forward reads an f16 copy (padded row stride Ph)
+        self.Ph = (self.P + 7) // 8 * 8
+        self.target_h = None
+        if cfg.precision == "fp16":
+            self.target_h = torch.zeros((NA, self.Ph), dtype=torch.float16, device=dev)
+            self._refresh_target_h()
         self.adam_m = torch.zeros_like(self.params)
         self.adam_v = torch.zeros_like(self.params)
         self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev)
@@ -201,6 +208,7 @@ class BatchedDQN:
         self.epsilon = cfg.epsilon_start
         self.learn_launches = 0
         self.learn_hook = None  # optional callable(before: bool), e.g. HIP event timing
+        self.stamps = None      # optional int64 [NA, 16] device tensor: phase timestamps
 
     # -------------------------------------------------------------- act
     def current_epsilon(self):
@@ -254,10 +262,12 @@ class BatchedDQN:
         sync = self.learn_step_counter % cfg.target_update_frequency == 0
         a = CLearn(self.NA, self.ring.cap, self.ring.start, cfg.batch_size, self.H,
                    PRECISIONS[cfg.precision], int(sync), self.P,
-                   *[t.data_ptr() for t in [self.ring.s, self.ring.n, self.ring.a, self.ring.d,
-                                            self.ring.r, self.idx, self.params, self.adam_m,
-                                            self.adam_v, self.target, self.loss]],
-                   np.float32(cfg.gamma), alpha, c1, c2, eps)
+                   *[None if t is None else t.data_ptr()
+                     for t in [self.ring.s, self.ring.n, self.ring.a, self.ring.d, self.ring.r,
+                               self.idx, self.params, self.adam_m, self.adam_v, self.target,
+                               self.target_h, self.loss]],
+                   np.float32(cfg.gamma), alpha, c1, c2, eps,
+                   None if self.stamps is None else self.stamps.data_ptr())
         if self.learn_hook:
             self.learn_hook(True)
         call("dmdqn_learn", C.byref(a), stream_of(self.device))
@@ -266,8 +276,13 @@ class BatchedDQN:
         self.learn_launches += 1
         return self.loss
 
+    def _refresh_target_h(self):
+        if self.target_h is not None:
+            self.target_h[:, :self.P].copy_(self.target.to(torch.float16))
+
     def update_target_network(self):
         self.target.copy_(self.params)
+        self._refresh_target_h()
 
     # -------------------------------------------------------------- weights
     def keras_params(self, which="params"):
@@ -290,6 +305,7 @@ class BatchedDQN:
         flat = np.concatenate([np.asarray(w, np.float32).reshape(-1) for w in weights])
         self.params[agent].copy_(torch.from_numpy(keras_to_kernel(flat, self.H)))
         self.target[agent].copy_(self.params[agent])
+        self._refresh_target_h()
 
     def state_dict(self):
         return {"params": self.params.cpu(), "target": self.target.cpu(),
@@ -300,5 +316,6 @@ class BatchedDQN:
     def load_state_dict(self, sd):
         for k in ["params", "target", "adam_m", "adam_v"]:
             getattr(self, k).copy_(sd[k].to(self.device))
+        self._refresh_target_h()
         self.learn_step_counter = int(sd["learn_step_counter"])
         self.global_step_count = int(sd["global_step_count"])

@@ -93,6 +93,25 @@ __device__ __forceinline__ half8 wfrag(const float *WT, int ld, int n0, int k0, 
     return r;
 }
 
+// Same fragment from an f16 copy (16-byte loads, no conversion).
+__device__ __forceinline__ half8 wfrag(const _Float16 *WT, int ld, int n0, int k0, int nvalid = 16) {
+    const int l = threadIdx.x & 63, lr = l & 15;
+    half8 r;
+    if (lr < nvalid) {
+        r = *reinterpret_cast<const half8 *>(WT + (size_t)(n0 + lr) * ld + k0 + 8 * (l >> 4));
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; e++) r[e] = (_Float16)0.0f;
+    }
+    return r;
+}
+
+__device__ __forceinline__ float4 ld_bias4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 ld_bias4(const _Float16 *p) {
+    const half4v h = *reinterpret_cast<const half4v *>(p);
+    return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+}
+
 __device__ __forceinline__ half8 ones8() {
     half8 r;
 #pragma unroll
@@ -107,78 +126,88 @@ struct Scratch {
     double *r64, *red;
 };
 
+// Per-wave register copy of one network's weights: the A-fragments of the
+// wave's 16 neurons for layers 1 and 2, the (4-row) output layer, and the
+// lane's biases.  Loaded once per network and reused by every forward that
+// network runs (the online net serves both the S' and the S forward).
+struct Frags {
+    half8 w1[3], w2[4];
+    float4 b1, b2;
+    // the output layer (2 KB, shared by all waves) is read at use, from the
+    // f32 master (online net) or the f16 copy (target net)
+    const float *Wg;
+    const _Float16 *Wh;
+};
+
+template <typename T>
+__device__ __forceinline__ void load_frags(const T *Wg, Frags &f) {
+    const int w = threadIdx.x >> 6, lg = (threadIdx.x & 63) >> 4;
+    const int n0 = 16 * w, n = n0 + 4 * lg;
+#pragma unroll
+    for (int s = 0; s < 3; s++) f.w1[s] = wfrag(Wg + L::oW1T, DP, n0, 32 * s);
+#pragma unroll
+    for (int s = 0; s < 4; s++) f.w2[s] = wfrag(Wg + L::oW2T, H, n0, 32 * s);
+    f.b1 = ld_bias4(Wg + L::ob1 + n);
+    f.b2 = ld_bias4(Wg + L::ob2 + n);
+    if constexpr (sizeof(T) == 4) { f.Wg = (const float *)Wg; f.Wh = nullptr; }
+    else { f.Wg = nullptr; f.Wh = (const _Float16 *)Wg; }
+}
+
+__device__ __forceinline__ half4v relu_h4(f32x4 acc, float4 b) {
+    half4v hv;
+    hv[0] = (_Float16)fmaxf(acc[0] + b.x, 0.0f);
+    hv[1] = (_Float16)fmaxf(acc[1] + b.y, 0.0f);
+    hv[2] = (_Float16)fmaxf(acc[2] + b.z, 0.0f);
+    hv[3] = (_Float16)fmaxf(acc[3] + b.w, 0.0f);
+    return hv;
+}
+
 // Forward of one 128-row batch X (in R2).  Leaves H1 in R1 and H2 in R2 (X is
 // overwritten by H2), Q in qout[128][4] (f32 of the f16 output, as Keras'
 // mixed policy emits f16 from the last Dense).
-__device__ void forward(const float *Wg, _Float16 *R1, _Float16 *R2, float *qout) {
+__device__ void forward(const Frags &f, _Float16 *R1, _Float16 *R2, float *qout) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
-    const int n0 = 16 * w;
-    const int n = n0 + 4 * lg;
-    // layer 1: K = 96 (3 k-steps); A from HBM, B = X rows
-    {
-        half8 a0 = wfrag(Wg + L::oW1T, DP, n0, 0);
-        half8 a1 = wfrag(Wg + L::oW1T, DP, n0, 32);
-        half8 a2 = wfrag(Wg + L::oW1T, DP, n0, 64);
-        const float4 bb = *reinterpret_cast<const float4 *>(Wg + L::ob1 + n);
-        f32x4 acc[8];
+    const int n = 16 * w + 4 * lg;
+    // layer 1: K = 96 (3 k-steps), B = X rows
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            f32x4 c = {0.f, 0.f, 0.f, 0.f};
-            c = mfma(a0, frag_row(R2, DP, 16 * t, 0), c);
-            c = mfma(a1, frag_row(R2, DP, 16 * t, 32), c);
-            acc[t] = mfma(a2, frag_row(R2, DP, 16 * t, 64), c);
-        }
+    for (int t = 0; t < 8; t++) {
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            half4v hv;
-            hv[0] = (_Float16)fmaxf(acc[t][0] + bb.x, 0.0f);
-            hv[1] = (_Float16)fmaxf(acc[t][1] + bb.y, 0.0f);
-            hv[2] = (_Float16)fmaxf(acc[t][2] + bb.z, 0.0f);
-            hv[3] = (_Float16)fmaxf(acc[t][3] + bb.w, 0.0f);
-            *reinterpret_cast<half4v *>(R1 + (16 * t + lr) * H + n) = hv;
-        }
+        for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row(R2, DP, 16 * t, 32 * s), c);
+        *reinterpret_cast<half4v *>(R1 + (16 * t + lr) * H + n) = relu_h4(c, f.b1);
     }
     __syncthreads();
-    // layer 2: K = 128; B = H1 rows (R1) ; output H2 -> R2 (X is dead)
+    // layer 2: K = 128, B = H1 rows (R1) ; H2 -> R2 (X is dead)
     {
-        const float *W2T = Wg + L::oW2T;
-        half8 a[4];
-#pragma unroll
-        for (int s = 0; s < 4; s++) a[s] = wfrag(W2T, H, n0, 32 * s);
-        const float4 bb = *reinterpret_cast<const float4 *>(Wg + L::ob2 + n);
         f32x4 acc[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; s++) c = mfma(a[s], frag_row(R1, H, 16 * t, 32 * s), c);
+            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row(R1, H, 16 * t, 32 * s), c);
             acc[t] = c;
         }
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            half4v hv;
-            hv[0] = (_Float16)fmaxf(acc[t][0] + bb.x, 0.0f);
-            hv[1] = (_Float16)fmaxf(acc[t][1] + bb.y, 0.0f);
-            hv[2] = (_Float16)fmaxf(acc[t][2] + bb.z, 0.0f);
-            hv[3] = (_Float16)fmaxf(acc[t][3] + bb.w, 0.0f);
-            *reinterpret_cast<half4v *>(R2 + (16 * t + lr) * H + n) = hv;
-        }
+        for (int t = 0; t < 8; t++)
+            *reinterpret_cast<half4v *>(R2 + (16 * t + lr) * H + n) = relu_h4(acc[t], f.b2);
     }
     __syncthreads();
     // layer 3: Q^T[a][b] = W3T[a][k] . H2[b][k]; wave w -> batch tile w
     {
-        const float *W3T = Wg + L::oW3T;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 4; s++)
-            acc = mfma(wfrag(W3T, H, 0, 32 * s, NACT), frag_row(R2, H, 16 * w, 32 * s), acc);
+        for (int s = 0; s < 4; s++) {
+            const half8 a3 = f.Wg ? wfrag(f.Wg + L::oW3T, H, 0, 32 * s, NACT)
+                                  : wfrag(f.Wh + L::oW3T, H, 0, 32 * s, NACT);
+            acc = mfma(a3, frag_row(R2, H, 16 * w, 32 * s), acc);
+        }
         if (lg == 0) {
-            const float4 bb = *reinterpret_cast<const float4 *>(Wg + L::ob3);
+            const float4 b3 = f.Wg ? ld_bias4(f.Wg + L::ob3) : ld_bias4(f.Wh + L::ob3);
             float4 q;
-            q.x = (float)(_Float16)(acc[0] + bb.x);
-            q.y = (float)(_Float16)(acc[1] + bb.y);
-            q.z = (float)(_Float16)(acc[2] + bb.z);
-            q.w = (float)(_Float16)(acc[3] + bb.w);
+            q.x = (float)(_Float16)(acc[0] + b3.x);
+            q.y = (float)(_Float16)(acc[1] + b3.y);
+            q.z = (float)(_Float16)(acc[2] + b3.z);
+            q.w = (float)(_Float16)(acc[3] + b3.w);
             *reinterpret_cast<float4 *>(qout + (16 * w + lr) * NACT) = q;
         }
     }
@@ -188,26 +217,53 @@ __device__ void forward(const float *Wg, _Float16 *R1, _Float16 *R2, float *qout
 struct AdamC {
     float alpha, c1, c2, eps;
     bool sync;
+    _Float16 *TH;  // f16 target copy written on syncs (or null)
 };
 
-// Keras-3 Adam on 4 consecutive parameters (one 16-byte lane access each).
+// Keras-3 Adam on NT groups of 4 consecutive parameters (one 16-byte lane
+// access each).  All w, m, v loads of the NT groups are issued before any
+// store, so one memory round trip covers NT tiles.
+template <int NT>
+__device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, const size_t *idx,
+                                       const f32x4 *g, const AdamC &k) {
+    float4 w[NT], m[NT], v[NT];
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+        w[q] = *reinterpret_cast<const float4 *>(W + idx[q]);
+        m[q] = *reinterpret_cast<const float4 *>(M + idx[q]);
+        v[q] = *reinterpret_cast<const float4 *>(V + idx[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+        float *pw = &w[q].x, *pm = &m[q].x, *pv = &v[q].x;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            float ge = g[q][e];
+            pm[e] = pm[e] + (ge - pm[e]) * k.c1;
+            pv[e] = pv[e] + (ge * ge - pv[e]) * k.c2;
+            pw[e] = pw[e] - (pm[e] * k.alpha) / (sqrtf(pv[e]) + k.eps);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+        *reinterpret_cast<float4 *>(W + idx[q]) = w[q];
+        *reinterpret_cast<float4 *>(M + idx[q]) = m[q];
+        *reinterpret_cast<float4 *>(V + idx[q]) = v[q];
+        if (k.sync) {
+            *reinterpret_cast<float4 *>(T + idx[q]) = w[q];
+            if (k.TH) {
+                half4v hv;
+                hv[0] = (_Float16)w[q].x; hv[1] = (_Float16)w[q].y;
+                hv[2] = (_Float16)w[q].z; hv[3] = (_Float16)w[q].w;
+                *reinterpret_cast<half4v *>(k.TH + idx[q]) = hv;
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void adam4(float *W, float *M, float *V, float *T, size_t i, f32x4 g,
                                       const AdamC &k) {
-    float4 w = *reinterpret_cast<float4 *>(W + i);
-    float4 m = *reinterpret_cast<float4 *>(M + i);
-    float4 v = *reinterpret_cast<float4 *>(V + i);
-    float *pw = &w.x, *pm = &m.x, *pv = &v.x;
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        float ge = g[e];
-        pm[e] = pm[e] + (ge - pm[e]) * k.c1;
-        pv[e] = pv[e] + (ge * ge - pv[e]) * k.c2;
-        pw[e] = pw[e] - (pm[e] * k.alpha) / (sqrtf(pv[e]) + k.eps);
-    }
-    *reinterpret_cast<float4 *>(W + i) = w;
-    *reinterpret_cast<float4 *>(M + i) = m;
-    *reinterpret_cast<float4 *>(V + i) = v;
-    if (k.sync) *reinterpret_cast<float4 *>(T + i) = w;
+    adam4n<1>(W, M, V, T, &i, &g, k);
 }
 
 __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, size_t i, float g,
@@ -219,8 +275,19 @@ __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, si
     M[i] = m;
     V[i] = v;
     W[i] = w;
-    if (k.sync) T[i] = w;
+    if (k.sync) {
+        T[i] = w;
+        if (k.TH) k.TH[i] = (_Float16)w;
+    }
 }
+
+// Diagnostics: block-level phase end time (after a barrier), only when a
+// stamps buffer is passed.  s_memrealtime ticks at 100 MHz.
+#define STAMP(i)                                                              \
+    do {                                                                      \
+        if (a.stamps && threadIdx.x == 0)                                     \
+            a.stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
 __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -235,7 +302,13 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     const size_t Pz = (size_t)L::P;
     float *Wp = a.params + agent * Pz, *Mp = a.adam_m + agent * Pz, *Vp = a.adam_v + agent * Pz;
     float *Tp = a.target + agent * Pz;
-    const AdamC AK{a.alpha, a.c1, a.c2, a.eps, a.sync_target != 0};
+    const size_t Ph = (Pz + 7) / 8 * 8;
+    _Float16 *TH = a.target_h ? reinterpret_cast<_Float16 *>(a.target_h) + agent * Ph : nullptr;
+    const AdamC AK{a.alpha, a.c1, a.c2, a.eps, a.sync_target != 0, TH};
+    STAMP(0);
+    Frags fr;
+    if (TH) load_frags(TH, fr);  // in flight during the z-score + gather
+    else load_frags(a.target + agent * Pz, fr);
 
     // ---- batch metadata + reward z-score (numpy pairwise order, f64)
     if (tid < B_) {
@@ -281,6 +354,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();
     if (tid < B_) S.rn[tid] = (float)__ddiv_rn(__dsub_rn(S.r64[tid], S.red[8]), S.red[9]);
+    STAMP(1);
 
     // replay rows (int8) -> X f16 [128][96] in R2
     auto gather = [&](const int8_t *ring) {
@@ -300,10 +374,15 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
 
     // ---- target(S') -> z3 ; online(S') -> Q in R1 (free during layer 3) ; y
     gather(a.ring_n);
-    forward(a.target + agent * Pz, R1, R2, S.z3);
+    STAMP(2);
+    forward(fr, R1, R2, S.z3);
+    STAMP(3);
+    load_frags(Wp, fr);  // online net: in flight during the gather, reused for S
     gather(a.ring_n);
+    STAMP(4);
     float *qo = (float *)R1;
-    forward(Wp, R1, R2, qo);
+    forward(fr, R1, R2, qo);
+    STAMP(5);
     if (tid < B_) {
         const float4 q = *reinterpret_cast<const float4 *>(qo + tid * NACT);
         int best = 0;
@@ -318,7 +397,9 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     __syncthreads();
     // ---- online(S), activations kept: H1 in R1, H2 in R2 ; q, loss, DQ
     gather(a.ring_s);
-    forward(Wp, R1, R2, S.z3);
+    STAMP(6);
+    forward(fr, R1, R2, S.z3);
+    STAMP(7);
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];
@@ -357,6 +438,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         }
     }
     __syncthreads();  // dW3 read H2; dZ2 overwrites it
+    STAMP(8);
     // ---- dZ2 = dq * W3[:, a] (ReLU mask), in place over H2 (8 columns per task)
     for (int t = tid; t < B_ * (H / 8); t += 512) {
         const int b = t >> 4, k8 = (t & 15) * 8, ac = S.act[b];
@@ -372,18 +454,22 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         *p = o;
     }
     __syncthreads();
-    // ---- dH1 A-fragments (OLD W2: W2[j][k] = W2T[k][j]) before Adam touches W2.
-    // Wave w reads and later updates exactly the columns j of its own tile.
-    half8 aw2[4];
+    STAMP(9);
+    // ---- ReLU mask of H1 as bits (the DQ region is free now): mask[b][j/32]
+    uint32_t *mask = reinterpret_cast<uint32_t *>(DQ);
     {
-        const float *W2T = Wp + L::oW2T;
+        const int b = tid >> 2, q = tid & 3;
+        const half8 *hp = reinterpret_cast<const half8 *>(R1 + b * H + 32 * q);
+        uint32_t bits = 0;
 #pragma unroll
-        for (int s = 0; s < 4; s++)
+        for (int c = 0; c < 4; c++) {
+            const half8 hv = hp[c];
 #pragma unroll
-            for (int e = 0; e < 8; e++)
-                aw2[s][e] = (_Float16)W2T[(size_t)(32 * s + 8 * lg + e) * H + 16 * w + lr];
+            for (int e = 0; e < 8; e++) bits |= ((float)hv[e] > 0.0f ? 1u : 0u) << (8 * c + e);
+        }
+        mask[b * 4 + q] = bits;
     }
-    // ---- dW2[j][k] = H1^T . dZ2 (wave w: j-tile w, 8 k-tiles) ; db2 (k-tile w)
+    // ---- dW2[j][k] = H1^T . dZ2 (wave w: j-tile w, 8 k-tiles) ; db2 (k-tile w) ; Adam
     {
         f32x4 g2[8], gb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -395,35 +481,50 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
 #pragma unroll
             for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr(R2, H, b0, 16 * t), g2[t]);
         }
-        // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3]
+        // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3].  The
+        // old W2 that dH1 needs is the f16 copy already held in fr.w2.
 #pragma unroll
-        for (int t = 0; t < 8; t++)
-            adam4(Wp, Mp, Vp, Tp, L::oW2T + (size_t)(16 * t + lr) * H + 16 * w + 4 * lg, g2[t], AK);
+        for (int h = 0; h < 4; h++) {
+            size_t ix[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) ix[q] = L::oW2T + (size_t)(16 * (2 * h + q) + lr) * H + 16 * w + 4 * lg;
+            adam4n<2>(Wp, Mp, Vp, Tp, ix, g2 + 2 * h, AK);
+        }
         if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob2 + 16 * w + lr, gb[0], AK);
     }
-    // ---- dH1^T[j][b] = W2[j][k] . dZ2^T  (wave w: j-tile w, 8 b-tiles)
+    __syncthreads();  // H1 fully consumed (dW2, mask): R1 becomes the W2^T image
+    // ---- W2^T f16 image [k][j] in R1 from the wave-owned forward fragments
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++)
+        *reinterpret_cast<half8 *>(R1 + (16 * w + lr) * H + 32 * s2 + 8 * lg) = fr.w2[s2];
+    __syncthreads();
+    // ---- dH1^T[j][b] = W2[j][k] . dZ2^T  (A: transposed read of the W2^T image)
     f32x4 d1[8];
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 8; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 4; s++) c = mfma(aw2[s], frag_row(R2, H, 16 * t, 32 * s), c);
-        d1[t] = c;
+    for (int s2 = 0; s2 < 4; s2++) {
+        const half8 av = frag_tr(R1, H, 32 * s2, 16 * w);
+#pragma unroll
+        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(R2, H, 16 * t, 32 * s2), d1[t]);
     }
-    __syncthreads();  // all reads of H1 (dW2) and dZ2 (dW2, dH1) done
-    // dZ1 = dH1 masked by ReLU(H1) -> R1 in place (lane: neurons j..j+3 of row b)
+    __syncthreads();  // image and dZ2 consumed
+    STAMP(10);
+    // dZ1 = dH1 masked by ReLU(H1) -> R1 (lane: neurons j..j+3 of row b)
     {
         const int j = 16 * w + 4 * lg;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
-            half4v *p = reinterpret_cast<half4v *>(R1 + (16 * t + lr) * H + j);
-            half4v h = *p, o;
+            const int b = 16 * t + lr;
+            const uint32_t bits = (mask[b * 4 + (j >> 5)] >> (j & 31)) & 0xfu;
+            half4v o;
 #pragma unroll
-            for (int e = 0; e < 4; e++) o[e] = (float)h[e] > 0.0f ? (_Float16)d1[t][e] : (_Float16)0.0f;
-            *p = o;
+            for (int e = 0; e < 4; e++) o[e] = ((bits >> e) & 1u) ? (_Float16)d1[t][e] : (_Float16)0.0f;
+            *reinterpret_cast<half4v *>(R1 + b * H + j) = o;
         }
     }
     gather(a.ring_s);  // X again (R2 is free), ends with a barrier
+    STAMP(11);
     // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
     {
         f32x4 g1[6], gb = {0.f, 0.f, 0.f, 0.f};
@@ -439,9 +540,17 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; padded
         // features 89..95 have zero weight and zero gradient and stay zero
 #pragma unroll
-        for (int t = 0; t < 6; t++)
-            adam4(Wp, Mp, Vp, Tp, L::oW1T + (size_t)(16 * w + lr) * DP + 16 * t + 4 * lg, g1[t], AK);
+        for (int h = 0; h < 2; h++) {
+            size_t ix[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) ix[q] = L::oW1T + (size_t)(16 * w + lr) * DP + 16 * (3 * h + q) + 4 * lg;
+            adam4n<3>(Wp, Mp, Vp, Tp, ix, g1 + 3 * h, AK);
+        }
         if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob1 + 16 * w + lr, gb[0], AK);
+    }
+    if (a.stamps) {
+        __syncthreads();
+        STAMP(12);
     }
 }
 

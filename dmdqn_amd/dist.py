@@ -47,6 +47,8 @@ def max_over_ranks(x: float, device="cpu"):
     """Slowest rank's value (the job's wall time)."""
     if not dist.is_initialized():
         return float(x)
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -154,8 +154,10 @@ int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *ac
  * (:376-377, :382-387) for NA independent agents in ONE launch (one workgroup
  * per agent): replay gather (ReplayBuffer.sample :64-84, z-scored rewards),
  * Double-DQN target, MSE loss, backward and Keras-3 Adam, fused.
- * Parameters use the Keras get_weights() layout per agent:
- *   W1[89][H] b1[H] W2[H][H] b2[H] W3[H][4] b3[4]   (P floats, row stride P).
+ * Parameters (and target, Adam m, v) use the device layout of qnet_layout.hpp
+ * per agent: W1T[H][96] W2T[H][H] W3T[4][H] b1[H] b2[H] b3[4] -- the Keras
+ * kernels transposed, fan-in padded to 96 (P floats, row stride P; the host
+ * converts to / from the Keras get_weights() order).
  * precision: 0 = fp32 MFMA (exact f32 products), 1 = fp16 MFMA with fp32
  * accumulation and fp32 master weights (the reference's mixed_float16). */
 typedef struct dmdqn_learn_args {
@@ -166,9 +168,17 @@ typedef struct dmdqn_learn_args {
     const int32_t *idx;              /* [NA][batch] deque positions          */
     float *params, *adam_m, *adam_v; /* [NA][P] online weights + Adam slots  */
     float *target;                   /* [NA][P] target network               */
+    uint16_t *target_h;              /* precision 1: [NA][Ph] f16 copy of the
+                                        target (Ph = P rounded up to 8) used by
+                                        the target forward -- Keras casts the
+                                        f32 target to f16 for its matmuls, so
+                                        this is the exact operand; written on
+                                        target syncs.  NULL: use `target`.     */
     float *loss;                     /* [NA] MSE loss of this learn (or NULL) */
     float gamma, alpha, c1, c2, eps; /* alpha = lr*sqrt(1-b2^t)/(1-b1^t),
                                         c1 = 1-b1, c2 = 1-b2 (float32)       */
+    uint64_t *stamps;                /* diagnostics: NULL, or [NA][16] phase
+                                        end times (s_memrealtime, 100 MHz)   */
 } dmdqn_learn_args;
 
 int dmdqn_learn(const dmdqn_learn_args *args, void *stream);
