@@ -27,6 +27,8 @@ PER_FILE = {
     "learn_f16.hip": ["-ffp-contract=fast"],
 }
 DEFAULT_FP = ["-ffp-contract=off"]
+# experiment hook: extra flags for every file (e.g. -D switches while tuning)
+EXTRA = os.environ.get("DMDQN_EXTRA_FLAGS", "").split()
 
 
 def _sources():
@@ -41,10 +43,12 @@ def _headers():
 def _compile(src, force):
     name = os.path.basename(src)
     obj = os.path.join(OBJDIR, name + ".o")
+    if EXTRA:
+        force = True
     newest = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest:
         return obj, False
-    flags = COMMON + PER_FILE.get(name, DEFAULT_FP)
+    flags = COMMON + PER_FILE.get(name, DEFAULT_FP) + EXTRA
     lang = ["-x", "hip"] if name.endswith(".hip") else []
     cmd = [HIPCC] + flags + lang + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -46,7 +46,9 @@ constexpr int R1_OFF = 0;
 constexpr int R2_OFF = R1_OFF + B_ * H * 2;
 constexpr int DQ_OFF = R2_OFF + B_ * H * 2;
 constexpr int SC_OFF = DQ_OFF + B_ * 16 * 2;
-constexpr int LDS_BYTES = SC_OFF + 6272;
+constexpr int W3_OFF = SC_OFF + 6272;          // f16 W3T images [2][4][128]: online, target
+constexpr int B3_OFF = W3_OFF + 2 * NACT * H * 2; // f32 b3 [2][4]
+constexpr int LDS_BYTES = B3_OFF + 2 * NACT * 4;
 static_assert(LDS_BYTES <= 81920, "two workgroups per CU");
 
 __device__ __forceinline__ f32x4 mfma(half8 a, half8 b, f32x4 c) {
@@ -133,25 +135,56 @@ struct Scratch {
 struct Frags {
     half8 w1[3], w2[4];
     float4 b1, b2;
-    // the output layer (2 KB, shared by all waves) is read at use, from the
-    // f32 master (online net) or the f16 copy (target net)
-    const float *Wg;
-    const _Float16 *Wh;
+};
+
+// The output layer (4 x 128) of a network as an f16 LDS image + f32 bias,
+// staged once per launch: the forwards' layer 3 and dZ2 read it from LDS, so
+// they never wait behind fragment prefetches in the in-order vmcnt queue, and
+// dZ2 sees the pre-update W3 (Adam on W3 runs before dZ2).
+struct OutL {
+    const _Float16 *w3;  // [4][128]
+    const float *b3;     // [4]
 };
 
 template <typename T>
-__device__ __forceinline__ void load_frags(const T *Wg, Frags &f) {
+__device__ __forceinline__ void load_w1(const T *Wg, Frags &f) {
     const int w = threadIdx.x >> 6, lg = (threadIdx.x & 63) >> 4;
-    const int n0 = 16 * w, n = n0 + 4 * lg;
 #pragma unroll
-    for (int s = 0; s < 3; s++) f.w1[s] = wfrag(Wg + L::oW1T, DP, n0, 32 * s);
-#pragma unroll
-    for (int s = 0; s < 4; s++) f.w2[s] = wfrag(Wg + L::oW2T, H, n0, 32 * s);
-    f.b1 = ld_bias4(Wg + L::ob1 + n);
-    f.b2 = ld_bias4(Wg + L::ob2 + n);
-    if constexpr (sizeof(T) == 4) { f.Wg = (const float *)Wg; f.Wh = nullptr; }
-    else { f.Wg = nullptr; f.Wh = (const _Float16 *)Wg; }
+    for (int s = 0; s < 3; s++) f.w1[s] = wfrag(Wg + L::oW1T, DP, 16 * w, 32 * s);
+    f.b1 = ld_bias4(Wg + L::ob1 + 16 * w + 4 * lg);
 }
+
+template <typename T>
+__device__ __forceinline__ void load_w2(const T *Wg, Frags &f) {
+    const int w = threadIdx.x >> 6, lg = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int s = 0; s < 4; s++) f.w2[s] = wfrag(Wg + L::oW2T, H, 16 * w, 32 * s);
+    f.b2 = ld_bias4(Wg + L::ob2 + 16 * w + 4 * lg);
+}
+
+// Stage W3T (f16) and b3 of one network into LDS (threads 0..127; caller syncs).
+template <typename T>
+__device__ __forceinline__ void stage_out(const T *Wg, _Float16 *w3, float *b3) {
+    const int t = threadIdx.x;
+    if (t < NACT * H / 4) {
+        const float4 v = ld_bias4(Wg + L::oW3T + 4 * t);
+        half4v hv;
+        hv[0] = (_Float16)v.x; hv[1] = (_Float16)v.y; hv[2] = (_Float16)v.z; hv[3] = (_Float16)v.w;
+        *reinterpret_cast<half4v *>(w3 + 4 * t) = hv;
+    } else if (t < NACT * H / 4 + NACT) {
+        b3[t - NACT * H / 4] = (float)Wg[L::ob3 + t - NACT * H / 4];
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void load_frags(const T *Wg, Frags &f) {
+    load_w1(Wg, f);
+    load_w2(Wg, f);
+}
+
+struct NoHook {
+    __device__ void operator()(Frags &) const {}
+};
 
 __device__ __forceinline__ half4v relu_h4(f32x4 acc, float4 b) {
     half4v hv;
@@ -162,10 +195,18 @@ __device__ __forceinline__ half4v relu_h4(f32x4 acc, float4 b) {
     return hv;
 }
 
-// Forward of one 128-row batch X (in R2).  Leaves H1 in R1 and H2 in R2 (X is
-// overwritten by H2), Q in qout[128][4] (f32 of the f16 output, as Keras'
-// mixed policy emits f16 from the last Dense).
-__device__ void forward(const Frags &f, _Float16 *R1, _Float16 *R2, float *qout) {
+// Forward of one 128-row batch X (in R2); Q -> qout[128][4] (f32 of the f16
+// output, as Keras' mixed policy emits f16 from the last Dense).
+//   KEEPX = false: H1 stays in R1, H2 goes to R2 over X (the training forward:
+//                  backward needs H1 and H2).
+//   KEEPX = true : H2 overwrites H1 in R1 after a barrier and X survives in R2
+//                  for a second forward on the same batch.
+// after_l1 / after_l2 run once the layer's MFMAs no longer need f.w1 / f.w2:
+// they may start loading the next network's fragments into f (the output
+// layer of THIS network is read through pointers captured before after_l2).
+template <bool KEEPX, typename H1k = NoHook, typename H2k = NoHook>
+__device__ void forward(Frags &f, const OutL o, _Float16 *R1, _Float16 *R2, float *qout,
+                        H1k after_l1 = {}, H2k after_l2 = {}) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
     const int n = 16 * w + 4 * lg;
     // layer 1: K = 96 (3 k-steps), B = X rows
@@ -176,8 +217,10 @@ __device__ void forward(const Frags &f, _Float16 *R1, _Float16 *R2, float *qout)
         for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row(R2, DP, 16 * t, 32 * s), c);
         *reinterpret_cast<half4v *>(R1 + (16 * t + lr) * H + n) = relu_h4(c, f.b1);
     }
+    after_l1(f);
     __syncthreads();
-    // layer 2: K = 128, B = H1 rows (R1) ; H2 -> R2 (X is dead)
+    // layer 2: K = 128, B = H1 rows (R1)
+    _Float16 *H2 = KEEPX ? R1 : R2;
     {
         f32x4 acc[8];
 #pragma unroll
@@ -187,9 +230,12 @@ __device__ void forward(const Frags &f, _Float16 *R1, _Float16 *R2, float *qout)
             for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row(R1, H, 16 * t, 32 * s), c);
             acc[t] = c;
         }
+        const float4 b2 = f.b2;
+        after_l2(f);
+        if (KEEPX) __syncthreads();  // every wave has read H1
 #pragma unroll
         for (int t = 0; t < 8; t++)
-            *reinterpret_cast<half4v *>(R2 + (16 * t + lr) * H + n) = relu_h4(acc[t], f.b2);
+            *reinterpret_cast<half4v *>(H2 + (16 * t + lr) * H + n) = relu_h4(acc[t], b2);
     }
     __syncthreads();
     // layer 3: Q^T[a][b] = W3T[a][k] . H2[b][k]; wave w -> batch tile w
@@ -197,17 +243,19 @@ __device__ void forward(const Frags &f, _Float16 *R1, _Float16 *R2, float *qout)
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            const half8 a3 = f.Wg ? wfrag(f.Wg + L::oW3T, H, 0, 32 * s, NACT)
-                                  : wfrag(f.Wh + L::oW3T, H, 0, 32 * s, NACT);
-            acc = mfma(a3, frag_row(R2, H, 16 * w, 32 * s), acc);
+            half8 a3;
+            if (lr < NACT) a3 = frag_row(o.w3, H, 0, 32 * s);
+            else
+#pragma unroll
+                for (int e = 0; e < 8; e++) a3[e] = (_Float16)0.0f;
+            acc = mfma(a3, frag_row(H2, H, 16 * w, 32 * s), acc);
         }
         if (lg == 0) {
-            const float4 b3 = f.Wg ? ld_bias4(f.Wg + L::ob3) : ld_bias4(f.Wh + L::ob3);
             float4 q;
-            q.x = (float)(_Float16)(acc[0] + b3.x);
-            q.y = (float)(_Float16)(acc[1] + b3.y);
-            q.z = (float)(_Float16)(acc[2] + b3.z);
-            q.w = (float)(_Float16)(acc[3] + b3.w);
+            q.x = (float)(_Float16)(acc[0] + o.b3[0]);
+            q.y = (float)(_Float16)(acc[1] + o.b3[1]);
+            q.z = (float)(_Float16)(acc[2] + o.b3[2]);
+            q.w = (float)(_Float16)(acc[3] + o.b3[3]);
             *reinterpret_cast<float4 *>(qout + (16 * w + lr) * NACT) = q;
         }
     }
@@ -309,6 +357,37 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     Frags fr;
     if (TH) load_frags(TH, fr);  // in flight during the z-score + gather
     else load_frags(a.target + agent * Pz, fr);
+    _Float16 *W3L = (_Float16 *)(smem + W3_OFF);
+    float *B3L = (float *)(smem + B3_OFF);
+    const OutL on{W3L, B3L}, tg{W3L + NACT * H, B3L + NACT};
+    stage_out(Wp, W3L, B3L);  // synced by the metadata barrier below
+    if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
+    else stage_out(Tp, W3L + NACT * H, B3L + NACT);
+
+    // replay rows (int8) -> X f16 [128][96] in R2, in two halves so the loads
+    // can be in flight across other work: issue (3 x 8 bytes per thread into
+    // registers), then commit (convert + LDS store) once R2 is free.
+    struct Rows { uint2 v[3]; };
+    auto gather_issue = [&](const int8_t *ring, Rows &g) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
+            g.v[i] = reinterpret_cast<const uint2 *>(ring + ((size_t)agent * a.cap + S.slot[b]) * DP)[q];
+        }
+    };
+    auto gather_commit = [&](const Rows &g) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
+            half8 hv;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                hv[e] = (_Float16)(float)(int8_t)(g.v[i].x >> (8 * e));
+                hv[e + 4] = (_Float16)(float)(int8_t)(g.v[i].y >> (8 * e));
+            }
+            *reinterpret_cast<half8 *>(R2 + b * DP + 8 * q) = hv;
+        }
+    };
 
     // ---- batch metadata + reward z-score (numpy pairwise order, f64)
     if (tid < B_) {
@@ -356,32 +435,27 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     if (tid < B_) S.rn[tid] = (float)__ddiv_rn(__dsub_rn(S.r64[tid], S.red[8]), S.red[9]);
     STAMP(1);
 
-    // replay rows (int8) -> X f16 [128][96] in R2
-    auto gather = [&](const int8_t *ring) {
-        for (int t = tid; t < B_ * (DP / 4); t += 512) {
-            int b = t / (DP / 4), q = t - b * (DP / 4);
-            const char4 c = reinterpret_cast<const char4 *>(
-                ring + ((size_t)agent * a.cap + S.slot[b]) * DP)[q];
-            half4v hv;
-            hv[0] = (_Float16)(float)c.x;
-            hv[1] = (_Float16)(float)c.y;
-            hv[2] = (_Float16)(float)c.z;
-            hv[3] = (_Float16)(float)c.w;
-            *reinterpret_cast<half4v *>(R2 + b * DP + 4 * q) = hv;
-        }
-        __syncthreads();
-    };
-
     // ---- target(S') -> z3 ; online(S') -> Q in R1 (free during layer 3) ; y
-    gather(a.ring_n);
+    {
+        Rows gn;
+        gather_issue(a.ring_n, gn);
+        gather_commit(gn);
+    }
+    __syncthreads();
     STAMP(2);
-    forward(fr, R1, R2, S.z3);
+    // target forward keeps X(S') in R2; the online net's fragments (reused by
+    // both online forwards) load layer by layer as the target's die
+    const float *Wpc = Wp;
+    forward<true>(fr, tg, R1, R2, S.z3, [Wpc](Frags &f) { load_w1(Wpc, f); },
+                  [Wpc](Frags &f) { load_w2(Wpc, f); });
     STAMP(3);
-    load_frags(Wp, fr);  // online net: in flight during the gather, reused for S
-    gather(a.ring_n);
+    // online(S'): X(S') is dead after layer 1, so the S rows for the training
+    // forward load during layers 1-2 and land in R2 while H2 sits in R1
+    float *qo = (float *)DQ;  // 2 KB; DQ is not needed until after the S forward
+    Rows gs;
+    forward<true>(fr, on, R1, R2, qo, [&](Frags &) { gather_issue(a.ring_s, gs); },
+                  [&](Frags &) { gather_commit(gs); });
     STAMP(4);
-    float *qo = (float *)R1;
-    forward(fr, R1, R2, qo);
     STAMP(5);
     if (tid < B_) {
         const float4 q = *reinterpret_cast<const float4 *>(qo + tid * NACT);
@@ -396,9 +470,8 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();
     // ---- online(S), activations kept: H1 in R1, H2 in R2 ; q, loss, DQ
-    gather(a.ring_s);
     STAMP(6);
-    forward(fr, R1, R2, S.z3);
+    forward<false>(fr, on, R1, R2, S.z3);
     STAMP(7);
     float lsum = 0.0f;
     if (tid < B_) {
@@ -444,13 +517,11 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         const int b = t >> 4, k8 = (t & 15) * 8, ac = S.act[b];
         half8 *p = reinterpret_cast<half8 *>(R2 + b * H + k8);
         half8 h = *p, o;
-        const float4 *w3 = reinterpret_cast<const float4 *>(Wp + L::oW3T + (size_t)ac * H + k8);
-        const float4 u = w3[0], v = w3[1];
-        const float wv[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        const half8 wv = *reinterpret_cast<const half8 *>(on.w3 + ac * H + k8);  // pre-update W3
         const float dq = S.dq[b];
 #pragma unroll
         for (int e = 0; e < 8; e++)
-            o[e] = (float)h[e] > 0.0f ? (_Float16)(dq * (float)(_Float16)wv[e]) : (_Float16)0.0f;
+            o[e] = (float)h[e] > 0.0f ? (_Float16)(dq * (float)wv[e]) : (_Float16)0.0f;
         *p = o;
     }
     __syncthreads();
@@ -493,6 +564,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob2 + 16 * w + lr, gb[0], AK);
     }
     __syncthreads();  // H1 fully consumed (dW2, mask): R1 becomes the W2^T image
+
     // ---- W2^T f16 image [k][j] in R1 from the wave-owned forward fragments
 #pragma unroll
     for (int s2 = 0; s2 < 4; s2++)
@@ -509,6 +581,11 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(R2, H, 16 * t, 32 * s2), d1[t]);
     }
     __syncthreads();  // image and dZ2 consumed
+    {
+        Rows gx;  // X(S) again for dW1 (R2 is free)
+        gather_issue(a.ring_s, gx);
+        gather_commit(gx);
+    }
     STAMP(10);
     // dZ1 = dH1 masked by ReLU(H1) -> R1 (lane: neurons j..j+3 of row b)
     {
@@ -523,7 +600,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
             *reinterpret_cast<half4v *>(R1 + b * H + j) = o;
         }
     }
-    gather(a.ring_s);  // X again (R2 is free), ends with a barrier
+    __syncthreads();
     STAMP(11);
     // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
     {

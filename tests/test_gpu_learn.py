@@ -104,9 +104,12 @@ def test_learn_gate_and_q_argmax():
 
 # ---------------------------------------------------------------------------
 # fp16 (mixed_float16) path
-def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e-3):
+def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e-3,
+                     w3_dz2=None):
     """numpy restatement of the kernel's rounding points: f16 operands, f32
-    accumulation, f16 activations / Q / activation-gradients, f32 Adam."""
+    accumulation, f16 activations / Q / activation-gradients, f32 Adam.
+    w3_dz2 overrides the W3 [H][4] that backprop uses for dZ2 (test hook: the
+    correct value is the pre-update W3)."""
     f16, f32 = np.float16, np.float32
 
     def split(w):
@@ -141,7 +144,8 @@ def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e
     W1, b1, W2, b2, W3, b3 = wo
     gW3 = h2.T @ DQ
     gb3 = DQ.sum(0)
-    dz2 = np.where(h2 > 0, (dq16[:, None] * W3[:, Aa].T), 0).astype(f16).astype(f32)
+    W3b = W3 if w3_dz2 is None else w3_dz2.astype(f16).astype(f32)
+    dz2 = np.where(h2 > 0, (dq16[:, None] * W3b[:, Aa].T), 0).astype(f16).astype(f32)
     gb2 = dz2.sum(0)
     gW2 = h1.T @ dz2
     dz1 = np.where(h1 > 0, dz2 @ W2.T, 0).astype(f16).astype(f32)
@@ -189,6 +193,17 @@ def test_learn_fp16_matches_mixed_emulation_and_fp32_oracle():
         p1, m1, v1 = p0[j].copy(), zero.copy(), zero.copy()
         l32 = O.learn(p1, t0[j], m1, v1, S, Aa, Rn, S2, D, 1)
         np.testing.assert_allclose(loss[j], l32, rtol=2e-2)
+        # backprop must use the PRE-update W3 (Adam on W3 runs first in the
+        # kernel): the gradients of W1/b1/W2/b2 sit far closer to that emulation
+        # than to one using the post-update W3 (a ~1% relative shift)
+        o_w3e = o_w3 + 4 * H
+        w3_new = p_e[o_w3:o_w3e].reshape(H, 4)
+        _, g_bad, _, _, _ = _mixed_emulation(p0[j], t0[j], zero, zero.copy(), S, Aa, Rn, S2, D, 1,
+                                             w3_dz2=w3_new)
+        big = np.abs(g_e[:o_w3]) > 0.1 * np.abs(g_e[:o_w3]).max()
+        err_ok = np.median(np.abs(g_g[:o_w3] - g_e[:o_w3])[big] / np.abs(g_e[:o_w3])[big])
+        err_bad = np.median(np.abs(g_g[:o_w3] - g_bad[:o_w3])[big] / np.abs(g_bad[:o_w3])[big])
+        assert err_ok < 0.3 * err_bad, (err_ok, err_bad)
         dw_g, dw_o = p_g[j] - p0[j], p1 - p0[j]
         assert np.corrcoef(dw_g, dw_o)[0, 1] > 0.97
     # second learn triggers the target sync (frequency 2)
