@@ -116,45 +116,147 @@ __device__ __forceinline__ uint32_t py_randbelow(MTWave &w, uint32_t n) {
     return r;
 }
 
-// CPython Random.sample (3.10/3.11), population = deque of length n.
-// Pool branch (n <= setsize): partial Fisher-Yates over a u32 pool in LDS.
-// Set branch: rejection against an n-bit "selected" bitmap in LDS.
-// All lanes execute the same loop and perform the same (identical-value)
-// LDS updates, so each lane's reads are ordered after its own writes.
+// CPython Random.sample (3.10/3.11), population = deque of length n:
+//   pool branch (n <= setsize): pool = list(range(n)); for i < k:
+//       j = randbelow(n - i); result[i] = pool[j]; pool[j] = pool[n - i - 1]
+//   set branch: for i < k: j = randbelow(n), redrawn while j in selected.
+// randbelow(m) = getrandbits(bit_length(m)), redrawn while >= m.
+//
+// One wave per env consumes the env's stream 64 tempered words at a time
+// ("chunk", lane l <-> word mti + l) and decides every word of the chunk at
+// once instead of one dependent LDS round trip per draw:
+//  * pool branch, phase 1: whether a word is accepted depends only on the
+//    word and on m = n - i, never on the pool.  Lane l is accepted iff
+//    getrandbits(bit_length(m - c_l)) < m - c_l, where c_l counts the accepted
+//    lanes below l.  That recurrence is solved by iterating
+//    c <- exclusive popcount(ballot(accepted(c))) from c = 0: each pass makes
+//    at least one more lane exact (lane 0 always is), and a fixed point is the
+//    sequential answer.  Accepted positions j go to LDS, per agent.
+//    Phase 2: every agent's k pool swaps run in parallel, lane = agent, each
+//    on its own u16 pool in LDS (only the swap chain is sequential).
+//  * set branch: out-of-range words and words already selected (LDS bitmap)
+//    are rejected in parallel; a repeat within the chunk is rejected when an
+//    earlier lane holds the same value (lane-shuffle compare); positions in
+//    the sample come from the popcount prefix.
+// In both branches the agent whose k-th pick falls inside a chunk consumes
+// the chunk only up to that lane; the next agent starts at the lane after.
+__device__ __forceinline__ uint32_t bitlen(uint32_t m) { return 32u - (uint32_t)__clz(m); }
+__device__ __forceinline__ uint32_t getbits(uint32_t u, uint32_t kb) {
+    return u >> (32u - kb);  // kb in 1..32
+}
+__device__ __forceinline__ uint64_t lanes_below() {
+    const int l = threadIdx.x;
+    return l ? (~0ull >> (64 - l)) : 0ull;
+}
+
 __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32_t n, int k,
                                                uint32_t setsize, int32_t *idx) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *mt = smem, *tmp = smem + MT_N, *aux = smem + 2 * MT_N;
     MTWave w{mt, tmp, 0};
-    const int e = blockIdx.x;
+    const int e = blockIdx.x, l = threadIdx.x;
     uint32_t *g = py_state + (size_t)e * DMDQN_MT_WORDS;
     w.load(g);
-    const bool pool_branch = n <= setsize;
-    for (int j = 0; j < A; j++) {
-        int32_t *out = idx + ((size_t)e * A + j) * k;
-        if (pool_branch) {
-            for (uint32_t i = threadIdx.x; i < n; i += 64) aux[i] = i;
-            __syncthreads();
-            for (int i = 0; i < k; i++) {
-                uint32_t m = n - (uint32_t)i;
-                uint32_t jj = py_randbelow(w, m);
-                uint32_t v = aux[jj];
-                if (threadIdx.x == 0) out[i] = (int32_t)v;
-                aux[jj] = aux[m - 1];
+    if (n <= setsize) {
+        uint16_t *sel = reinterpret_cast<uint16_t *>(aux);           // [A][k]
+        uint16_t *pool = sel + (((size_t)A * k + 1) & ~(size_t)1);  // [min(A,64)][n]
+        // ---- phase 1: the stream -> accepted j per (agent, i)
+        int j = 0, i = 0;
+        while (j < A) {
+            if (w.mti >= MT_N) w.refill();
+            const int cnt = min(64, MT_N - w.mti);
+            const bool live = l < cnt;
+            const uint32_t u = tmp[w.mti + (live ? l : 0)];
+            const uint32_t m0 = n - (uint32_t)i;
+            uint64_t acc = 0;
+            int c = 0;
+            uint32_t r = 0;
+            bool a = false;
+            for (;;) {
+                const uint32_t mm = (uint32_t)c < m0 ? m0 - (uint32_t)c : 1u;
+                r = getbits(u, bitlen(mm));
+                a = live && r < mm;
+                const uint64_t nacc = __ballot(a);
+                if (nacc == acc) break;
+                acc = nacc;
+                c = __popcll(acc & lanes_below());
             }
-        } else {
-            const uint32_t words = (n + 31u) >> 5;
-            for (uint32_t i = threadIdx.x; i < words; i += 64) aux[i] = 0u;
-            __syncthreads();
-            for (int i = 0; i < k; i++) {
-                uint32_t jj = py_randbelow(w, n);
-                while (aux[jj >> 5] & (1u << (jj & 31))) jj = py_randbelow(w, n);
-                aux[jj >> 5] |= (1u << (jj & 31));
-                if (threadIdx.x == 0) out[i] = (int32_t)jj;
+            const int total = __popcll(acc), need = k - i;
+            int taken = total, consumed = cnt;
+            if (total >= need) {
+                const uint64_t last = __ballot(a && c == need - 1);
+                consumed = __ffsll((unsigned long long)last);  // lane + 1
+                taken = need;
             }
+            if (a && c < taken) sel[(size_t)j * k + i + c] = (uint16_t)r;
+            w.mti += consumed;
+            i += taken;
+            if (i == k) { j++; i = 0; }
         }
         __syncthreads();
+        // ---- phase 2: pool swaps, lane = agent (groups of 64 agents)
+        for (int j0 = 0; j0 < A; j0 += 64) {
+            const int G = min(64, A - j0);
+            for (uint32_t t = l; t < (uint32_t)G * n; t += 64) pool[t] = (uint16_t)(t % n);
+            __syncthreads();
+            if (l < G) {
+                uint16_t *P = pool + (size_t)l * n;
+                const uint16_t *Sj = sel + (size_t)(j0 + l) * k;
+                int32_t *o = idx + ((size_t)e * A + j0 + l) * k;
+                for (int q = 0; q < k; q++) {
+                    const uint32_t x = Sj[q];
+                    const uint16_t v = P[x], last = P[n - 1 - (uint32_t)q];
+                    o[q] = (int32_t)v;
+                    P[x] = last;
+                }
+            }
+            __syncthreads();
+        }
+    } else {
+        uint32_t *bm = aux;  // selected bitmap, n bits
+        const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
+        for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
+        __syncthreads();
+        int j = 0, i = 0;
+        while (j < A) {
+            if (w.mti >= MT_N) w.refill();
+            const int cnt = min(64, MT_N - w.mti);
+            const bool live = l < cnt;
+            const uint32_t r = getbits(tmp[w.mti + (live ? l : 0)], kb);
+            bool cand = live && r < n;
+            if (cand) cand = !((bm[r >> 5] >> (r & 31)) & 1u);
+            // a repeat of an earlier candidate lane in the same chunk is rejected
+            const uint32_t key = cand ? r : (0x80000000u | (uint32_t)l);
+            bool dup = false;
+            for (int d = 1; d < cnt; d++) {
+                const uint32_t o = __shfl(key, (l - d) & 63);
+                dup |= (l >= d) && (o == key);
+            }
+            const bool a = cand && !dup;
+            const uint64_t acc = __ballot(a);
+            const int c = __popcll(acc & lanes_below());
+            const int total = __popcll(acc), need = k - i;
+            int taken = total, consumed = cnt;
+            if (total >= need) {
+                const uint64_t last = __ballot(a && c == need - 1);
+                consumed = __ffsll((unsigned long long)last);
+                taken = need;
+            }
+            if (a && c < taken) {
+                idx[((size_t)e * A + j) * k + i + c] = (int32_t)r;
+                atomicOr(&bm[r >> 5], 1u << (r & 31));
+            }
+            w.mti += consumed;
+            i += taken;
+            if (i == k) {
+                j++;
+                i = 0;
+                for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
+            }
+            __syncthreads();
+        }
     }
+    __syncthreads();
     w.store(g);
 }
 
@@ -202,8 +304,12 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
     DMDQN_REQUIRE(k >= 1 && n >= k, "dmdqn_replay_sample: need 1 <= k <= n (k=%d n=%d)", k, n);
     uint32_t setsize = 21;
     if (k > 5) setsize += (uint32_t)pow(4.0, ceil(log((double)k * 3.0) / log(4.0)));
-    size_t aux_words = ((uint32_t)n <= setsize) ? (size_t)n : (size_t)((n + 31) / 32);
-    size_t lds = (2 * MT_N + aux_words) * sizeof(uint32_t);
+    const bool pool = (uint32_t)n <= setsize;
+    DMDQN_REQUIRE(!pool || n <= 65535, "dmdqn_replay_sample: pool branch needs n <= 65535");
+    // pool branch: u16 sel [A][k] + u16 pools [min(A,64)][n]; set branch: n-bit bitmap
+    size_t aux_bytes = pool ? (((size_t)A * k + 1) & ~(size_t)1) * 2 + (size_t)(A < 64 ? A : 64) * n * 2
+                            : (size_t)((n + 31) / 32) * 4;
+    size_t lds = 2 * MT_N * sizeof(uint32_t) + aux_bytes;
     DMDQN_REQUIRE(lds <= 160 * 1024, "dmdqn_replay_sample: n=%d too large for LDS", n);
     hipLaunchKernelGGL(k_sample, dim3(E), dim3(64), lds, as_stream(stream), py_state, A,
                        (uint32_t)n, k, setsize, idx);

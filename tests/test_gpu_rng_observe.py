@@ -67,6 +67,21 @@ def test_replay_sample_matches_cpython(n):
                 np.testing.assert_array_equal(idx[e, j], O.py_sample(refs[e], n, 128))
 
 
+@pytest.mark.parametrize("A,n,k", [(64, 200, 128), (70, 300, 32), (3, 21, 5), (3, 22, 5),
+                                   (5, 7, 7), (2, 3000, 1000), (64, 10000, 128), (1, 128, 128)])
+def test_replay_sample_shapes(A, n, k):
+    """Agent groups beyond one wave (A > 64), small k (setsize 21), k = n and
+    large k: every branch and chunk-boundary case of the chunked sampler."""
+    seeds = [5, 6, 7]
+    st = K.seed_streams(seeds, "py")
+    refs = [O.py_stream(s) for s in seeds]
+    for rep in range(2):
+        idx = K.replay_sample(st, A, n, k).cpu().numpy().reshape(len(seeds), A, k)
+        for e in range(len(seeds)):
+            for j in range(A):
+                np.testing.assert_array_equal(idx[e, j], O.py_sample(refs[e], n, k))
+
+
 @pytest.mark.parametrize("grid", [(1, 1), (2, 2), (3, 3), (4, 4), (8, 8), (2, 3)])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_observe_reward(grid, mode):
