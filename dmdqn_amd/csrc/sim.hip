@@ -69,7 +69,7 @@ struct EnvView {
 };
 
 // ---------------------------------------------------------------- substep
-__device__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
+__device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
     const dmdqn_sim &S = V.S;
     const int R = S.R, C = S.C, A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -279,13 +279,66 @@ __device__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
     __syncthreads();
 }
 
+// LDS image of one env's mutable state (kLDS path): x, v, dst rings
+// [NL][cap], then head, cnt, req, gfrom, fx, fv [NL], phase, ts [A], qptr [4A],
+// stats [4].  4x4 grid, cap 24: 75 KB -> two envs per CU.
+__host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
+    const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
+    return (size_t)NL * cap * 12 + (size_t)NL * 6 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16;
+}
+
+// One RL step per env (block).  kLDS: the env's state is staged into LDS for
+// the K substeps (every pass is then an LDS-latency loop instead of an L2 one:
+// pass C walks each lane's vehicles front to back) and only occupied ring
+// slots move between HBM and LDS.  !kLDS: the same passes on global memory,
+// for grids whose state exceeds LDS.
+template <bool kLDS>
 __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, const int32_t *actions,
                                                   int stride, int t0, int K, int max_time,
                                                   int32_t *halt, int32_t *phase_out,
                                                   int32_t *tspent, uint8_t *done) {
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    EnvView G(S, blockIdx.x);
     EnvView V(S, blockIdx.x);
-    const int A = V.A;
+    const int A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
+    if constexpr (kLDS) {
+        const size_t NS = (size_t)NL * cap;
+        V.x = reinterpret_cast<float *>(dyn);
+        V.v = V.x + NS;
+        V.dst = reinterpret_cast<int32_t *>(V.v + NS);
+        V.head = V.dst + NS;
+        V.cnt = V.head + NL;
+        V.req = V.cnt + NL;
+        V.gfrom = V.req + NL;
+        V.fx = reinterpret_cast<float *>(V.gfrom + NL);
+        V.fv = V.fx + NL;
+        V.phase = reinterpret_cast<int32_t *>(V.fv + NL);
+        V.ts = V.phase + A;
+        V.qptr = V.ts + A;
+        V.stats = V.qptr + 4 * A;
+        for (int l = tid; l < NL; l += nt) {
+            V.head[l] = G.head[l];
+            V.cnt[l] = G.cnt[l];
+        }
+        for (int a = tid; a < A; a += nt) {
+            V.phase[a] = G.phase[a];
+            V.ts[a] = G.ts[a];
+        }
+        for (int e = tid; e < 4 * A; e += nt) V.qptr[e] = G.qptr[e];
+        if (tid < 4) V.stats[tid] = G.stats[tid];
+        __syncthreads();
+        for (int i = tid; i < (int)NS; i += nt) {
+            const int l = i / cap, sl = i - l * cap;
+            int off = sl - V.head[l];
+            if (off < 0) off += cap;
+            if (off < V.cnt[l]) {
+                V.x[i] = G.x[i];
+                V.v[i] = G.v[i];
+                V.dst[i] = G.dst[i];
+            }
+        }
+    }
     if (actions) {
         for (int a = tid; a < A; a += nt) {
             V.phase[a] = stride * actions[(size_t)blockIdx.x * A + a];
@@ -300,15 +353,15 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, cons
     if (tid == 0) { s_running = 0; s_pending = 0; }
     __syncthreads();
     int run = 0, pend = 0;
-    for (int l = tid; l < V.NL; l += nt) {
+    for (int l = tid; l < NL; l += nt) {
         const int n = V.cnt[l];
         run += n;
         if (l < 12 * A) {
             int h = 0, s = V.head[l];
-            const size_t base = (size_t)l * V.cap;
+            const size_t base = (size_t)l * cap;
             for (int i = 0; i < n; i++) {
                 h += V.v[base + s] < P.halt_speed ? 1 : 0;
-                s = (s + 1 == V.cap) ? 0 : s + 1;
+                s = (s + 1 == cap) ? 0 : s + 1;
             }
             halt[(size_t)blockIdx.x * 12 * A + l] = h;
         }
@@ -322,9 +375,34 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, cons
     }
     __syncthreads();
     if (tid == 0) {
-        V.stats[2] = s_running;
-        V.stats[3] = s_pending;
+        G.stats[0] = V.stats[0];
+        G.stats[1] = V.stats[1];
+        G.stats[2] = s_running;
+        G.stats[3] = s_pending;
         done[blockIdx.x] = (t >= max_time || (s_running + s_pending) == 0) ? 1 : 0;
+    }
+    if constexpr (kLDS) {
+        // write back: occupied slots, lane heads/counts, signals, queues
+        const size_t NS = (size_t)NL * cap;
+        for (int i = tid; i < (int)NS; i += nt) {
+            const int l = i / cap, sl = i - l * cap;
+            int off = sl - V.head[l];
+            if (off < 0) off += cap;
+            if (off < V.cnt[l]) {
+                G.x[i] = V.x[i];
+                G.v[i] = V.v[i];
+                G.dst[i] = V.dst[i];
+            }
+        }
+        for (int l = tid; l < NL; l += nt) {
+            G.head[l] = V.head[l];
+            G.cnt[l] = V.cnt[l];
+        }
+        for (int a = tid; a < A; a += nt) {
+            G.phase[a] = V.phase[a];
+            G.ts[a] = V.ts[a];
+        }
+        for (int e = tid; e < 4 * A; e += nt) G.qptr[e] = V.qptr[e];
     }
 }
 
@@ -377,8 +455,14 @@ extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const 
     DMDQN_REQUIRE(idm && halt && phase && tspent && done, "dmdqn_sim_step: null output");
     DMDQN_REQUIRE(K >= 0 && t0 >= 0 && action_stride >= 0, "dmdqn_sim_step: K/t0");
     DMDQN_REQUIRE(action_stride * 3 < 12, "dmdqn_sim_step: action_stride*3 must be < 12");
-    hipLaunchKernelGGL(k_sim_step, dim3(sim->E), dim3(256), 0, as_stream(stream), *sim, *idm,
-                       actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+    const size_t lds = sim_lds_bytes(sim->R, sim->C, sim->cap_lane);
+    if (lds <= 160 * 1024 - 64) {
+        hipLaunchKernelGGL(k_sim_step<true>, dim3(sim->E), dim3(256), lds, as_stream(stream), *sim,
+                           *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+    } else {
+        hipLaunchKernelGGL(k_sim_step<false>, dim3(sim->E), dim3(256), 0, as_stream(stream), *sim,
+                           *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+    }
     DMDQN_LAUNCH_CHECK("k_sim_step");
     return DMDQN_OK;
 }
