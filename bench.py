@@ -38,6 +38,13 @@ def learn_bytes_per_agent(P, batch=128):
     return batch * REPLAY_ROW_BYTES + 28 * P
 
 
+# Q-net FLOPs of one agent's learn: B*(4F + F') with
+# F = 2(89*128 + 128*128 + 128*4), F' = 2(128*128 + 128*4) -> 33.3 MFLOP
+LEARN_FLOP_PER_AGENT = 128 * (4 * 2 * (89 * 128 + 128 * 128 + 128 * 4) + 2 * (128 * 128 + 128 * 4))
+MFMA_F16_DENSE_TFLOPS = 2500.0  # MI355X dense F16/BF16 MFMA peak (MI355X_MICROARCH.md)
+SIM_BYTES_PER_VEH_SUBSTEP = 20  # read x, v, lane cursor (12 B) + write x, v (8 B)
+
+
 def cpu_baseline(rows, cols, budget_s=15.0, max_steps=200, seed=0):
     """The C oracle (oracle/, a restatement of the reference semantics) running
     the same loop for ONE env of the same grid, 1 thread, learn active.
@@ -114,6 +121,20 @@ def read_traffic(workload_key):
         return None
 
 
+def _sim_roofline(E, K, vbar, sim_ms, traffic):
+    """Sim-only HBM figure: 20*K*V-bar algorithmic bytes per env
+    step over the average k_sim_step duration (HIP events, timed region)."""
+    t = float(np.mean(sim_ms)) / 1e3
+    b = E * SIM_BYTES_PER_VEH_SUBSTEP * K * vbar
+    return {"kernel": "k_sim_step (K IDM substeps per launch, env state staged in LDS)",
+            "bound": "hbm", "achieved": round(b / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 5),
+            "traffic": traffic, "bytes_per_launch": int(b), "mean_running_vehicles": round(vbar, 1),
+            "avg_launch_ms": round(t * 1e3, 4),
+            "note": "latency-bound: the per-env working set is cache-resident; bytes are "
+                    "20 B per vehicle-substep as SURVEY 8d defines them"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,6 +167,10 @@ def main():
     from dmdqn_amd.env import EnvConfig
     from dmdqn_amd.trainer import Trainer
 
+    # all work on one dedicated stream: HIP events recorded on the legacy null
+    # stream block the host and would inflate the timed region
+    work = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
     agent_cfg = AgentConfig(precision=args.precision, seed=1000 + rank)
@@ -166,17 +191,32 @@ def main():
         ev.record(torch.cuda.current_stream(dev))
         (starts if before else ends).append(ev)
 
+    sim_starts, sim_ends = [], []
+
+    def sim_hook(before):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        (sim_starts if before else sim_ends).append(ev)
+
+    # running vehicles per env after each step, summed on the device (V-bar for
+    # the sim's algorithmic bytes); one tiny elementwise add per step
+    vsum = torch.zeros(E, dtype=torch.int64, device=dev)
     learn_before = tr.agent.learn_launches
     D.barrier()
     torch.cuda.synchronize(dev)
     tr.agent.learn_hook = hook
+    tr.env.sim_hook = sim_hook
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.step()
+        vsum += tr.env.t_stats[:, 2]
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     D.barrier()
     tr.agent.learn_hook = None
+    tr.env.sim_hook = None
+    sim_ms = [s.elapsed_time(e) for s, e in zip(sim_starts, sim_ends)]
+    vbar = float(vsum.double().mean().item()) / args.steps
     n_learn = tr.agent.learn_launches - learn_before
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
@@ -233,6 +273,17 @@ def main():
                 "learn_share_of_step": round(avg_learn_s / (el_max / args.steps), 3),
             },
             "cpu_baseline": cpu,
+            # secondary figures SURVEY 8d asks for next to the headline roofline
+            "sim_roofline": _sim_roofline(E, tr.env.cfg.step_duration, vbar, sim_ms,
+                                          read_traffic(f"{wl}_sim")),
+            "mfma": {
+                "kernel": "k_learn_f16 (Q-net forward/backward, v_mfma_f32_16x16x32_f16)",
+                "flop_per_launch": NA * LEARN_FLOP_PER_AGENT,
+                "achieved": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12, 2),
+                "peak": MFMA_F16_DENSE_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12 / MFMA_F16_DENSE_TFLOPS, 4),
+            },
         }
         print(json.dumps(out))
     if world > 1:

@@ -141,6 +141,7 @@ class TrafficEnv:
         self.obs = None
         self.t = 0
         self.episode = 0
+        self.sim_hook = None  # callable(before: bool) around the sim launch (bench timing)
 
     # ------------------------------------------------------------ batched API
     def reset(self):
@@ -163,9 +164,13 @@ class TrafficEnv:
         if actions.dtype != torch.int32 or tuple(actions.shape) != (self.E, self.A):
             raise ValueError(f"actions must be int32 [{self.E},{self.A}]")
         cfg = self.cfg
+        if self.sim_hook:
+            self.sim_hook(True)
         call("dmdqn_sim_step", C.byref(self.csim), C.byref(self.cidm), ptr(actions),
              cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time, ptr(self.halt),
              ptr(self.phase), ptr(self.tspent), ptr(self.done_u8), stream_of(self.device))
+        if self.sim_hook:
+            self.sim_hook(False)
         self.t += cfg.step_duration
         prev = self.local
         self.local, self.obs, reward = K.observe(self.R, self.C, self.halt, self.phase,

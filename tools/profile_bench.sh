@@ -23,6 +23,7 @@ F=$(find $O/pmcF_$TAG -name '*counter_collection.csv' | head -n 1)
 W=$(find $O/pmcW_$TAG -name '*counter_collection.csv' | head -n 1)
 cd $R
 python3 tools/pmc_learn.py "$F" "$W" "$KEY" k_learn
+python3 tools/pmc_learn.py "$F" "$W" "${KEY%_*}_sim" k_sim_step
 cp profiles/learn_pmc.json $O/keep_$TAG/
 cp "$(find $O/prof_$TAG -name '*kernel_stats.csv' | head -n 1)" $O/keep_$TAG/kernel_stats.csv
 gzip -c "$F" > $O/keep_$TAG/fetch_size_counter_collection.csv.gz
