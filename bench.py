@@ -146,6 +146,9 @@ def main():
     ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
                     help="fp16 = the reference's mixed_float16 policy (f16 MFMA operands, "
                          "f32 accumulate, f32 master weights + Adam); fp32 = strict path")
+    ap.add_argument("--shared", action="store_true",
+                    help="C5: one shared network (mean per-agent loss, RCCL gradient "
+                         "all-reduce across ranks); use with --rows 8 --cols 8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--dist-backend", default="nccl",
@@ -173,7 +176,9 @@ def main():
     torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
-    agent_cfg = AgentConfig(precision=args.precision, seed=1000 + rank)
+    # independent nets are seeded per rank; the shared net must start identical on every rank
+    agent_cfg = AgentConfig(precision=args.precision, seed=1000 if args.shared else 1000 + rank,
+                            shared_params=args.shared)
     tr = Trainer(env_cfg, agent_cfg, device=dev)
     E, A = tr.env.E, tr.env.A
     NA = E * A
@@ -226,7 +231,8 @@ def main():
         value = args.steps * NA * world / el_max
         from dmdqn_amd.agent import n_params_keras
         P = n_params_keras(tr.agent.H)  # the reference's 28,548 parameters
-        bpl = NA * learn_bytes_per_agent(P)
+        # independent = NA * (128*721 + 28P); shared (C5) = NA*128*721 + 28P
+        bpl = (NA * 128 * REPLAY_ROW_BYTES + 28 * P) if args.shared else NA * learn_bytes_per_agent(P)
         avg_learn_s = float(np.mean(learn_ms)) / 1e3
         achieved = bpl / avg_learn_s / 1e9
         wl = f"{args.rows}x{args.cols}x{args.envs}"
@@ -236,6 +242,10 @@ def main():
             cv, sample = cpu_baseline(args.rows, args.cols, args.cpu_budget)
             cpu = {"value": round(cv, 2), "unit": "agent-env steps/s", "cores": 1,
                    "kind": "port", "sample": sample}
+        cname = "C5" if args.shared else "C3"
+        learn_desc = ("shared-network Double-DQN learn (mean per-agent loss"
+                      + (", RCCL gradient all-reduce" if world > 1 else "") + ") + one Adam"
+                      if args.shared else "Double-DQN learn + Adam")
         out = {
             "metric": "agent-env steps/sec (whole node), 16-intersection x 1024 envs",
             "value": round(value, 1),
@@ -250,18 +260,21 @@ def main():
             "dtype": ("f32" if args.precision == "fp32" else
                       "f16 (mixed_float16 as the reference: f16 MFMA operands, f32 accumulate, "
                       "f32 master weights + Adam)"),
-            "data": "synthetic (4x4 grid, randomTrips-style demand, Keras-style random init)",
+            "data": f"synthetic ({args.rows}x{args.cols} grid, randomTrips-style demand, "
+                    "Keras-style random init)",
             "config": {
-                "workload": f"C3: {args.rows}x{args.cols} grid ({A} agents) x {args.envs} envs/GPU, "
-                            "full RL step (act, 10 IDM substeps, observe, remember, sample, "
-                            "Double-DQN learn + Adam), H=128, batch 128, replay 10000",
+                "workload": f"{cname}: {args.rows}x{args.cols} grid ({A} agents) x {args.envs} "
+                            "envs/GPU, full RL step (act, 10 IDM substeps, observe, remember, "
+                            f"sample, {learn_desc}), H=128, batch 128, replay 10000",
                 "envs_per_gpu": args.envs, "agents_per_env": A, "global_envs": args.envs * world,
                 "replay_prefill_steps": agent_cfg.batch_size - 1,
-                "parallelism": f"env-shard x{world} (no collectives)",
+                "parallelism": (f"env-shard x{world}" + (" + RCCL all-reduce of the 114 KB "
+                                "gradient" if args.shared and world > 1 else " (no collectives)")),
                 "precision": args.precision,
             },
             "roofline": {
-                "kernel": "k_learn (fused gather + 3x fwd + bwd + Adam, MFMA)",
+                "kernel": ("k_learn_shared_f16 + k_reduce_slabs + k_adam" if args.shared else
+                           "k_learn (fused gather + 3x fwd + bwd + Adam, MFMA)"),
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

@@ -28,6 +28,21 @@ class DmdqnError(RuntimeError):
     pass
 
 
+def register(sigs):
+    """Add entry-point signatures (modules that define the ctypes structs call
+    this); applied at once if the library is already loaded."""
+    SIGNATURES.update(sigs)
+    if _LIB is not None:
+        _apply(_LIB, sigs)
+
+
+def _apply(lib, sigs):
+    for name, args in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+
+
 def load(path=None):
     """Load the HIP library (raises if it is absent: no fallback path)."""
     global _LIB
@@ -41,10 +56,7 @@ def load(path=None):
     lib.dmdqn_last_error.restype = C.c_char_p
     lib.dmdqn_last_error.argtypes = []
     lib.dmdqn_version.restype = C.c_int
-    for name, args in SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.argtypes = args
-        fn.restype = C.c_int
+    _apply(lib, SIGNATURES)
     _LIB = lib
     return lib
 

@@ -39,10 +39,16 @@ class CLearn(C.Structure):
         (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]] + [("stamps", C.c_void_p)]
 
 
-_lib.SIGNATURES.update({
+_lib.register({
     "dmdqn_learn": [C.POINTER(CLearn), C.c_void_p],
     "dmdqn_q_argmax": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                        C.c_void_p],
+    "dmdqn_q_argmax_shared": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                              C.c_void_p, C.c_void_p],
+    "dmdqn_learn_shared_grad": [C.POINTER(CLearn), C.c_void_p, C.c_int, C.c_void_p, C.c_float,
+                                C.c_void_p],
+    "dmdqn_adam": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                   C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_void_p],
 })
 
 PRECISIONS = {"fp32": 0, "fp16": 1}
@@ -148,6 +154,10 @@ class AgentConfig:
     precision: str = "fp32"          # "fp32" | "fp16" (mixed, the reference's policy)
     count_env_steps: bool = False    # True fixes A-1 (epsilon decays); False = reference
     seed: int = 0
+    # C5 (not in the reference): ONE network shared by every agent,
+    # trained on the mean of the per-agent losses; gradients all-reduced over
+    # RCCL across ranks.  Requires precision "fp16" and nn_layers [128, 128].
+    shared_params: bool = False
 
     @classmethod
     def from_dict(cls, d):
@@ -169,24 +179,34 @@ class BatchedDQN:
             raise ValueError("the fused learn kernel is built for batch_size 128")
         if cfg.precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {list(PRECISIONS)}")
+        if cfg.shared_params and (cfg.precision != "fp16" or H != 128):
+            raise ValueError("shared_params needs precision 'fp16' and nn_layers [128, 128]")
         self.device = dev = torch.device(device)
         self.E, self.A = num_envs, n_agents
         self.NA = NA = num_envs * n_agents
+        self.shared = cfg.shared_params
+        self.NW = NW = 1 if self.shared else NA   # parameter sets
         self.H, self.P = H, n_params(H)
         if init_weights is None:
-            init_weights = keras_initial_weights(np.random.RandomState(cfg.seed), H, NA)
-        init = np.asarray(init_weights, dtype=np.float32).reshape(NA, -1)
+            init_weights = keras_initial_weights(np.random.RandomState(cfg.seed), H, NW)
+        init = np.asarray(init_weights, dtype=np.float32).reshape(NW, -1)
         if init.shape[1] == n_params_keras(H):
             init = keras_to_kernel(init, H)
-        w = torch.as_tensor(init.reshape(NA, self.P))
+        w = torch.as_tensor(init.reshape(NW, self.P))
         self.params = w.to(dev).contiguous()
         self.target = self.params.clone()
         # fp16 path: the target forward reads an f16 copy (padded row stride Ph)
         self.Ph = (self.P + 7) // 8 * 8
         self.target_h = None
         if cfg.precision == "fp16":
-            self.target_h = torch.zeros((NA, self.Ph), dtype=torch.float16, device=dev)
+            self.target_h = torch.zeros((NW, self.Ph), dtype=torch.float16, device=dev)
             self._refresh_target_h()
+        if self.shared:
+            # one partial gradient per persistent workgroup (one per CU)
+            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+            self.n_slabs = max(1, min(NA, n_cu))
+            self.slab = torch.empty((self.n_slabs, self.P), dtype=torch.float32, device=dev)
+            self.grad = torch.zeros(self.P, dtype=torch.float32, device=dev)
         self.adam_m = torch.zeros_like(self.params)
         self.adam_v = torch.zeros_like(self.params)
         self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev)
@@ -226,8 +246,9 @@ class BatchedDQN:
         eps = self.current_epsilon()
         greedy = None
         if eps < 1.0:
-            call("dmdqn_q_argmax", ptr(self.params), self.NA, self.P, self.H,
-                 ptr(obs.reshape(self.NA, D_IN)), ptr(self.greedy), None, stream_of(self.device))
+            call("dmdqn_q_argmax_shared" if self.shared else "dmdqn_q_argmax", ptr(self.params),
+                 self.NA, self.P, self.H, ptr(obs.reshape(self.NA, D_IN)), ptr(self.greedy), None,
+                 stream_of(self.device))
             greedy = self.greedy
         return K.act(self.np_state, self.A, eps=eps, n_actions=N_ACTIONS, greedy=greedy,
                      out=self.actions)
@@ -268,13 +289,33 @@ class BatchedDQN:
                                self.target_h, self.loss]],
                    np.float32(cfg.gamma), alpha, c1, c2, eps,
                    None if self.stamps is None else self.stamps.data_ptr())
+        self._last_args = a  # keeps the struct (and what it points at) inspectable
         if self.learn_hook:
             self.learn_hook(True)
-        call("dmdqn_learn", C.byref(a), stream_of(self.device))
+        if self.shared:
+            self._learn_shared(a, alpha, c1, c2, eps, sync)
+        else:
+            call("dmdqn_learn", C.byref(a), stream_of(self.device))
         if self.learn_hook:
             self.learn_hook(False)
         self.learn_launches += 1
         return self.loss
+
+    def _learn_shared(self, a, alpha, c1, c2, eps, sync):
+        """C5: grad = mean over this rank's agents of the per-agent gradients,
+        all-reduced (sum, RCCL) across ranks, then one Adam step with 1/world."""
+        import torch.distributed as dist
+        st = stream_of(self.device)
+        call("dmdqn_learn_shared_grad", C.byref(a), ptr(self.slab), self.n_slabs, ptr(self.grad),
+             C.c_float(1.0 / self.NA), st)
+        world = 1
+        if dist.is_available() and dist.is_initialized():
+            world = dist.get_world_size()
+            if world > 1:
+                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)  # one flat 114 KB buffer
+        call("dmdqn_adam", ptr(self.params), ptr(self.adam_m), ptr(self.adam_v), ptr(self.target),
+             ptr(self.target_h), ptr(self.grad), self.P, C.c_float(1.0 / world), C.c_float(alpha),
+             C.c_float(c1), C.c_float(c2), C.c_float(eps), int(sync), st)
 
     def _refresh_target_h(self):
         if self.target_h is not None:
@@ -291,7 +332,7 @@ class BatchedDQN:
 
     def get_weights(self, agent):
         """Keras get_weights() order for one agent: [W1, b1, W2, b2, W3, b3]."""
-        p = kernel_to_keras(self.params[agent].cpu().numpy(), self.H)
+        p = kernel_to_keras(self.params[0 if self.shared else agent].cpu().numpy(), self.H)
         H = self.H
         shapes = [(D_IN, H), (H,), (H, H), (H,), (H, N_ACTIONS), (N_ACTIONS,)]
         out, o = [], 0
@@ -303,6 +344,7 @@ class BatchedDQN:
 
     def set_weights(self, agent, weights):
         flat = np.concatenate([np.asarray(w, np.float32).reshape(-1) for w in weights])
+        agent = 0 if self.shared else agent
         self.params[agent].copy_(torch.from_numpy(keras_to_kernel(flat, self.H)))
         self.target[agent].copy_(self.params[agent])
         self._refresh_target_h()

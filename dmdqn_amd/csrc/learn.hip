@@ -389,12 +389,12 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
 
 // ------------------------------------------------------------------ greedy act
 template <int H>
-__global__ void __launch_bounds__(256) k_q_argmax(const float *params, int P, const float *obs,
-                                                  int32_t *out, float *q_out) {
+__global__ void __launch_bounds__(256) k_q_argmax(const float *params, size_t pstride,
+                                                  const float *obs, int32_t *out, float *q_out) {
     using L = Lay<H>;
     __shared__ float x[D_], h1[H], h2[H], q[NACT];
     const int agent = blockIdx.x, tid = threadIdx.x;
-    const float *Wp = params + (size_t)agent * P;
+    const float *Wp = params + (size_t)agent * pstride;  // pstride 0: one shared net
     for (int i = tid; i < D_; i += blockDim.x) x[i] = obs[(size_t)agent * D_ + i];
     __syncthreads();
     for (int j = tid; j < H; j += blockDim.x) {
@@ -457,20 +457,30 @@ extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
     return DMDQN_OK;
 }
 
-extern "C" int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, const float *obs,
-                              int32_t *out, float *q_out, void *stream) {
+static int q_argmax(const float *params, size_t pstride, int NA, int P, int hidden,
+                    const float *obs, int32_t *out, float *q_out, void *stream) {
     DMDQN_REQUIRE(params && obs && out && NA > 0, "dmdqn_q_argmax: bad args");
     if (hidden == 128) {
         DMDQN_REQUIRE(P == Lay<128>::P, "dmdqn_q_argmax: P");
-        hipLaunchKernelGGL(k_q_argmax<128>, dim3(NA), dim3(128), 0, as_stream(stream), params, P,
-                           obs, out, q_out);
+        hipLaunchKernelGGL(k_q_argmax<128>, dim3(NA), dim3(128), 0, as_stream(stream), params,
+                           pstride, obs, out, q_out);
     } else if (hidden == 64) {
         DMDQN_REQUIRE(P == Lay<64>::P, "dmdqn_q_argmax: P");
-        hipLaunchKernelGGL(k_q_argmax<64>, dim3(NA), dim3(64), 0, as_stream(stream), params, P,
-                           obs, out, q_out);
+        hipLaunchKernelGGL(k_q_argmax<64>, dim3(NA), dim3(64), 0, as_stream(stream), params,
+                           pstride, obs, out, q_out);
     } else {
         DMDQN_REQUIRE(false, "dmdqn_q_argmax: hidden must be 64 or 128");
     }
     DMDQN_LAUNCH_CHECK("k_q_argmax");
     return DMDQN_OK;
+}
+
+extern "C" int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, const float *obs,
+                              int32_t *out, float *q_out, void *stream) {
+    return q_argmax(params, (size_t)P, NA, P, hidden, obs, out, q_out, stream);
+}
+
+extern "C" int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden,
+                                     const float *obs, int32_t *out, float *q_out, void *stream) {
+    return q_argmax(params, 0, NA, P, hidden, obs, out, q_out, stream);
 }

@@ -38,7 +38,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short v4s __attribute__((vector_size(8)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
-constexpr int B_ = 128, D_ = QN_D, DP = QN_DP, H = 128, NACT = QN_NA;
+constexpr int B_ = 128, DP = QN_DP, H = 128, NACT = QN_NA;
 using L = QL<H>;
 
 // LDS byte offsets
@@ -329,67 +329,46 @@ __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, si
     }
 }
 
-// Diagnostics: block-level phase end time (after a barrier), only when a
-// stamps buffer is passed.  s_memrealtime ticks at 100 MHz.
-#define STAMP(i)                                                              \
-    do {                                                                      \
-        if (a.stamps && threadIdx.x == 0)                                     \
-            a.stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
+// ----------------------------------------------------------------------------
+// Per-agent pieces shared by the independent kernel (k_learn_f16) and the
+// shared-parameter kernel (k_learn_shared_f16).  All are called by every
+// thread of the 512-thread workgroup.
 
-__global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    _Float16 *R1 = (_Float16 *)(smem + R1_OFF), *R2 = (_Float16 *)(smem + R2_OFF);
-    _Float16 *DQ = (_Float16 *)(smem + DQ_OFF);
-    char *sc = smem + SC_OFF;
-    Scratch S{(float *)sc,          (float *)(sc + 2048), (float *)(sc + 2560),
-              (float *)(sc + 3072), (float *)(sc + 3584), (int *)(sc + 4096),
-              (int *)(sc + 4608),   (double *)(sc + 5120), (double *)(sc + 6144)};
-    const int agent = blockIdx.x;
-    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
-    const size_t Pz = (size_t)L::P;
-    float *Wp = a.params + agent * Pz, *Mp = a.adam_m + agent * Pz, *Vp = a.adam_v + agent * Pz;
-    float *Tp = a.target + agent * Pz;
-    const size_t Ph = (Pz + 7) / 8 * 8;
-    _Float16 *TH = a.target_h ? reinterpret_cast<_Float16 *>(a.target_h) + agent * Ph : nullptr;
-    const AdamC AK{a.alpha, a.c1, a.c2, a.eps, a.sync_target != 0, TH};
-    STAMP(0);
-    Frags fr;
-    if (TH) load_frags(TH, fr);  // in flight during the z-score + gather
-    else load_frags(a.target + agent * Pz, fr);
-    _Float16 *W3L = (_Float16 *)(smem + W3_OFF);
-    float *B3L = (float *)(smem + B3_OFF);
-    const OutL on{W3L, B3L}, tg{W3L + NACT * H, B3L + NACT};
-    stage_out(Wp, W3L, B3L);  // synced by the metadata barrier below
-    if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
-    else stage_out(Tp, W3L + NACT * H, B3L + NACT);
+struct Rows { uint2 v[3]; };
 
-    // replay rows (int8) -> X f16 [128][96] in R2, in two halves so the loads
-    // can be in flight across other work: issue (3 x 8 bytes per thread into
-    // registers), then commit (convert + LDS store) once R2 is free.
-    struct Rows { uint2 v[3]; };
-    auto gather_issue = [&](const int8_t *ring, Rows &g) {
+// Replay rows (int8) of one agent's batch -> X f16 [128][96] in R2, in two
+// halves so the loads can be in flight across other work: issue (3 x 8 bytes
+// per thread into registers), then commit (convert + LDS store) once R2 is free.
+__device__ __forceinline__ void gather_issue(const int8_t *ring, const dmdqn_learn_args &a,
+                                             int agent, const int *slot, Rows &g) {
+    const int tid = threadIdx.x;
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
-            const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
-            g.v[i] = reinterpret_cast<const uint2 *>(ring + ((size_t)agent * a.cap + S.slot[b]) * DP)[q];
+    for (int i = 0; i < 3; i++) {
+        const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
+        g.v[i] = reinterpret_cast<const uint2 *>(ring + ((size_t)agent * a.cap + slot[b]) * DP)[q];
+    }
+}
+
+__device__ __forceinline__ void gather_commit(_Float16 *R2, const Rows &g) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
+        half8 hv;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            hv[e] = (_Float16)(float)(int8_t)(g.v[i].x >> (8 * e));
+            hv[e + 4] = (_Float16)(float)(int8_t)(g.v[i].y >> (8 * e));
         }
-    };
-    auto gather_commit = [&](const Rows &g) {
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
-            half8 hv;
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                hv[e] = (_Float16)(float)(int8_t)(g.v[i].x >> (8 * e));
-                hv[e + 4] = (_Float16)(float)(int8_t)(g.v[i].y >> (8 * e));
-            }
-            *reinterpret_cast<half8 *>(R2 + b * DP + 8 * q) = hv;
-        }
-    };
+        *reinterpret_cast<half8 *>(R2 + b * DP + 8 * q) = hv;
+    }
+}
 
-    // ---- batch metadata + reward z-score (numpy pairwise order, f64)
+// Batch metadata (ring slots, actions, dones) and the reward z-score of
+// ReplayBuffer.sample (dqn_agent.py:64-69): f64 mean and population std over
+// the 128 rewards in numpy's pairwise order (8 partial sums of 16), + 1e-8.
+__device__ __forceinline__ void batch_meta(const dmdqn_learn_args &a, int agent, const Scratch &S) {
+    const int tid = threadIdx.x;
     if (tid < B_) {
         int pos = a.idx[(size_t)agent * B_ + tid];
         int s = a.start + pos;
@@ -433,30 +412,14 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();
     if (tid < B_) S.rn[tid] = (float)__ddiv_rn(__dsub_rn(S.r64[tid], S.red[8]), S.red[9]);
-    STAMP(1);
+}
 
-    // ---- target(S') -> z3 ; online(S') -> Q in R1 (free during layer 3) ; y
-    {
-        Rows gn;
-        gather_issue(a.ring_n, gn);
-        gather_commit(gn);
-    }
-    __syncthreads();
-    STAMP(2);
-    // target forward keeps X(S') in R2; the online net's fragments (reused by
-    // both online forwards) load layer by layer as the target's die
-    const float *Wpc = Wp;
-    forward<true>(fr, tg, R1, R2, S.z3, [Wpc](Frags &f) { load_w1(Wpc, f); },
-                  [Wpc](Frags &f) { load_w2(Wpc, f); });
-    STAMP(3);
-    // online(S'): X(S') is dead after layer 1, so the S rows for the training
-    // forward load during layers 1-2 and land in R2 while H2 sits in R1
-    float *qo = (float *)DQ;  // 2 KB; DQ is not needed until after the S forward
-    Rows gs;
-    forward<true>(fr, on, R1, R2, qo, [&](Frags &) { gather_issue(a.ring_s, gs); },
-                  [&](Frags &) { gather_commit(gs); });
-    STAMP(4);
-    STAMP(5);
+// Double-DQN target y = r^ + gamma (1 - d) Q_target(S')[argmax Q_online(S')]
+// (dqn_agent.py:342-347; first max on ties).  qo: online Q(S') [128][4];
+// S.z3: target Q(S').  Ends with a barrier.
+__device__ __forceinline__ void ddqn_target(const dmdqn_learn_args &a, const float *qo,
+                                            const Scratch &S) {
+    const int tid = threadIdx.x;
     if (tid < B_) {
         const float4 q = *reinterpret_cast<const float4 *>(qo + tid * NACT);
         int best = 0;
@@ -469,10 +432,14 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         S.y[tid] = S.rn[tid] + gd * tq;
     }
     __syncthreads();
-    // ---- online(S), activations kept: H1 in R1, H2 in R2 ; q, loss, DQ
-    STAMP(6);
-    forward<false>(fr, on, R1, R2, S.z3);
-    STAMP(7);
+}
+
+// MSE loss (dqn_agent.py:350-352) of Q_online(S) in S.z3 at the taken actions,
+// written to a.loss[agent]; dL/dQ (2 (q - y) / B, f16) into DQ [128][16] and
+// S.dq.  Ends with a barrier.
+__device__ __forceinline__ void loss_dq(const dmdqn_learn_args &a, int agent, _Float16 *DQ,
+                                        const Scratch &S) {
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];
@@ -493,6 +460,148 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();
     if (tid == 0 && a.loss) a.loss[agent] = (float)(S.red[10] + S.red[11]) / (float)B_;
+}
+
+// dZ2 = dq * W3[:, a] masked by ReLU(H2), in place over H2 in R2 (8 columns
+// per task); `on` holds the pre-update W3.  Ends with a barrier.
+__device__ __forceinline__ void bwd_dz2(_Float16 *R2, const OutL on, const Scratch &S) {
+    for (int t = threadIdx.x; t < B_ * (H / 8); t += 512) {
+        const int b = t >> 4, k8 = (t & 15) * 8, ac = S.act[b];
+        half8 *p = reinterpret_cast<half8 *>(R2 + b * H + k8);
+        half8 h = *p, o;
+        const half8 wv = *reinterpret_cast<const half8 *>(on.w3 + ac * H + k8);
+        const float dq = S.dq[b];
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+            o[e] = (float)h[e] > 0.0f ? (_Float16)(dq * (float)wv[e]) : (_Float16)0.0f;
+        *p = o;
+    }
+    __syncthreads();
+}
+
+// ReLU mask of H1 (R1) as bits: mask[b][j/32] (128 x 4 words).
+__device__ __forceinline__ void h1_mask(const _Float16 *R1, uint32_t *mask) {
+    const int tid = threadIdx.x, b = tid >> 2, q = tid & 3;
+    const half8 *hp = reinterpret_cast<const half8 *>(R1 + b * H + 32 * q);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const half8 hv = hp[c];
+#pragma unroll
+        for (int e = 0; e < 8; e++) bits |= ((float)hv[e] > 0.0f ? 1u : 0u) << (8 * c + e);
+    }
+    mask[b * 4 + q] = bits;
+}
+
+// dH1^T[j][b] = W2[j][k] . dZ2^T.  The caller has synced after the last use of
+// H1; the W2^T f16 image [k][j] goes into R1 from the wave-owned forward
+// fragments (the exact f16 operand of the forward), and the A operand is its
+// transposed read.  Ends with a barrier (image and dZ2 consumed).
+__device__ __forceinline__ void bwd_dh1(_Float16 *R1, const _Float16 *R2, const Frags &fr,
+                                        f32x4 d1[8]) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++)
+        *reinterpret_cast<half8 *>(R1 + (16 * w + lr) * H + 32 * s2 + 8 * lg) = fr.w2[s2];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 8; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) {
+        const half8 av = frag_tr(R1, H, 32 * s2, 16 * w);
+#pragma unroll
+        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(R2, H, 16 * t, 32 * s2), d1[t]);
+    }
+    __syncthreads();
+}
+
+// dZ1 = dH1 masked by ReLU(H1) -> R1 (lane: neurons j..j+3 of row b).
+__device__ __forceinline__ void bwd_dz1(_Float16 *R1, const uint32_t *mask, const f32x4 d1[8]) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
+    const int j = 16 * w + 4 * lg;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const int b = 16 * t + lr;
+        const uint32_t bits = (mask[b * 4 + (j >> 5)] >> (j & 31)) & 0xfu;
+        half4v o;
+#pragma unroll
+        for (int e = 0; e < 4; e++) o[e] = ((bits >> e) & 1u) ? (_Float16)d1[t][e] : (_Float16)0.0f;
+        *reinterpret_cast<half4v *>(R1 + b * H + j) = o;
+    }
+}
+
+#define LEARN_SMEM_SETUP                                                                        \
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];                              \
+    _Float16 *R1 = (_Float16 *)(smem + R1_OFF), *R2 = (_Float16 *)(smem + R2_OFF);             \
+    _Float16 *DQ = (_Float16 *)(smem + DQ_OFF);                                                \
+    char *sc = smem + SC_OFF;                                                                  \
+    Scratch S{(float *)sc,          (float *)(sc + 2048), (float *)(sc + 2560),                \
+              (float *)(sc + 3072), (float *)(sc + 3584), (int *)(sc + 4096),                  \
+              (int *)(sc + 4608),   (double *)(sc + 5120), (double *)(sc + 6144)};             \
+    _Float16 *W3L = (_Float16 *)(smem + W3_OFF);                                               \
+    float *B3L = (float *)(smem + B3_OFF);                                                     \
+    const OutL on{W3L, B3L}, tg{W3L + NACT * H, B3L + NACT};                                   \
+    uint32_t *mask = reinterpret_cast<uint32_t *>(DQ)
+
+// Diagnostics: block-level phase end time (after a barrier), only when a
+// stamps buffer is passed.  s_memrealtime ticks at 100 MHz.
+#define STAMP(i)                                                              \
+    do {                                                                      \
+        if (a.stamps && threadIdx.x == 0)                                     \
+            a.stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+// ----------------------------------------------------------------------------
+// Independent agents: one workgroup per agent, Adam fused on the gradient tiles.
+__global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
+    LEARN_SMEM_SETUP;
+    const int agent = blockIdx.x;
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
+    const size_t Pz = (size_t)L::P;
+    float *Wp = a.params + agent * Pz, *Mp = a.adam_m + agent * Pz, *Vp = a.adam_v + agent * Pz;
+    float *Tp = a.target + agent * Pz;
+    const size_t Ph = (Pz + 7) / 8 * 8;
+    _Float16 *TH = a.target_h ? reinterpret_cast<_Float16 *>(a.target_h) + agent * Ph : nullptr;
+    const AdamC AK{a.alpha, a.c1, a.c2, a.eps, a.sync_target != 0, TH};
+    STAMP(0);
+    Frags fr;
+    if (TH) load_frags(TH, fr);  // in flight during the z-score + gather
+    else load_frags(a.target + agent * Pz, fr);
+    stage_out(Wp, W3L, B3L);  // synced by the metadata barrier below
+    if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
+    else stage_out(Tp, W3L + NACT * H, B3L + NACT);
+
+    batch_meta(a, agent, S);
+    STAMP(1);
+
+    // ---- target(S') -> z3 ; online(S') -> Q ; y
+    {
+        Rows gn;
+        gather_issue(a.ring_n, a, agent, S.slot, gn);
+        gather_commit(R2, gn);
+    }
+    __syncthreads();
+    STAMP(2);
+    // target forward keeps X(S') in R2; the online net's fragments (reused by
+    // both online forwards) load layer by layer as the target's die
+    const float *Wpc = Wp;
+    forward<true>(fr, tg, R1, R2, S.z3, [Wpc](Frags &f) { load_w1(Wpc, f); },
+                  [Wpc](Frags &f) { load_w2(Wpc, f); });
+    STAMP(3);
+    // online(S'): X(S') is dead after layer 1, so the S rows for the training
+    // forward load during layers 1-2 and land in R2 while H2 sits in R1
+    float *qo = (float *)DQ;  // 2 KB; DQ is not needed until after the S forward
+    Rows gs;
+    forward<true>(fr, on, R1, R2, qo, [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); },
+                  [&](Frags &) { gather_commit(R2, gs); });
+    STAMP(4);
+    STAMP(5);
+    ddqn_target(a, qo, S);
+    // ---- online(S), activations kept: H1 in R1, H2 in R2 ; q, loss, DQ
+    STAMP(6);
+    forward<false>(fr, on, R1, R2, S.z3);
+    STAMP(7);
+    loss_dq(a, agent, DQ, S);
 
     const half8 ones = ones8();
     // ---- dW3[k][a] = H2^T . DQ (wave w: k-tile w) ; db3 (wave 0)
@@ -512,34 +621,9 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();  // dW3 read H2; dZ2 overwrites it
     STAMP(8);
-    // ---- dZ2 = dq * W3[:, a] (ReLU mask), in place over H2 (8 columns per task)
-    for (int t = tid; t < B_ * (H / 8); t += 512) {
-        const int b = t >> 4, k8 = (t & 15) * 8, ac = S.act[b];
-        half8 *p = reinterpret_cast<half8 *>(R2 + b * H + k8);
-        half8 h = *p, o;
-        const half8 wv = *reinterpret_cast<const half8 *>(on.w3 + ac * H + k8);  // pre-update W3
-        const float dq = S.dq[b];
-#pragma unroll
-        for (int e = 0; e < 8; e++)
-            o[e] = (float)h[e] > 0.0f ? (_Float16)(dq * (float)wv[e]) : (_Float16)0.0f;
-        *p = o;
-    }
-    __syncthreads();
+    bwd_dz2(R2, on, S);
     STAMP(9);
-    // ---- ReLU mask of H1 as bits (the DQ region is free now): mask[b][j/32]
-    uint32_t *mask = reinterpret_cast<uint32_t *>(DQ);
-    {
-        const int b = tid >> 2, q = tid & 3;
-        const half8 *hp = reinterpret_cast<const half8 *>(R1 + b * H + 32 * q);
-        uint32_t bits = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const half8 hv = hp[c];
-#pragma unroll
-            for (int e = 0; e < 8; e++) bits |= ((float)hv[e] > 0.0f ? 1u : 0u) << (8 * c + e);
-        }
-        mask[b * 4 + q] = bits;
-    }
+    h1_mask(R1, mask);  // the DQ region is free now
     // ---- dW2[j][k] = H1^T . dZ2 (wave w: j-tile w, 8 k-tiles) ; db2 (k-tile w) ; Adam
     {
         f32x4 g2[8], gb = {0.f, 0.f, 0.f, 0.f};
@@ -564,42 +648,15 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob2 + 16 * w + lr, gb[0], AK);
     }
     __syncthreads();  // H1 fully consumed (dW2, mask): R1 becomes the W2^T image
-
-    // ---- W2^T f16 image [k][j] in R1 from the wave-owned forward fragments
-#pragma unroll
-    for (int s2 = 0; s2 < 4; s2++)
-        *reinterpret_cast<half8 *>(R1 + (16 * w + lr) * H + 32 * s2 + 8 * lg) = fr.w2[s2];
-    __syncthreads();
-    // ---- dH1^T[j][b] = W2[j][k] . dZ2^T  (A: transposed read of the W2^T image)
     f32x4 d1[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s2 = 0; s2 < 4; s2++) {
-        const half8 av = frag_tr(R1, H, 32 * s2, 16 * w);
-#pragma unroll
-        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(R2, H, 16 * t, 32 * s2), d1[t]);
-    }
-    __syncthreads();  // image and dZ2 consumed
+    bwd_dh1(R1, R2, fr, d1);
     {
         Rows gx;  // X(S) again for dW1 (R2 is free)
-        gather_issue(a.ring_s, gx);
-        gather_commit(gx);
+        gather_issue(a.ring_s, a, agent, S.slot, gx);
+        gather_commit(R2, gx);
     }
     STAMP(10);
-    // dZ1 = dH1 masked by ReLU(H1) -> R1 (lane: neurons j..j+3 of row b)
-    {
-        const int j = 16 * w + 4 * lg;
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int b = 16 * t + lr;
-            const uint32_t bits = (mask[b * 4 + (j >> 5)] >> (j & 31)) & 0xfu;
-            half4v o;
-#pragma unroll
-            for (int e = 0; e < 4; e++) o[e] = ((bits >> e) & 1u) ? (_Float16)d1[t][e] : (_Float16)0.0f;
-            *reinterpret_cast<half4v *>(R1 + b * H + j) = o;
-        }
-    }
+    bwd_dz1(R1, mask, d1);
     __syncthreads();
     STAMP(11);
     // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
@@ -631,7 +688,159 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
 }
 
+// ----------------------------------------------------------------------------
+// Shared-parameter DQN (not in the reference): ONE online /
+// target network for every agent.  Persistent workgroups (one per CU, 256
+// VGPRs) hold both networks' fragments in registers for the whole launch and
+// loop over agents; each agent's batch runs the same forward/backward as the
+// independent kernel, and its gradient tiles accumulate straight into MFMA
+// accumulators that live across the agent loop.  Each workgroup then writes
+// its partial sum (kernel layout, P floats) to slab[blockIdx.x].  No Adam
+// here: k_reduce_slabs + (RCCL all-reduce across ranks) + k_adam follow.
+__global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a, float *slab) {
+    LEARN_SMEM_SETUP;
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
+    const float *Wp = a.params;
+    const _Float16 *TH = a.target_h ? reinterpret_cast<const _Float16 *>(a.target_h) : nullptr;
+    Frags fr;
+    stage_out(Wp, W3L, B3L);
+    if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
+    else stage_out(a.target, W3L + NACT * H, B3L + NACT);
+    const half8 ones = ones8();
+    // dW2 accumulators (64 KB f32) live in LDS -- one workgroup per CU leaves
+    // room -- laid out [wave][tile][lane] so each access is one contiguous
+    // 1 KB wave row; the rest stay in registers.
+    __shared__ f32x4 G2L[8 * 8 * 64];
+    f32x4 G3 = {0.f, 0.f, 0.f, 0.f}, GB3 = G3, GB2 = G3, GB1 = G3, G1[6];
+#pragma unroll
+    for (int t = 0; t < 8; t++) G2L[(w * 8 + t) * 64 + l] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 6; t++) G1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int agent = blockIdx.x; agent < a.NA; agent += gridDim.x) {
+        // the shared nets are L2-resident: reload the fragments per agent (as
+        // the independent kernel does from HBM) rather than pin 72 VGPRs
+        if (TH) load_frags(TH, fr);
+        else load_frags(a.target, fr);
+        batch_meta(a, agent, S);
+        {
+            Rows gn;
+            gather_issue(a.ring_n, a, agent, S.slot, gn);
+            gather_commit(R2, gn);
+        }
+        __syncthreads();
+        forward<true>(fr, tg, R1, R2, S.z3, [Wp](Frags &f) { load_w1(Wp, f); },
+                      [Wp](Frags &f) { load_w2(Wp, f); });  // X(S') stays in R2
+        float *qo = (float *)DQ;
+        Rows gs;
+        forward<true>(fr, on, R1, R2, qo, [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); },
+                      [&](Frags &) { gather_commit(R2, gs); });
+        ddqn_target(a, qo, S);
+        forward<false>(fr, on, R1, R2, S.z3);
+        loss_dq(a, agent, DQ, S);
+        // dW3 / db3
+#pragma unroll
+        for (int b0 = 0; b0 < B_; b0 += 32) {
+            const half8 dqf = frag_tr(DQ, 16, b0, 0);
+            G3 = mfma(frag_tr(R2, H, b0, 16 * w), dqf, G3);
+            GB3 = mfma(ones, dqf, GB3);
+        }
+        __syncthreads();
+        bwd_dz2(R2, on, S);
+        h1_mask(R1, mask);
+        // dW2 / db2 (tile by tile, accumulating into the LDS accumulators)
+        {
+            half8 av[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                av[q] = frag_tr(R1, H, 32 * q, 16 * w);
+                GB2 = mfma(ones, frag_tr(R2, H, 32 * q, 16 * w), GB2);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                f32x4 c = G2L[(w * 8 + t) * 64 + l];
+#pragma unroll
+                for (int q = 0; q < 4; q++) c = mfma(av[q], frag_tr(R2, H, 32 * q, 16 * t), c);
+                G2L[(w * 8 + t) * 64 + l] = c;
+            }
+        }
+        __syncthreads();
+        f32x4 d1[8];
+        bwd_dh1(R1, R2, fr, d1);
+        {
+            Rows gx;
+            gather_issue(a.ring_s, a, agent, S.slot, gx);
+            gather_commit(R2, gx);
+        }
+        bwd_dz1(R1, mask, d1);
+        __syncthreads();
+        // dW1 / db1
+#pragma unroll
+        for (int b0 = 0; b0 < B_; b0 += 32) {
+            const half8 bv = frag_tr(R1, H, b0, 16 * w);
+            GB1 = mfma(ones, bv, GB1);
+#pragma unroll
+            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr(R2, DP, b0, 16 * t), bv, G1[t]);
+        }
+        __syncthreads();  // R1 / R2 / scratch are rewritten by the next agent
+    }
+    // partial sums of this workgroup, kernel layout (every index written once)
+    float *G = slab + (size_t)blockIdx.x * L::P;
+    if (lr < NACT) {
+        *reinterpret_cast<float4 *>(G + L::oW3T + lr * H + 16 * w + 4 * lg) =
+            make_float4(G3[0], G3[1], G3[2], G3[3]);
+        if (w == 0 && lg == 0) G[L::ob3 + lr] = GB3[0];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const f32x4 c = G2L[(w * 8 + t) * 64 + l];
+        *reinterpret_cast<float4 *>(G + L::oW2T + (16 * t + lr) * H + 16 * w + 4 * lg) =
+            make_float4(c[0], c[1], c[2], c[3]);
+    }
+    if (lg == 0) G[L::ob2 + 16 * w + lr] = GB2[0];
+#pragma unroll
+    for (int t = 0; t < 6; t++)
+        *reinterpret_cast<float4 *>(G + L::oW1T + (16 * w + lr) * DP + 16 * t + 4 * lg) =
+            make_float4(G1[t][0], G1[t][1], G1[t][2], G1[t][3]);
+    if (lg == 0) G[L::ob1 + 16 * w + lr] = GB1[0];
+}
+
+// grad[i] = scale * sum_w slab[w][i]  (fixed order over workgroups)
+__global__ void __launch_bounds__(256) k_reduce_slabs(const float *slab, int nw, float scale,
+                                                      float *grad) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= L::P / 4) return;
+    float4 acc = reinterpret_cast<const float4 *>(slab)[i];
+    for (int k = 1; k < nw; k++) {
+        const float4 v = reinterpret_cast<const float4 *>(slab + (size_t)k * L::P)[i];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
+    reinterpret_cast<float4 *>(grad)[i] = acc;
+}
+
 }  // namespace f16k
+
+// Keras-3 Adam over n flat parameters (A-11) with g = gscale * grad; on a
+// target sync also writes the target copy and its f16 shadow.
+__global__ void __launch_bounds__(256) k_adam(float *W, float *M, float *V, float *T,
+                                              _Float16 *TH, const float *G, int n, float gscale,
+                                              float alpha, float c1, float c2, float eps, int sync) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float g = G[i] * gscale;
+    float m = M[i], v = V[i], w = W[i];
+    m = m + (g - m) * c1;
+    v = v + (g * g - v) * c2;
+    w = w - (m * alpha) / (sqrtf(v) + eps);
+    M[i] = m;
+    V[i] = v;
+    W[i] = w;
+    if (sync) {
+        T[i] = w;
+        if (TH) TH[i] = (_Float16)w;
+    }
+}
 
 int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s) {
     DMDQN_REQUIRE(a->hidden == 128 && a->P == f16k::L::P,
@@ -642,3 +851,39 @@ int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s) {
 }
 
 }  // namespace dmdqn
+
+using namespace dmdqn;
+
+extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, int n_slabs,
+                                       float *grad, float scale, void *stream) {
+    DMDQN_REQUIRE(a && slab && grad, "dmdqn_learn_shared_grad: null argument");
+    DMDQN_REQUIRE(a->NA > 0 && a->cap >= a->batch && a->start >= 0 && a->start < a->cap,
+                  "dmdqn_learn_shared_grad: NA=%d cap=%d start=%d", a->NA, a->cap, a->start);
+    DMDQN_REQUIRE(a->batch == f16k::B_, "dmdqn_learn_shared_grad: batch must be %d", f16k::B_);
+    DMDQN_REQUIRE(a->precision == 1 && a->hidden == 128 && a->P == f16k::L::P,
+                  "dmdqn_learn_shared_grad: fp16 precision with hidden=128 (P=%d) only",
+                  f16k::L::P);
+    DMDQN_REQUIRE(a->ring_s && a->ring_n && a->ring_a && a->ring_d && a->ring_r && a->idx &&
+                      a->params && a->target,
+                  "dmdqn_learn_shared_grad: null array");
+    DMDQN_REQUIRE(n_slabs >= 1, "dmdqn_learn_shared_grad: n_slabs must be >= 1");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(f16k::k_learn_shared_f16, dim3(n_slabs), dim3(512), 0, s, *a, slab);
+    DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
+    hipLaunchKernelGGL(f16k::k_reduce_slabs, dim3((f16k::L::P / 4 + 255) / 256), dim3(256), 0, s,
+                       slab, n_slabs, scale, grad);
+    DMDQN_LAUNCH_CHECK("k_reduce_slabs");
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_adam(float *params, float *adam_m, float *adam_v, float *target,
+                          uint16_t *target_h, const float *grad, int n, float gscale, float alpha,
+                          float c1, float c2, float eps, int sync, void *stream) {
+    DMDQN_REQUIRE(params && adam_m && adam_v && grad && n > 0, "dmdqn_adam: bad args");
+    DMDQN_REQUIRE(!sync || target, "dmdqn_adam: target required on a sync");
+    hipLaunchKernelGGL(k_adam, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), params,
+                       adam_m, adam_v, target, reinterpret_cast<_Float16 *>(target_h), grad, n,
+                       gscale, alpha, c1, c2, eps, sync);
+    DMDQN_LAUNCH_CHECK("k_adam");
+    return DMDQN_OK;
+}

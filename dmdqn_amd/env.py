@@ -86,7 +86,7 @@ class CIdm(C.Structure):
                                          "two_sqrt_ab", "halt_speed", "len_inner", "len_outer"]]
 
 
-_lib.SIGNATURES.update({
+_lib.register({
     "dmdqn_sim_reset": [C.POINTER(CSim), C.c_void_p],
     "dmdqn_sim_step": [C.POINTER(CSim), C.POINTER(CIdm), C.c_void_p, C.c_int, C.c_int, C.c_int,
                        C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],

@@ -188,6 +188,34 @@ int dmdqn_learn(const dmdqn_learn_args *args, void *stream);
 int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, const float *obs,
                    int32_t *out, float *q_out, void *stream);
 
+/* dmdqn_q_argmax with ONE parameter set shared by all NA agents (C5). */
+int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, const float *obs,
+                          int32_t *out, float *q_out, void *stream);
+
+/* ------------------------------------------------------------------ shared-parameter DQN
+ * Configuration C5 (NOT in the reference, which trains one network
+ * per junction): ONE online / target network for all agents of all envs (and
+ * all ranks).  Every agent keeps its own replay ring and draws its own batch
+ * indices exactly as in the independent configuration; its batch runs the same
+ * Double-DQN forward/backward as dmdqn_learn, and the gradients are summed:
+ *     grad[P] = scale * sum_agents dL_agent / dtheta     (device layout, f32)
+ * With scale = 1 / (agents on all ranks) and an all-reduce(sum) of grad across
+ * ranks in between, the following dmdqn_adam step is the Adam step of the mean
+ * per-agent loss, identical on every rank.
+ * args: params / target / target_h point at ONE network ([P], [Ph]); adam_m /
+ * adam_v are not used here; loss [NA] receives each agent's loss.
+ * slab: f32 [n_slabs][P] scratch, one partial sum per persistent workgroup
+ * (one workgroup per CU: n_slabs = 256 on MI355X).  precision must be 1. */
+int dmdqn_learn_shared_grad(const dmdqn_learn_args *args, float *slab, int n_slabs, float *grad,
+                            float scale, void *stream);
+
+/* Keras-3 Adam (dqn_agent.py:357, A-11) on n flat parameters with gradient
+ * gscale * grad[i]; sync != 0 also copies params to target (and its f16 shadow
+ * target_h, when not NULL) -- the hard target sync of dqn_agent.py:376-387. */
+int dmdqn_adam(float *params, float *adam_m, float *adam_v, float *target, uint16_t *target_h,
+               const float *grad, int n, float gscale, float alpha, float c1, float c2, float eps,
+               int sync, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

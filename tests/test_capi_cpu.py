@@ -37,7 +37,7 @@ def test_all_declared_symbols_exported(lib):
 
 
 def test_python_signatures_cover_header(lib):
-    from dmdqn_amd import _lib
+    from dmdqn_amd import _lib, agent, env  # noqa: F401  (agent / env register theirs)
     declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version"}
     assert declared <= set(_lib.SIGNATURES), sorted(declared - set(_lib.SIGNATURES))
 
