@@ -56,3 +56,56 @@ def test_single_process_defaults():
     assert torch.equal(D.allreduce_mean_(t), torch.ones(3))
     off, seeds = D.shard(3, 4, 10)
     assert off == 12 and list(seeds) == [22, 23, 24, 25]
+
+
+def _shared_worker(rank, ws, port, q):
+    """C5 orchestration across ranks with the kernels stubbed (CPU): the
+    gradient each rank hands to Adam is the SUM over ranks of the per-rank
+    (already 1/NA-scaled) gradients, with gscale = 1/world."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    from types import SimpleNamespace
+
+    import dmdqn_amd.agent as AG
+    from dmdqn_amd import dist as D
+    D.init(backend="gloo")
+    P = 8
+    fake = SimpleNamespace(NA=4, n_slabs=2, P=P, device="cpu",
+                           slab=torch.zeros((2, P)), grad=torch.zeros(P),
+                           params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
+                           target=torch.zeros(P), target_h=None)
+    seen = {}
+
+    def fake_call(name, *args):
+        if name == "dmdqn_learn_shared_grad":
+            fake.grad.copy_(torch.arange(P, dtype=torch.float32) * (rank + 1))
+            seen["scale"] = args[4].value
+        elif name == "dmdqn_adam":
+            seen["grad"] = fake.grad.tolist()
+            seen["gscale"] = args[7].value
+            seen["sync"] = args[12]
+        return 0
+
+    AG.call, AG.stream_of = fake_call, (lambda *a: None)
+    AG.BatchedDQN._learn_shared(fake, AG.CLearn(), 1e-3, 0.1, 1e-3, 1e-7, True)
+    q.put((rank, seen))
+    dist.destroy_process_group()
+
+
+def test_shared_param_gradient_allreduce_two_ranks():
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shared_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(ws))
+    for p in ps:
+        p.join(timeout=60)
+    expect = (np.arange(8) * (1 + 2)).tolist()        # rank 0 (x1) + rank 1 (x2)
+    for _, seen in res:
+        assert np.isclose(seen["scale"], 1 / 4)        # 1 / local agents
+        assert np.allclose(seen["grad"], expect)       # identical on every rank
+        assert np.isclose(seen["gscale"], 1 / ws)      # mean over ranks in Adam
+        assert seen["sync"] == 1
