@@ -67,6 +67,11 @@ class EnvConfig:
     end_ms: int = 2_500_000      # last departure (trips_p06.trips.xml:7-9)
     period_ms: Optional[int] = None
     idm: IDMParams = field(default_factory=IDMParams)
+    # a real scenario instead of synthetic demand: a .sumocfg (net + routes, as
+    # the reference's src/sumo_files/scenarios/grid_3x3.sumocfg) or the .npz
+    # sumo_scenario.Scenario.save writes (config/scenarios/grid_3x3_p06.npz).
+    # Sets rows / cols / departures (identical in every replica) / lane lengths.
+    scenario: Optional[str] = None
 
     @property
     def n_agents(self):
@@ -102,11 +107,21 @@ class TrafficEnv:
             raise ValueError(f"signal_features must be one of {list(SIGNAL_MODES)}")
         _lib.load()
         self.device = torch.device(device)
+        self.scenario = None
+        if cfg.scenario:
+            from .sumo_scenario import load_scenario, scenario_tables
+            sc = self.scenario = load_scenario(cfg.scenario)
+            cfg.rows, cfg.cols = sc.rows, sc.cols
+            cfg.idm.len_inner, cfg.idm.len_outer = sc.lane_len_inner, sc.lane_len_outer
         self.grid = g = Grid(cfg.rows, cfg.cols)
         self.R, self.C, self.A, self.E = cfg.rows, cfg.cols, g.A, cfg.num_envs
         E, A, NL, cap = self.E, self.A, g.NL, cfg.cap_lane
         self.seeds = np.arange(cfg.num_envs, dtype=np.int64) + cfg.seed + cfg.env_offset
-        q_ids, q_off, vdst, nveh, period = demand_tables(g, self.seeds, cfg.end_ms, cfg.period_ms)
+        if self.scenario is not None:
+            q_ids, q_off, vdst, nveh, period = scenario_tables(self.scenario, E)
+        else:
+            q_ids, q_off, vdst, nveh, period = demand_tables(g, self.seeds, cfg.end_ms,
+                                                             cfg.period_ms)
         self.nveh, self.period_ms = nveh, period
         dev = self.device
         z32 = lambda *s: torch.zeros(s, dtype=torch.int32, device=dev)  # noqa: E731

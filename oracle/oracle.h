@@ -46,6 +46,8 @@ typedef struct orc_env orc_env;
 orc_env *orc_env_create(int R, int C, int cap, uint64_t seed, long end_ms, int period_ms,
                         const orc_idm *P);
 void orc_env_free(orc_env *g);
+void orc_env_set_demand(orc_env *g, int nveh, int period_ms, const uint16_t *q_ids,
+                        const int32_t *q_off, const uint16_t *vdst);
 void orc_env_reset(orc_env *g);
 void orc_env_step(orc_env *g, const int32_t *actions, int stride, int t0, int K, int max_time,
                   int32_t *halt, int32_t *phase, int32_t *tspent, uint8_t *done);

@@ -176,6 +176,7 @@ def _declare_env(L):
     L.orc_env_info.argtypes = [C.c_void_p, _i32]
     L.orc_env_lanes.argtypes = [C.c_void_p, _f32, _f32, _i32, _i32, _i32]
     L.orc_env_demand.argtypes = [C.c_void_p, _u16, _i32, _u16]
+    L.orc_env_set_demand.argtypes = [C.c_void_p, C.c_int, C.c_int, _u16, _i32, _u16]
 
 
 class OracleEnv:
@@ -225,6 +226,14 @@ class OracleEnv:
         hd, cn = np.zeros(self.NL, np.int32), np.zeros(self.NL, np.int32)
         lib().orc_env_lanes(self.h, x, v, d, hd, cn)
         return x.reshape(self.NL, self.cap), v.reshape(self.NL, self.cap), d.reshape(self.NL, self.cap), hd, cn
+
+    def set_demand(self, q_ids, q_off, vdst, period_ms):
+        """Explicit departures (a loaded SUMO scenario); resets the replica."""
+        q = np.ascontiguousarray(q_ids, np.uint16)
+        lib().orc_env_set_demand(self.h, len(q), int(period_ms), q,
+                                 np.ascontiguousarray(q_off, np.int32),
+                                 np.ascontiguousarray(vdst, np.uint16))
+        self.nveh = len(q)
 
     def demand(self):
         q = np.zeros(self.nveh, np.uint16)

@@ -238,6 +238,23 @@ orc_env *orc_env_create(int R, int C, int cap, uint64_t seed, long end_ms, int p
     return g;
 }
 
+/* Replace the generated demand with explicit tables (a loaded SUMO scenario,
+ * dmdqn_amd/sumo_scenario.py): vehicle i departs at i * period_ms from origin
+ * queue q (ids q_ids[q_off[q] .. q_off[q+1])) toward edge vdst[i]. Resets. */
+void orc_env_set_demand(orc_env *g, int nveh, int period_ms, const uint16_t *q_ids,
+                        const int32_t *q_off, const uint16_t *vdst) {
+    free(g->q_ids); free(g->vdst); free(g->q_off);
+    g->nveh = nveh;
+    g->period_ms = period_ms;
+    g->q_ids = (uint16_t *)malloc(sizeof(uint16_t) * (size_t)(nveh > 0 ? nveh : 1));
+    g->vdst = (uint16_t *)malloc(sizeof(uint16_t) * (size_t)(nveh > 0 ? nveh : 1));
+    g->q_off = (int *)malloc(sizeof(int) * (size_t)(4 * g->A + 1));
+    memcpy(g->q_ids, q_ids, sizeof(uint16_t) * (size_t)nveh);
+    memcpy(g->vdst, vdst, sizeof(uint16_t) * (size_t)nveh);
+    for (int i = 0; i <= 4 * g->A; i++) g->q_off[i] = q_off[i];
+    orc_env_reset(g);
+}
+
 void orc_env_free(orc_env *g) {
     if (!g) return;
     free(g->x); free(g->v); free(g->dst); free(g->head); free(g->cnt); free(g->req);

@@ -68,6 +68,12 @@ class SmoothedValue:  # train.py:144-156
         return self.value
 
 
+# SUMO_CFG_PATH of the reference (train.py:50: grid_3x3.sumocfg), derived into the
+# simulator's tables by tests/golden/make_scenario.py
+DEFAULT_SCENARIO = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "config", "scenarios", "grid_3x3_p06.npz")
+
+
 def calculate_local_reward(current_state, next_state):  # train.py:159-160
     return -1.0 * sum(current_state[:12])
 
@@ -76,10 +82,10 @@ def calculate_global_reward(global_state: dict, next_global_state: dict):  # tra
     return -1.0 * sum(sum(state[:12]) for state in global_state.values())
 
 
-def initialize_environment(rows=3, cols=3, seed=0, signal_features="reference"):
+def initialize_environment(rows=3, cols=3, seed=0, signal_features="reference", scenario=None):
     env = TrafficEnv(EnvConfig(rows=rows, cols=cols, num_envs=1, seed=seed,
                                step_duration=int(STEP_DURATION), max_sim_time=MAX_SIM_TIME,
-                               signal_features=signal_features))
+                               signal_features=signal_features, scenario=scenario))
     return env, env.get_controlled_intersection_ids()
 
 
@@ -87,11 +93,11 @@ def create_agents(tl_junctions, config=AGENT_CONFIG):
     return {j: DQNAgent(state_size=89, action_size=4, agent_id=j, config=config) for j in tl_junctions}
 
 
-def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None):
+def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None, scenario=None):
     dqn_agent.seed(seed)
-    env, tl_junctions = initialize_environment(rows, cols, seed)
+    env, tl_junctions = initialize_environment(rows, cols, seed, scenario=scenario)
     agents = create_agents(tl_junctions)
-    assert len(agents) == rows * cols
+    assert len(agents) == env.R * env.C
     smooth_total = SmoothedValue(alpha=0.3)
     out = open(metrics, "w") if metrics else None
     for episode in range(episodes):
@@ -119,12 +125,13 @@ def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None):
     return agents
 
 
-def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None):
+def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None, scenario=None,
+                  shared=False):
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.trainer import Trainer
     cfg = AgentConfig.from_dict(AGENT_CONFIG)
-    cfg.precision, cfg.seed = precision, seed
-    tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=seed), cfg)
+    cfg.precision, cfg.seed, cfg.shared_params = precision, seed, shared
+    tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=seed, scenario=scenario), cfg)
     out = open(metrics, "w") if metrics else None
     t0 = time.perf_counter()
     steps = 0
@@ -153,13 +160,25 @@ def main():
     ap.add_argument("--envs", type=int, default=1024)
     ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"])
     ap.add_argument("--metrics", default=None, help="offline JSONL metrics (replaces wandb)")
+    ap.add_argument("--scenario", default=None,
+                    help="SUMO scenario: a .sumocfg or a .npz from sumo_scenario (default for the "
+                         "single-env path: the reference's grid_3x3 + grid_3x3_p06 routes, as "
+                         "train.py's SUMO_CONFIG); 'synthetic' = generated demand for --grid")
+    ap.add_argument("--shared", action="store_true",
+                    help="batched only: one network shared by all agents (C5)")
     args = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
     rows, cols = (int(x) for x in args.grid.split("x"))
+    scenario = args.scenario
+    if scenario is None and not args.batched:
+        scenario = DEFAULT_SCENARIO
+    if scenario == "synthetic":
+        scenario = None
     if args.batched:
-        train_batched(args.episodes, rows, cols, args.envs, args.precision, args.seed, args.metrics)
+        train_batched(args.episodes, rows, cols, args.envs, args.precision, args.seed, args.metrics,
+                      scenario, args.shared)
     else:
-        train_agents(args.episodes, rows, cols, args.seed, args.metrics)
+        train_agents(args.episodes, rows, cols, args.seed, args.metrics, scenario)
 
 
 if __name__ == "__main__":

@@ -10,11 +10,19 @@ import oracle as O  # noqa: E402
 from dmdqn_amd.env import EnvConfig, TrafficEnv  # noqa: E402
 
 
-def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_at=()):
-    cfg = EnvConfig(rows=R, cols=C, num_envs=E, seed=seed, signal_features=mode)
+def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_at=(),
+         scenario=None):
+    cfg = EnvConfig(rows=R, cols=C, num_envs=E, seed=seed, signal_features=mode,
+                    scenario=scenario)
     env = TrafficEnv(cfg)
+    R, C = env.R, env.C
     obs = env.reset()
     refs = [O.OracleEnv(R, C, seed + e) for e in range(E)]
+    if scenario is not None:
+        from dmdqn_amd.sumo_scenario import scenario_tables
+        q, off, vd, _, period = scenario_tables(env.scenario, 1)
+        for r in refs:
+            r.set_demand(q[0], off[0], vd[0], period)
     m = 1 if mode == "intended" else 0
     A = R * C
     prev_local = [O.local_state(np.zeros((A, 12)), np.zeros(A), np.zeros(A), m) for _ in range(E)]
@@ -92,3 +100,16 @@ def test_dict_api_single_replica():
     nobs, rew, done, info = env.step_dict({j: 1 for j in obs})
     assert set(rew) == set(obs) and not done and info["simulation_time"] == 10.0
     assert env.get_state_size() == 89 and env.get_action_size() == 4
+
+
+def test_sim_shipped_3x3_scenario_matches_oracle():
+    """The reference's own scenario (grid_3x3.net.xml + grid_3x3_p06.rou.xml,
+    4167 routed vehicles, derived by tests/golden/make_scenario.py) through
+    the HIP sim: a full 240-step episode, bit-exact vs the oracle."""
+    from conftest import GOLDEN
+    import os
+    env = _run(0, 0, E=3, steps=240, check_every=10, full_state_at=(100, 200),
+               scenario=os.path.join(GOLDEN, "grid_3x3_p06_scenario.npz"))
+    st = env.stats()  # inserted, arrived, running, pending
+    assert (st[:, 0] > 3900).all() and (st[:, 1] > 3500).all()
+    assert (st[:, 0] + st[:, 3] == 4167).all()
