@@ -241,9 +241,10 @@ class BatchedDQN:
             self.epsilon = max(0.01, 1.0 * float(np.exp(-(g - 8000) / 16000)))
         return self.epsilon
 
-    def act(self, obs):
-        """obs f32 [E, A, 89] -> actions int32 [E, A] (device)."""
-        eps = self.current_epsilon()
+    def act(self, obs, eps=None):
+        """obs f32 [E, A, 89] -> actions int32 [E, A] (device).  eps overrides the
+        schedule (evaluation, test.py:84-87)."""
+        eps = self.current_epsilon() if eps is None else float(eps)
         greedy = None
         if eps < 1.0:
             call("dmdqn_q_argmax_shared" if self.shared else "dmdqn_q_argmax", ptr(self.params),

@@ -93,7 +93,8 @@ def create_agents(tl_junctions, config=AGENT_CONFIG):
     return {j: DQNAgent(state_size=89, action_size=4, agent_id=j, config=config) for j in tl_junctions}
 
 
-def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None, scenario=None):
+def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None, scenario=None,
+                 save_dir=None):
     dqn_agent.seed(seed)
     env, tl_junctions = initialize_environment(rows, cols, seed, scenario=scenario)
     agents = create_agents(tl_junctions)
@@ -122,16 +123,23 @@ def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None, scenar
         logger.info(f"Episode {episode + 1} complete. Total Reward: {total_reward}")
     if out:
         out.close()
+    if save_dir:  # additive: the reference never saves (test.py:195 expects this naming)
+        os.makedirs(save_dir, exist_ok=True)
+        for j in tl_junctions:
+            agents[j].save_model(os.path.join(save_dir, f"agent_{j}.weights.npz"))
     return agents
 
 
 def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None, scenario=None,
-                  shared=False):
+                  shared=False, save_dir=None, resume=None):
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.trainer import Trainer
     cfg = AgentConfig.from_dict(AGENT_CONFIG)
     cfg.precision, cfg.seed, cfg.shared_params = precision, seed, shared
     tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=seed, scenario=scenario), cfg)
+    from dmdqn_amd import checkpoint as CK
+    if resume:
+        CK.load(resume, tr)
     out = open(metrics, "w") if metrics else None
     t0 = time.perf_counter()
     steps = 0
@@ -148,6 +156,10 @@ def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None, sce
                       "agent_env_steps_per_s": round(steps * tr.env.E * tr.env.A / el, 1)}))
     if out:
         out.close()
+    if save_dir:
+        os.makedirs(save_dir, exist_ok=True)
+        CK.save(os.path.join(save_dir, "checkpoint.pt"), tr)
+        CK.export_keras_weights(tr.agent, save_dir, tr.env.grid.junction_ids, env_index=0)
     return tr
 
 
@@ -166,6 +178,9 @@ def main():
                          "train.py's SUMO_CONFIG); 'synthetic' = generated demand for --grid")
     ap.add_argument("--shared", action="store_true",
                     help="batched only: one network shared by all agents (C5)")
+    ap.add_argument("--save_dir", default=None,
+                    help="write agent_<id>.weights.npz (and, batched, checkpoint.pt) at the end")
+    ap.add_argument("--resume", default=None, help="batched only: a checkpoint.pt to resume from")
     args = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
     rows, cols = (int(x) for x in args.grid.split("x"))
@@ -176,9 +191,9 @@ def main():
         scenario = None
     if args.batched:
         train_batched(args.episodes, rows, cols, args.envs, args.precision, args.seed, args.metrics,
-                      scenario, args.shared)
+                      scenario, args.shared, args.save_dir, args.resume)
     else:
-        train_agents(args.episodes, rows, cols, args.seed, args.metrics, scenario)
+        train_agents(args.episodes, rows, cols, args.seed, args.metrics, scenario, args.save_dir)
 
 
 if __name__ == "__main__":
