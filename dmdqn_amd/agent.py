@@ -36,7 +36,8 @@ class CLearn(C.Structure):
         (n, C.c_void_p) for n in ["ring_s", "ring_n", "ring_a", "ring_d", "ring_r", "idx",
                                   "params", "adam_m", "adam_v", "target", "target_h",
                                   "loss"]] + [
-        (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]] + [("stamps", C.c_void_p)]
+        (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]] + [
+        ("stamps", C.c_void_p), ("qstats", C.c_void_p)]
 
 
 _lib.register({
@@ -221,6 +222,7 @@ class BatchedDQN:
             self.py_state = K.seed_streams(seeds, "py", dev)
         self.idx = torch.empty((NA, cfg.batch_size), dtype=torch.int32, device=dev)
         self.loss = torch.zeros(NA, dtype=torch.float32, device=dev)
+        self.qstats = torch.zeros((NA, 6), dtype=torch.float32, device=dev)
         self.actions = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
         self.greedy = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
         self.global_step_count = 0
@@ -273,7 +275,10 @@ class BatchedDQN:
         or None while the buffers hold fewer than batch_size transitions."""
         return self.learn()
 
-    def learn(self):
+    def learn(self, collect_stats=False):
+        """One fused learn for every agent (None while underfilled).  With
+        collect_stats, self.qstats [NA, 6] receives the batch metrics of
+        dqn_agent.py:361-363 (see learn_metrics)."""
         n = len(self.ring)
         if n < self.cfg.batch_size:
             return None
@@ -289,7 +294,8 @@ class BatchedDQN:
                                self.idx, self.params, self.adam_m, self.adam_v, self.target,
                                self.target_h, self.loss]],
                    np.float32(cfg.gamma), alpha, c1, c2, eps,
-                   None if self.stamps is None else self.stamps.data_ptr())
+                   None if self.stamps is None else self.stamps.data_ptr(),
+                   self.qstats.zero_().data_ptr() if collect_stats else None)
         self._last_args = a  # keeps the struct (and what it points at) inspectable
         if self.learn_hook:
             self.learn_hook(True)
@@ -301,6 +307,19 @@ class BatchedDQN:
             self.learn_hook(False)
         self.learn_launches += 1
         return self.loss
+
+    def learn_metrics(self):
+        """The scalars dqn_agent.py:361-370 logs, from the last learn(collect_stats=True):
+        mean over agents of q_values_mean / q_values_std (population std over
+        each batch's 128x4 online Q values), the action histogram summed over
+        agents, mean loss and epsilon.  Syncs."""
+        qs = self.qstats.double()
+        n = float(self.cfg.batch_size * N_ACTIONS)
+        mean = qs[:, 0] / n
+        std = (qs[:, 1] / n - mean * mean).clamp_min(0).sqrt()
+        return {"loss": float(self.loss.double().mean()), "epsilon": float(self.epsilon),
+                "q_values_mean": float(mean.mean()), "q_values_std": float(std.mean()),
+                "action_distribution": qs[:, 2:6].sum(0).round().long().tolist()}
 
     def _learn_shared(self, a, alpha, c1, c2, eps, sync):
         """C5: grad = mean over this rank's agents of the per-agent gradients,

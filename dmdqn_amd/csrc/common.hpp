@@ -135,4 +135,32 @@ struct MTWave {
     }
 };
 
+// Learn metrics of dqn_agent.py:361-363 for one agent's batch: sum and sum of
+// squares of the online Q(S) values [128][4] (q_values_mean / _std) and the
+// histogram of the batch actions (action_distribution), added into
+// qstats[agent][6].  Called by every thread after Q(S) is in z3; waves 0-1
+// (batch rows 0..127) contribute, no barrier inside.
+__device__ inline void learn_qstats(float *qstats, int agent, const float *z3, const int *act) {
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    if (w >= 2) return;
+    const float4 q = *reinterpret_cast<const float4 *>(z3 + tid * 4);
+    float s1 = (q.x + q.y) + (q.z + q.w);
+    float s2 = (q.x * q.x + q.y * q.y) + (q.z * q.z + q.w * q.w);
+    for (int off = 32; off > 0; off >>= 1) {
+        s1 += __shfl_xor(s1, off);
+        s2 += __shfl_xor(s2, off);
+    }
+    const int ac = act[tid];
+    float cnt[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cnt[k] = (float)__popcll(__ballot(ac == k));
+    if (l == 0) {
+        float *o = qstats + (size_t)agent * 6;
+        atomicAdd(o + 0, s1);
+        atomicAdd(o + 1, s2);
+#pragma unroll
+        for (int k = 0; k < 4; k++) atomicAdd(o + 2 + k, cnt[k]);
+    }
+}
+
 }  // namespace dmdqn

@@ -240,6 +240,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     // ---- P4/P5: gather S, online forward keeping H1, H2; q, loss, dq
     gather(a.ring_s);
     forward<H>(Wp, X, H1, H2, S.z3);
+    if (a.qstats) learn_qstats(a.qstats, agent, S.z3, S.act);
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];

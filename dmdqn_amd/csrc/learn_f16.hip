@@ -440,6 +440,7 @@ __device__ __forceinline__ void ddqn_target(const dmdqn_learn_args &a, const flo
 __device__ __forceinline__ void loss_dq(const dmdqn_learn_args &a, int agent, _Float16 *DQ,
                                         const Scratch &S) {
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    if (a.qstats) learn_qstats(a.qstats, agent, S.z3, S.act);
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];

@@ -31,12 +31,14 @@ class Trainer:
         self.last_loss = None
         self.last_reward = None
 
-    def step(self):
+    def step(self, collect_stats=False):
+        """One loop iteration for every replica; collect_stats makes the learn
+        also produce the metrics of dqn_agent.py:361-370 (agent.learn_metrics)."""
         env, agent = self.env, self.agent
         actions = agent.act(self.obs)                          # train.py:211-222
         next_obs, reward, done, info = env.step(actions)       # train.py:225-270
         agent.remember(self.obs, actions, reward, next_obs, done)  # train.py:274-282
-        loss = agent.replay()
+        loss = agent.learn(collect_stats=collect_stats)
         self.last_loss, self.last_reward = loss, reward
         self.step_count += 1
         self.total_steps += 1

@@ -179,6 +179,10 @@ typedef struct dmdqn_learn_args {
                                         c1 = 1-b1, c2 = 1-b2 (float32)       */
     uint64_t *stamps;                /* diagnostics: NULL, or [NA][16] phase
                                         end times (s_memrealtime, 100 MHz)   */
+    float *qstats;                   /* metrics: NULL, or [NA][6] += sum Q(S),
+                                        sum Q(S)^2 over the batch's 128x4
+                                        online values, counts of actions 0..3
+                                        (dqn_agent.py:361-363); zero it first */
 } dmdqn_learn_args;
 
 int dmdqn_learn(const dmdqn_learn_args *args, void *stream);

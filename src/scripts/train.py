@@ -131,7 +131,12 @@ def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None, scenar
 
 
 def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None, scenario=None,
-                  shared=False, save_dir=None, resume=None):
+                  shared=False, save_dir=None, resume=None, log_every=20):
+    """E env replicas of the loop on the GPU.  The optional JSONL carries the
+    reference's learn scalars (dqn_agent.py:361-370: loss, epsilon,
+    q_values_mean / _std, action_distribution) and its per-step rewards with
+    EMA smoothing (train.py:295-307, SmoothedValue alpha 0.3), averaged over
+    replicas, every `log_every` steps (each record syncs)."""
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.trainer import Trainer
     cfg = AgentConfig.from_dict(AGENT_CONFIG)
@@ -141,15 +146,26 @@ def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None, sce
     if resume:
         CK.load(resume, tr)
     out = open(metrics, "w") if metrics else None
+    smooth_global, smooth_total = SmoothedValue(alpha=0.3), SmoothedValue(alpha=0.3)
     t0 = time.perf_counter()
     steps = 0
     while tr.episode < episodes:
-        st = tr.step()
+        log = out is not None and steps % log_every == 0
+        if log:  # global reward of the PRE-step state (train.py:241, A-3)
+            glob = -tr.env.local[..., :12].sum(dim=(1, 2), dtype=torch.float64)
+        st = tr.step(collect_stats=log)
         steps += 1
-        if out and (st.done or steps % 20 == 0):
-            loss = None if tr.last_loss is None else float(tr.last_loss.mean().item())
-            out.write(json.dumps({"episode": tr.episode, "step": steps, "mean_loss": loss,
-                                  "mean_reward": float(tr.last_reward.mean().item())}) + "\n")
+        if log:
+            total = tr.last_reward.sum(dim=1)                  # train.py:255 per replica
+            g, tt = float(glob.mean()), float(total.mean())
+            smooth_global.update(g)
+            smooth_total.update(tt)
+            rec = {"episode": tr.episode, "step": steps, "global_reward": g, "total_reward": tt,
+                   "smooth_global_reward": smooth_global.get_value(),
+                   "smooth_total_reward": smooth_total.get_value()}
+            if st.loss_launched:
+                rec.update(tr.agent.learn_metrics())
+            out.write(json.dumps(rec) + "\n")
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     print(json.dumps({"agent_env_steps": steps * tr.env.E * tr.env.A, "seconds": round(el, 3),
@@ -181,6 +197,7 @@ def main():
     ap.add_argument("--save_dir", default=None,
                     help="write agent_<id>.weights.npz (and, batched, checkpoint.pt) at the end")
     ap.add_argument("--resume", default=None, help="batched only: a checkpoint.pt to resume from")
+    ap.add_argument("--log_every", type=int, default=20, help="batched metrics interval (steps)")
     args = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
     rows, cols = (int(x) for x in args.grid.split("x"))
@@ -191,7 +208,7 @@ def main():
         scenario = None
     if args.batched:
         train_batched(args.episodes, rows, cols, args.envs, args.precision, args.seed, args.metrics,
-                      scenario, args.shared, args.save_dir, args.resume)
+                      scenario, args.shared, args.save_dir, args.resume, args.log_every)
     else:
         train_agents(args.episodes, rows, cols, args.seed, args.metrics, scenario, args.save_dir)
 

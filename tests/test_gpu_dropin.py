@@ -50,3 +50,42 @@ def test_train_loop_one_episode(tmp_path):
 def test_graft_smoke():
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+@pytest.mark.parametrize("precision,rtol", [("fp32", 1e-4), ("fp16", 2e-2)])
+def test_learn_metrics_match_host(precision, rtol):
+    """qstats (dqn_agent.py:361-363) vs the host: action histogram exact, Q
+    moments of the online net on the sampled S within the precision's tolerance."""
+    import oracle as O
+    from dmdqn_amd.agent import AgentConfig, BatchedDQN
+    from test_gpu_learn import _fill, _host_batch
+    ag = BatchedDQN(2, 3, AgentConfig(replay_buffer_size=300, seed=2, precision=precision))
+    _fill(ag, 150, np.random.RandomState(3))
+    p0 = ag.keras_params("params").copy()
+    ag.learn(collect_stats=True)
+    qs = ag.qstats.cpu().numpy()
+    idx = ag.idx.cpu().numpy()
+    for j in range(ag.NA):
+        S, Aa, _, _, _ = _host_batch(ag, j, idx[j])
+        q = O.qnet_forward(p0[j], S)
+        np.testing.assert_array_equal(qs[j, 2:], np.bincount(Aa, minlength=4))
+        np.testing.assert_allclose(qs[j, 0], q.sum(), rtol=rtol, atol=rtol * np.abs(q).sum())
+        np.testing.assert_allclose(qs[j, 1], (q * q).sum(), rtol=5 * rtol)
+    m = ag.learn_metrics()
+    assert sum(m["action_distribution"]) == ag.NA * 128 and m["epsilon"] == 1.0
+
+
+def test_train_batched_metrics_and_save(tmp_path):
+    import json
+    from src.scripts import train
+    mfile, sdir = tmp_path / "m.jsonl", tmp_path / "save"
+    tr = train.train_batched(1, 2, 2, 8, "fp16", 1, metrics=str(mfile), save_dir=str(sdir),
+                             log_every=20)
+    recs = [json.loads(x) for x in mfile.read_text().strip().splitlines()]
+    assert len(recs) == 12 and recs[0]["step"] == 1
+    learned = [r for r in recs if "q_values_mean" in r]
+    assert len(learned) == 5                                  # 0-based steps 140, 160, ..., 220
+    assert all(sum(r["action_distribution"]) == 8 * 4 * 128 for r in learned)
+    assert all(r["global_reward"] <= 0 for r in recs)
+    assert (sdir / "checkpoint.pt").exists() and (sdir / "agent_J_1_1.weights.npz").exists()
+    assert tr.episode == 1
