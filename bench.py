@@ -45,68 +45,25 @@ MFMA_F16_DENSE_TFLOPS = 2500.0  # MI355X dense F16/BF16 MFMA peak (MI355X_MICROA
 SIM_BYTES_PER_VEH_SUBSTEP = 20  # read x, v, lane cursor (12 B) + write x, v (8 B)
 
 
-def cpu_baseline(rows, cols, budget_s=15.0, max_steps=200, seed=0):
-    """The C oracle (oracle/, a restatement of the reference semantics) running
-    the same loop for ONE env of the same grid, 1 thread, learn active.
-    Returns (agent-env steps/s, sample description)."""
+def cpu_baseline(rows, cols, steps=60, seed=0):
+    """The reference loop body on the GPU box's host cores: oracle/oracle_loop.c
+    (the C restatement the parity tests pin -- act, sim, observe, reward,
+    remember, CPython sample, z-score, Double-DQN learn with Keras Adam) for env
+    replicas of the same grid, learn active after a 127-step untimed fill.
+    Runs 1 thread x 1 replica and T threads x T replicas (OpenMP over replicas,
+    T = OMP_NUM_THREADS capped by the CPU count).  Returns the cpu_baseline dict
+    (value = the T-thread throughput)."""
     import oracle as O
     A = rows * cols
-    env = O.OracleEnv(rows, cols, seed)
-    nps, pys = O.np_stream(seed), O.py_stream(seed)
-    rng = np.random.RandomState(seed)
-    P = O.qnet_nparams()
-    params = [O.keras_init(rng) for _ in range(A)]
-    target = [p.copy() for p in params]
-    m = [np.zeros(P, np.float32) for _ in range(A)]
-    v = [np.zeros(P, np.float32) for _ in range(A)]
-    cap, B = 10000, 128
-    S = np.zeros((A, cap, 89), np.float32)
-    S2 = np.zeros((A, cap, 89), np.float32)
-    Aa = np.zeros((A, cap), np.int32)
-    Rr = np.zeros((A, cap), np.float64)
-    Dd = np.zeros((A, cap), np.float32)
-    L = O.local_state(np.zeros((A, 12)), np.zeros(A), np.zeros(A), 0)
-    obs = O.build_obs(rows, cols, L)
-    t, n, learn_steps = 0, 0, 0
-
-    def one_step(learn):
-        nonlocal t, n, L, obs, learn_steps
-        acts = O.act(nps, A, 1.0)
-        halt, ph, ts, done = env.step(acts, 3, t, 10, 2400)
-        t += 10
-        L2 = O.local_state(halt, ph, ts, 0)
-        obs2 = O.build_obs(rows, cols, L2)
-        rew = O.reward(L)
-        slot = n % cap
-        S[:, slot], S2[:, slot], Aa[:, slot], Rr[:, slot], Dd[:, slot] = obs, obs2, acts, rew, done
-        n += 1
-        size = min(n, cap)
-        if learn and size >= B:
-            learn_steps += 1
-            start = 0 if n <= cap else n % cap
-            for j in range(A):
-                idx = (start + O.py_sample(pys, size, B)) % cap
-                O.learn(params[j], target[j], m[j], v[j], S[j, idx], Aa[j, idx],
-                        O.zscore(Rr[j, idx]), S2[j, idx], Dd[j, idx], learn_steps)
-            if learn_steps % 500 == 0:
-                for j in range(A):
-                    target[j][:] = params[j]
-        L, obs = L2, obs2
-        if done:
-            env.reset()
-            t = 0
-
-    for _ in range(B - 1):  # replay fill, untimed (learn inactive, as in the reference)
-        one_step(False)
-    steps = 0
-    t0 = time.perf_counter()
-    while steps < max_steps and (time.perf_counter() - t0) < budget_s:
-        one_step(True)
-        steps += 1
-    el = time.perf_counter() - t0
-    sample = (f"1 env x {A} agents ({rows}x{cols}), {steps} RL steps with learn active after a "
-              f"{B - 1}-step untimed replay fill; C oracle (oracle/), 1 thread, {el:.1f} s")
-    return steps * A / el, sample
+    el1, n1 = O.train_loop(rows, cols, 1, 127, steps, seed, 1)
+    T = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    elT, nT = O.train_loop(rows, cols, T, 127, steps, seed, T)
+    return {"value": round(nT / elT, 2), "unit": "agent-env steps/s", "cores": T, "kind": "port",
+            "single_thread_value": round(n1 / el1, 2),
+            "sample": (f"{rows}x{cols} grid ({A} agents): {T} replicas x {steps} RL steps on "
+                       f"{T} threads ({elT:.1f} s) and 1 replica x {steps} steps on 1 thread "
+                       f"({el1:.1f} s), learn active after a 127-step untimed fill; "
+                       "oracle/oracle_loop.c (C restatement, OpenMP over replicas)")}
 
 
 def read_traffic(workload_key):
@@ -150,7 +107,8 @@ def main():
                     help="C5: one shared network (mean per-agent loss, RCCL gradient "
                          "all-reduce across ranks); use with --rows 8 --cols 8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-steps", type=int, default=60,
+                    help="timed RL steps per replica of the CPU baseline")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo; only barrier + timing use it")
     args = ap.parse_args()
@@ -239,9 +197,7 @@ def main():
         traffic = read_traffic(f"{wl}_{args.precision}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cv, sample = cpu_baseline(args.rows, args.cols, args.cpu_budget)
-            cpu = {"value": round(cv, 2), "unit": "agent-env steps/s", "cores": 1,
-                   "kind": "port", "sample": sample}
+            cpu = cpu_baseline(args.rows, args.cols, args.cpu_steps)
         cname = "C5" if args.shared else "C3"
         learn_desc = ("shared-network Double-DQN learn (mean per-agent loss"
                       + (", RCCL gradient all-reduce" if world > 1 else "") + ") + one Adam"

@@ -63,6 +63,10 @@ float orc_learn(float *p, const float *target, float *m, float *v, int H1, int H
                 int B, const float *S, const int32_t *A, const float *Rn, const float *S2,
                 const float *Dn, const float *hyper, float *grad_out);
 
+/* ---- the whole training loop, OpenMP over replicas (oracle_loop.c; bench CPU baseline) ---- */
+double orc_train_loop(int R, int C, int E, int fill, int steps, uint64_t seed, int threads,
+                      long *agent_steps);
+
 #ifdef __cplusplus
 }
 #endif

@@ -313,3 +313,18 @@ def keras_init(rng, H1=128, H2=128, NA=4):
     parts = [he(89, H1), np.zeros(H1), he(H1, H2), np.zeros(H2),
              rng.uniform(-lim, lim, size=(H2, NA)), np.zeros(NA)]
     return np.concatenate([x.reshape(-1) for x in parts]).astype(np.float32)
+
+
+# ---------------------------------------------------------------- CPU baseline loop
+def train_loop(R, Cc, E, fill, steps, seed=0, threads=1):
+    """The training loop body for E replicas in C (oracle_loop.c), OpenMP over
+    replicas.  Returns (timed seconds, agent-env steps timed)."""
+    L = lib()
+    if not hasattr(L, "_loop_declared"):
+        L.orc_train_loop.restype = C.c_double
+        L.orc_train_loop.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                     C.c_int, C.POINTER(C.c_long)]
+        L._loop_declared = True
+    n = C.c_long(0)
+    el = L.orc_train_loop(R, Cc, E, fill, steps, seed, threads, C.byref(n))
+    return el, n.value

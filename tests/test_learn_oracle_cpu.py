@@ -88,3 +88,11 @@ def test_keras_adam_constants():
     # t=1: alpha = lr*sqrt(1-b2)/(1-b1) = 1e-3*sqrt(1e-3)/0.1
     np.testing.assert_allclose(alpha, 1e-3 * np.sqrt(1e-3) / 0.1, rtol=1e-4)
     assert c1 == np.float32(0.1) and c2 == np.float32(0.001) and eps == np.float32(1e-7)
+
+
+def test_cpu_baseline_loop_runs_multithreaded():
+    """oracle_loop.c (bench's CPU baseline): the full loop body over replicas
+    with OpenMP; learn is active in every timed step (fill 127)."""
+    import oracle as O
+    el, n = O.train_loop(2, 2, 3, 127, 2, 0, 3)
+    assert el > 0 and n == 3 * 2 * 4
