@@ -437,10 +437,11 @@ __device__ __forceinline__ void ddqn_target(const dmdqn_learn_args &a, const flo
 // MSE loss (dqn_agent.py:350-352) of Q_online(S) in S.z3 at the taken actions,
 // written to a.loss[agent]; dL/dQ (2 (q - y) / B, f16) into DQ [128][16] and
 // S.dq.  Ends with a barrier.
+template <bool QSTATS>
 __device__ __forceinline__ void loss_dq(const dmdqn_learn_args &a, int agent, _Float16 *DQ,
                                         const Scratch &S) {
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-    if (a.qstats) learn_qstats(a.qstats, agent, S.z3, S.act);
+    if (QSTATS) learn_qstats(a.qstats, agent, S.z3, S.act);
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];
@@ -554,6 +555,7 @@ __device__ __forceinline__ void bwd_dz1(_Float16 *R1, const uint32_t *mask, cons
 
 // ----------------------------------------------------------------------------
 // Independent agents: one workgroup per agent, Adam fused on the gradient tiles.
+template <bool QSTATS>  // QSTATS: also emit the learn metrics (a.qstats != NULL)
 __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     LEARN_SMEM_SETUP;
     const int agent = blockIdx.x;
@@ -602,7 +604,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     STAMP(6);
     forward<false>(fr, on, R1, R2, S.z3);
     STAMP(7);
-    loss_dq(a, agent, DQ, S);
+    loss_dq<QSTATS>(a, agent, DQ, S);
 
     const half8 ones = ones8();
     // ---- dW3[k][a] = H2^T . DQ (wave w: k-tile w) ; db3 (wave 0)
@@ -698,6 +700,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
 // accumulators that live across the agent loop.  Each workgroup then writes
 // its partial sum (kernel layout, P floats) to slab[blockIdx.x].  No Adam
 // here: k_reduce_slabs + (RCCL all-reduce across ranks) + k_adam follow.
+template <bool QSTATS>
 __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a, float *slab) {
     LEARN_SMEM_SETUP;
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
@@ -738,7 +741,7 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
                       [&](Frags &) { gather_commit(R2, gs); });
         ddqn_target(a, qo, S);
         forward<false>(fr, on, R1, R2, S.z3);
-        loss_dq(a, agent, DQ, S);
+        loss_dq<QSTATS>(a, agent, DQ, S);
         // dW3 / db3
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
@@ -846,7 +849,10 @@ __global__ void __launch_bounds__(256) k_adam(float *W, float *M, float *V, floa
 int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s) {
     DMDQN_REQUIRE(a->hidden == 128 && a->P == f16k::L::P,
                   "dmdqn_learn: precision 1 (fp16) needs hidden=128 (P=%d)", f16k::L::P);
-    hipLaunchKernelGGL(f16k::k_learn_f16, dim3(a->NA), dim3(512), 0, s, *a);
+    if (a->qstats)
+        hipLaunchKernelGGL(f16k::k_learn_f16<true>, dim3(a->NA), dim3(512), 0, s, *a);
+    else
+        hipLaunchKernelGGL(f16k::k_learn_f16<false>, dim3(a->NA), dim3(512), 0, s, *a);
     DMDQN_LAUNCH_CHECK("k_learn_f16");
     return DMDQN_OK;
 }
@@ -869,7 +875,11 @@ extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, i
                   "dmdqn_learn_shared_grad: null array");
     DMDQN_REQUIRE(n_slabs >= 1, "dmdqn_learn_shared_grad: n_slabs must be >= 1");
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(f16k::k_learn_shared_f16, dim3(n_slabs), dim3(512), 0, s, *a, slab);
+    if (a->qstats)
+        hipLaunchKernelGGL(f16k::k_learn_shared_f16<true>, dim3(n_slabs), dim3(512), 0, s, *a, slab);
+    else
+        hipLaunchKernelGGL(f16k::k_learn_shared_f16<false>, dim3(n_slabs), dim3(512), 0, s, *a,
+                           slab);
     DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
     hipLaunchKernelGGL(f16k::k_reduce_slabs, dim3((f16k::L::P / 4 + 255) / 256), dim3(256), 0, s,
                        slab, n_slabs, scale, grad);
