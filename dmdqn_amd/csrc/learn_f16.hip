@@ -499,6 +499,27 @@ __device__ __forceinline__ void h1_mask(const _Float16 *R1, uint32_t *mask) {
 // H1; the W2^T f16 image [k][j] goes into R1 from the wave-owned forward
 // fragments (the exact f16 operand of the forward), and the A operand is its
 // transposed read.  Ends with a barrier (image and dZ2 consumed).
+__device__ __forceinline__ void w2t_image(_Float16 *R1, const Frags &fr) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++)
+        *reinterpret_cast<half8 *>(R1 + (16 * w + lr) * H + 32 * s2 + 8 * lg) = fr.w2[s2];
+}
+
+__device__ __forceinline__ void bwd_dh1_from_image(const _Float16 *R1, const _Float16 *R2,
+                                                   f32x4 d1[8]) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < 8; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) {
+        const half8 av = frag_tr(R1, H, 32 * s2, 16 * w);
+#pragma unroll
+        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(R2, H, 16 * t, 32 * s2), d1[t]);
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ void bwd_dh1(_Float16 *R1, const _Float16 *R2, const Frags &fr,
                                         f32x4 d1[8]) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
@@ -639,8 +660,11 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
 #pragma unroll
             for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr(R2, H, b0, 16 * t), g2[t]);
         }
-        // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3].  The
-        // old W2 that dH1 needs is the f16 copy already held in fr.w2.
+        // H1 fully consumed (dW2, mask): R1 becomes the W2^T image now, from
+        // the register copy of old W2 (fr.w2), which is then dead during Adam
+        __syncthreads();
+        w2t_image(R1, fr);
+        // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3]
 #pragma unroll
         for (int h = 0; h < 4; h++) {
             size_t ix[2];
@@ -650,9 +674,9 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         }
         if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob2 + 16 * w + lr, gb[0], AK);
     }
-    __syncthreads();  // H1 fully consumed (dW2, mask): R1 becomes the W2^T image
+    __syncthreads();  // W2^T image complete
     f32x4 d1[8];
-    bwd_dh1(R1, R2, fr, d1);
+    bwd_dh1_from_image(R1, R2, d1);
     {
         Rows gx;  // X(S) again for dW1 (R2 is free)
         gather_issue(a.ring_s, a, agent, S.slot, gx);
