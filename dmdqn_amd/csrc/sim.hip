@@ -41,7 +41,7 @@ struct EnvView {
     float *fx, *fv;
     int32_t *phase, *ts, *qptr, *stats;
     const int32_t *q_off;
-    const uint16_t *q_ids, *vdst;
+    const uint16_t *q_ids, *vdst, *q_dst;
 
     __device__ EnvView(const dmdqn_sim &s, int env) : S(s), e(env) {
         A = s.R * s.C;
@@ -64,14 +64,39 @@ struct EnvView {
         q_off = s.q_off + (size_t)env * (4 * A + 1);
         q_ids = s.q_ids + (size_t)env * s.nveh;
         vdst = s.vdst + (size_t)env * s.nveh;
+        q_dst = s.q_dst + (size_t)env * s.nveh;
         stats = s.stats + (size_t)env * 4;
     }
 };
 
 // ---------------------------------------------------------------- substep
-__device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
+// Next vehicle of an origin queue: queue position p -> (id, destination).
+struct QNext {
+    int id, dst;
+};
+constexpr int QSLOTS = 2;  // queues per thread: 4A <= 2 * blockDim (grids up to 128 junctions)
+
+__device__ __forceinline__ QNext next_vehicle(const EnvView &V, int p) {
+    return QNext{(int)V.q_ids[p], (int)V.q_dst[p]};
+}
+
+#ifdef DMDQN_SIM_PROFILE  // diagnostic build: per-pass ticks of thread 0 -> halt[env][0][0..7]
+#define SIM_PROF(i)                                                          \
+    do {                                                                     \
+        if (threadIdx.x == 0) {                                              \
+            const uint64_t _n = __builtin_amdgcn_s_memrealtime();           \
+            prof[i] += _n - prof_t;                                          \
+            prof_t = _n;                                                     \
+        }                                                                    \
+    } while (0)
+#else
+#define SIM_PROF(i) do { } while (0)
+#endif
+
+__device__ __forceinline__ void substep(EnvView &V, const Topo &T, const IdmK &P, int t,
+                                        QNext qn[QSLOTS], uint64_t *prof, uint64_t &prof_t) {
     const dmdqn_sim &S = V.S;
-    const int R = S.R, C = S.C, A = V.A, NL = V.NL, cap = V.cap;
+    const int A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
 
     // ---- TL: natural phase advance (fixed durations)
@@ -83,6 +108,7 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
         }
     }
     __syncthreads();
+    SIM_PROF(0);
 
     // ---- A: front vehicles decide
     for (int l = tid; l < NL; l += nt) {
@@ -95,7 +121,7 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
         const size_t base = (size_t)l * cap;
         const float x0 = V.x[base + h0], v0 = V.v[base + h0];
         const int d0 = V.dst[base + h0];
-        const float len = lane_length(e, A, R, C, P);
+        const float len = lane_length(T, e);
         float acc, vn, xn;
         if (e >= 4 * A || d0 == e) {  // exit edge or destination edge: free road
             acc = idm_free(v0, P);
@@ -104,10 +130,10 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
             V.req[l] = kArrive;
         } else {
             const int aj = e >> 2, d = e & 3, h = opp(d);
-            const int o = route_out(aj, h, d0, R, C, S.exit_ao);
+            const int o = route_out(T, aj, h, d0);
             const int m = movement(h, o);
-            const int e2 = next_edge(aj, o, R, C, S.exit_id);
-            const int k2 = lane_for(e2, kf, d0, V.cnt, A, R, C, S.exit_ao);
+            const int e2 = next_edge(T, aj, o);
+            const int k2 = lane_for(T, e2, kf, d0, V.cnt);
             const int tl = e2 * 3 + k2;
             const bool green = (kGreen[V.phase[aj]] >> (d * 4 + m)) & 1;
             if (green) {
@@ -139,33 +165,46 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
         V.fv[l] = vn;
     }
     __syncthreads();
+    SIM_PROF(1);
 
     // ---- B: target lanes grant one request
+    // All 5 request slots are read at once; the first requester in the order
+    // rotated by t % 5 is the only one considered (granted if there is room).
     for (int tl = tid; tl < NL; tl += nt) {
-        int fl[5];
-        if (!feeders(tl / 3, A, R, C, S.exit_ao, fl)) continue;
-        const int start = t % 5;
+        int as, o;
+        if (!feed_src(T, tl / 3, as, o)) continue;
+        int f[5];
+        uint32_t mask = 0;
+#pragma unroll
         for (int i = 0; i < 5; i++) {
-            int f = fl[(start + i) % 5];
-            if (V.req[f] != tl) continue;
-            int nc = V.cnt[tl];
-            bool room = nc < cap;
-            if (room && nc > 0) {
-                int ls = last_slot(V.head[tl], nc, cap);
-                room = (V.x[(size_t)tl * cap + ls] - P.length) >= P.min_gap;
-            }
-            if (room) V.gfrom[tl] = f;
-            break;  // only the highest-priority requester is considered
+            f[i] = feeder(as, o, i);
+            mask |= (V.req[f[i]] == tl ? 1u : 0u) << i;
         }
+        if (!mask) continue;
+        const int start = t % 5;
+        const uint32_t rot = ((mask >> start) | (mask << (5 - start))) & 31u;
+        int k = start + __ffs(rot) - 1;
+        if (k >= 5) k -= 5;
+        int fsel = f[0];
+#pragma unroll
+        for (int i = 1; i < 5; i++) fsel = k == i ? f[i] : fsel;
+        int nc = V.cnt[tl];
+        bool room = nc < cap;
+        if (room && nc > 0) {
+            int ls = last_slot(V.head[tl], nc, cap);
+            room = (V.x[(size_t)tl * cap + ls] - P.length) >= P.min_gap;
+        }
+        if (room) V.gfrom[tl] = fsel;
     }
     __syncthreads();
+    SIM_PROF(2);
 
     // ---- C: advance every lane; fronts leave (granted) or arrive
     for (int l = tid; l < NL; l += nt) {
         int n = V.cnt[l];
         if (n == 0) continue;
         const int e = l / 3;
-        const float len = lane_length(e, A, R, C, P);
+        const float len = lane_length(T, e);
         const size_t base = (size_t)l * cap;
         int hd = V.head[l];
         // front
@@ -219,6 +258,7 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
         }
     }
     __syncthreads();
+    SIM_PROF(3);
 
     // ---- D: append granted vehicles
     for (int tl = tid; tl < NL; tl += nt) {
@@ -226,7 +266,7 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
         if (f < 0) continue;
         const int e2 = tl / 3;
         (void)e2;
-        const float over = V.fx[f] - lane_length(f / 3, A, R, C, P);
+        const float over = V.fx[f] - lane_length(T, f / 3);
         const float vin = V.fv[f];
         // the source lane already popped its front; read its (old) destination
         // from the slot it vacated
@@ -248,16 +288,24 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
         V.cnt[tl] = nc + 1;
     }
     __syncthreads();
+    SIM_PROF(4);
 
-    // ---- E: insertion from the origin queues (vehicles with depart <= t)
-    for (int e = tid; e < 4 * A; e += nt) {
+    // ---- E: insertion from the origin queues (vehicles with depart <= t).
+    // Queue e is always handled by thread e % nt (slot q = e / nt), which keeps
+    // the queue's next vehicle (id, destination) in registers: after an
+    // insertion it issues the loads of the following one, consumed a substep
+    // later, so the HBM/L2 latency of the departure table is off the chain.
+#pragma unroll
+    for (int q = 0; q < QSLOTS; q++) {
+        const int e = tid + q * nt;
+        if (e >= 4 * A) continue;
         int p = V.qptr[e];
         if (p >= V.q_off[e + 1]) continue;
-        const int id = V.q_ids[p];
+        const int id = qn[q].id;
         if ((long long)id * S.period_ms > (long long)t * 1000) continue;
-        const int d0 = V.vdst[id];
+        const int d0 = qn[q].dst;
         const int aj = e >> 2, d = e & 3, h = opp(d);
-        const int o = route_out(aj, h, d0, R, C, S.exit_ao);
+        const int o = route_out(T, aj, h, d0);
         const int m = movement(h, o);
         const int k = lane_for_move(m, e, V.cnt);
         const int l = e * 3 + k;
@@ -275,8 +323,10 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
         V.cnt[l] = nc + 1;
         V.qptr[e] = p + 1;
         atomicAdd(&V.stats[0], 1);
+        if (p + 1 < V.q_off[e + 1]) qn[q] = next_vehicle(V, p + 1);
     }
     __syncthreads();
+    SIM_PROF(5);
 }
 
 // LDS image of one env's mutable state (kLDS path): x, v, dst rings
@@ -284,7 +334,8 @@ __device__ __forceinline__ void substep(EnvView &V, const dmdqn_idm &P, int t) {
 // stats [4].  4x4 grid, cap 24: 75 KB -> two envs per CU.
 __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
     const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
-    return (size_t)NL * cap * 12 + (size_t)NL * 6 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16;
+    return (size_t)NL * cap * 12 + (size_t)NL * 6 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16 +
+           (size_t)(4 * A + 1) * 4;  // q_off
 }
 
 // One RL step per env (block).  kLDS: the env's state is staged into LDS for
@@ -293,11 +344,17 @@ __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
 // slots move between HBM and LDS.  !kLDS: the same passes on global memory,
 // for grids whose state exceeds LDS.
 template <bool kLDS>
-__global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, const int32_t *actions,
+__global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions,
                                                   int stride, int t0, int K, int max_time,
                                                   int32_t *halt, int32_t *phase_out,
                                                   int32_t *tspent, uint8_t *done) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
+    const uint64_t prof_t0 = __builtin_amdgcn_s_memrealtime();
+    const IdmK P(Pa);
+    // topology tables after the state image (kLDS) or alone (global path)
+    const size_t topo_off = kLDS ? sim_lds_bytes(S.R, S.C, S.cap_lane) : 0;
+    const Topo T = build_topo(reinterpret_cast<int32_t *>(dyn + topo_off), S.R, S.C, S.exit_id,
+                              S.exit_ao, P.len_inner, P.len_outer);  // synced below
     EnvView G(S, blockIdx.x);
     EnvView V(S, blockIdx.x);
     const int A = V.A, NL = V.NL, cap = V.cap;
@@ -317,9 +374,20 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, cons
         V.ts = V.phase + A;
         V.qptr = V.ts + A;
         V.stats = V.qptr + 4 * A;
+        int32_t *qoff = V.stats + 4;
+        for (int i = tid; i <= 4 * A; i += nt) qoff[i] = G.q_off[i];
+        V.q_off = qoff;
+        // each thread stages its lanes' occupied slots only (~8 % of the rings)
         for (int l = tid; l < NL; l += nt) {
-            V.head[l] = G.head[l];
-            V.cnt[l] = G.cnt[l];
+            const int h = G.head[l], n = G.cnt[l];
+            V.head[l] = h;
+            V.cnt[l] = n;
+            const size_t base = (size_t)l * cap;
+            for (int i = 0, s = h; i < n; i++, s = (s + 1 == cap) ? 0 : s + 1) {
+                V.x[base + s] = G.x[base + s];
+                V.v[base + s] = G.v[base + s];
+                V.dst[base + s] = G.dst[base + s];
+            }
         }
         for (int a = tid; a < A; a += nt) {
             V.phase[a] = G.phase[a];
@@ -327,17 +395,6 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, cons
         }
         for (int e = tid; e < 4 * A; e += nt) V.qptr[e] = G.qptr[e];
         if (tid < 4) V.stats[tid] = G.stats[tid];
-        __syncthreads();
-        for (int i = tid; i < (int)NS; i += nt) {
-            const int l = i / cap, sl = i - l * cap;
-            int off = sl - V.head[l];
-            if (off < 0) off += cap;
-            if (off < V.cnt[l]) {
-                V.x[i] = G.x[i];
-                V.v[i] = G.v[i];
-                V.dst[i] = G.dst[i];
-            }
-        }
     }
     if (actions) {
         for (int a = tid; a < A; a += nt) {
@@ -346,7 +403,16 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, cons
         }
     }
     __syncthreads();
-    for (int k = 0; k < K; k++) substep(V, P, t0 + k);
+    QNext qn[QSLOTS];
+#pragma unroll
+    for (int q = 0; q < QSLOTS; q++) {
+        const int e = tid + q * nt;
+        qn[q] = QNext{0, 0};
+        if (e < 4 * A && V.qptr[e] < V.q_off[e + 1]) qn[q] = next_vehicle(V, V.qptr[e]);
+    }
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memrealtime();
+    prof[6] = prof_t - prof_t0;  // staging
+    for (int k = 0; k < K; k++) substep(V, T, P, t0 + k, qn, prof, prof_t);
     const int t = t0 + K;
     // halting counts on the observed (incoming) lanes + bookkeeping
     __shared__ int s_running, s_pending;
@@ -383,20 +449,16 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, cons
     }
     if constexpr (kLDS) {
         // write back: occupied slots, lane heads/counts, signals, queues
-        const size_t NS = (size_t)NL * cap;
-        for (int i = tid; i < (int)NS; i += nt) {
-            const int l = i / cap, sl = i - l * cap;
-            int off = sl - V.head[l];
-            if (off < 0) off += cap;
-            if (off < V.cnt[l]) {
-                G.x[i] = V.x[i];
-                G.v[i] = V.v[i];
-                G.dst[i] = V.dst[i];
-            }
-        }
         for (int l = tid; l < NL; l += nt) {
-            G.head[l] = V.head[l];
-            G.cnt[l] = V.cnt[l];
+            const int h = V.head[l], n = V.cnt[l];
+            G.head[l] = h;
+            G.cnt[l] = n;
+            const size_t base = (size_t)l * cap;
+            for (int i = 0, s = h; i < n; i++, s = (s + 1 == cap) ? 0 : s + 1) {
+                G.x[base + s] = V.x[base + s];
+                G.v[base + s] = V.v[base + s];
+                G.dst[base + s] = V.dst[base + s];
+            }
         }
         for (int a = tid; a < A; a += nt) {
             G.phase[a] = V.phase[a];
@@ -404,6 +466,13 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm P, cons
         }
         for (int e = tid; e < 4 * A; e += nt) G.qptr[e] = V.qptr[e];
     }
+#ifdef DMDQN_SIM_PROFILE
+    __syncthreads();
+    if (tid == 0) {
+        prof[7] = __builtin_amdgcn_s_memrealtime() - prof_t;  // halting + write-back
+        for (int i = 0; i < 8; i++) halt[(size_t)blockIdx.x * 12 * A + i] = (int32_t)prof[i];
+    }
+#endif
 }
 
 __global__ void k_sim_reset(dmdqn_sim S) {
@@ -432,9 +501,11 @@ static int check_sim(const dmdqn_sim *s) {
                   s->R, s->C);
     DMDQN_REQUIRE(s->E >= 1 && s->cap_lane >= 2 && s->cap_lane <= 64, "dmdqn_sim: E/cap_lane");
     DMDQN_REQUIRE(s->nveh >= 0 && s->nveh <= 65535 && s->period_ms > 0, "dmdqn_sim: demand");
+    DMDQN_REQUIRE(4 * s->R * s->C <= 2 * 256, "dmdqn_sim: at most 128 junctions (queue slots)");
     DMDQN_REQUIRE(s->x && s->v && s->dst && s->head && s->cnt && s->req && s->gfrom && s->fx &&
                       s->fv && s->tl_phase && s->tl_ts && s->qptr && s->q_off && s->exit_id &&
-                      s->exit_ao && s->stats && (s->nveh == 0 || (s->q_ids && s->vdst)),
+                      s->exit_ao && s->stats &&
+                      (s->nveh == 0 || (s->q_ids && s->vdst && s->q_dst)),
                   "dmdqn_sim: null array");
     return DMDQN_OK;
 }
@@ -456,11 +527,13 @@ extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const 
     DMDQN_REQUIRE(K >= 0 && t0 >= 0 && action_stride >= 0, "dmdqn_sim_step: K/t0");
     DMDQN_REQUIRE(action_stride * 3 < 12, "dmdqn_sim_step: action_stride*3 must be < 12");
     const size_t lds = sim_lds_bytes(sim->R, sim->C, sim->cap_lane);
-    if (lds <= 160 * 1024 - 64) {
-        hipLaunchKernelGGL(k_sim_step<true>, dim3(sim->E), dim3(256), lds, as_stream(stream), *sim,
-                           *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+    const size_t topo = topo_bytes(sim->R, sim->C);
+    if (lds + topo <= 160 * 1024 - 64) {
+        hipLaunchKernelGGL(k_sim_step<true>, dim3(sim->E), dim3(256), lds + topo, as_stream(stream),
+                           *sim, *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent,
+                           done);
     } else {
-        hipLaunchKernelGGL(k_sim_step<false>, dim3(sim->E), dim3(256), 0, as_stream(stream), *sim,
+        hipLaunchKernelGGL(k_sim_step<false>, dim3(sim->E), dim3(256), topo, as_stream(stream), *sim,
                            *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
     }
     DMDQN_LAUNCH_CHECK("k_sim_step");

@@ -29,41 +29,79 @@ __device__ __forceinline__ int movement(int h, int o) {
     return MV_L;
 }
 
-__device__ __forceinline__ int nbr(int a, int d, int R, int C) {
-    int r = a / C, c = a - r * C;
-    switch (d) {
-        case DIR_N: return r > 0 ? a - C : -1;
-        case DIR_S: return r < R - 1 ? a + C : -1;
-        case DIR_E: return c < C - 1 ? a + 1 : -1;
-        default: return c > 0 ? a - 1 : -1;
+// Static grid topology as LDS tables, built once per launch (k_sim_step), so
+// that no pass divides by the runtime grid width:
+//   jrc[a]    = r * 16 + c of junction a = r*C + c
+//   dinfo[e]  = tj * 4 + to for destination edge e: the junction tj to steer
+//               toward and the out-direction `to` taken there (approach edge
+//               b*4+db: tj = nbr(b, db), to = opp(db); exit x: exit_ao[x])
+struct Topo {
+    int R, C, A;
+    const int32_t *jrc, *dinfo, *exit_id, *exit_ao;
+    const float *elen;  // [4A + X] lane length of each edge
+
+    __device__ __forceinline__ int row(int a) const { return jrc[a] >> 4; }
+    __device__ __forceinline__ int col(int a) const { return jrc[a] & 15; }
+    __device__ __forceinline__ int nbr(int a, int d) const {
+        const int rc = jrc[a], r = rc >> 4, c = rc & 15;
+        switch (d) {
+            case DIR_N: return r > 0 ? a - C : -1;
+            case DIR_S: return r < R - 1 ? a + C : -1;
+            case DIR_E: return c < C - 1 ? a + 1 : -1;
+            default: return c > 0 ? a - 1 : -1;
+        }
     }
+};
+
+// Bytes of the tables for an R x C grid (dynamic LDS, 4-byte entries).
+__host__ __device__ inline size_t topo_bytes(int R, int C) {
+    const int A = R * C, X = 2 * R + 2 * C;
+    return (size_t)(A + (4 * A + X) + 4 * A + 2 * X + (4 * A + X)) * 4;
 }
 
-__device__ __forceinline__ float lane_length(int e, int A, int R, int C, const dmdqn_idm &P) {
-    if (e >= 4 * A) return P.len_outer;
-    return nbr(e >> 2, e & 3, R, C) >= 0 ? P.len_inner : P.len_outer;
+// Fill the tables at `mem` (all threads; caller syncs) and return the view.
+__device__ __forceinline__ Topo build_topo(int32_t *mem, int R, int C, const int32_t *g_exit_id,
+                                           const int32_t *g_exit_ao, float len_inner,
+                                           float len_outer) {
+    const int A = R * C, X = 2 * R + 2 * C, NE = 4 * A + X, tid = threadIdx.x,
+              nt = blockDim.x;
+    int32_t *jrc = mem, *dinfo = jrc + A, *xid = dinfo + NE, *xao = xid + 4 * A;
+    float *elen = reinterpret_cast<float *>(xao + 2 * X);
+    for (int a = tid; a < A; a += nt) jrc[a] = (a / C) * 16 + (a % C);
+    for (int i = tid; i < 4 * A; i += nt) xid[i] = g_exit_id[i];
+    for (int i = tid; i < 2 * X; i += nt) xao[i] = g_exit_ao[i];
+    for (int e = tid; e < NE; e += nt) {
+        int tj, to;
+        bool inner = false;
+        if (e >= 4 * A) {
+            tj = g_exit_ao[2 * (e - 4 * A)];
+            to = g_exit_ao[2 * (e - 4 * A) + 1];
+        } else {  // upstream junction of approach edge e (none for fringe edges: never a
+                  // routing target -- a vehicle on its destination edge drives free)
+            const int b = e >> 2, db = e & 3, r = b / C, c = b % C;
+            tj = db == DIR_N ? (r > 0 ? b - C : -1) : db == DIR_S ? (r < R - 1 ? b + C : -1)
+               : db == DIR_E ? (c < C - 1 ? b + 1 : -1) : (c > 0 ? b - 1 : -1);
+            inner = tj >= 0;
+            if (tj < 0) tj = 0;
+            to = opp(db);
+        }
+        dinfo[e] = tj * 4 + to;
+        elen[e] = inner ? len_inner : len_outer;
+    }
+    return Topo{R, C, A, jrc, dinfo, xid, xao, elen};
 }
+
+__device__ __forceinline__ float lane_length(const Topo &T, int e) { return T.elen[e]; }
 
 // Out-direction at junction a for a vehicle heading h toward destination edge
 // dst: move toward the junction the destination edge leaves from, keeping
 // straight when that reduces the distance, vertical before horizontal, a
 // U-turn only when it is the only reducing move; at that junction take the
 // destination's direction.
-__device__ __forceinline__ int route_out(int a, int h, int dst, int R, int C,
-                                         const int32_t *exit_ao) {
-    const int A = R * C;
-    int tj, to;
-    if (dst >= 4 * A) {
-        int x = dst - 4 * A;
-        tj = exit_ao[2 * x];
-        to = exit_ao[2 * x + 1];
-    } else {
-        int b = dst >> 2, db = dst & 3;
-        tj = nbr(b, db, R, C);
-        to = opp(db);
-    }
+__device__ __forceinline__ int route_out(const Topo &T, int a, int h, int dst) {
+    const int tt = T.dinfo[dst], tj = tt >> 2, to = tt & 3;
     if (a == tj) return to;
-    int r = a / C, c = a - r * C, rt = tj / C, ct = tj - rt * C;
+    const int r = T.row(a), c = T.col(a), rt = T.row(tj), ct = T.col(tj);
     int dv = rt < r ? DIR_N : (rt > r ? DIR_S : -1);
     int dh = ct > c ? DIR_E : (ct < c ? DIR_W : -1);
     if (h == dv || h == dh) return h;
@@ -72,9 +110,9 @@ __device__ __forceinline__ int route_out(int a, int h, int dst, int R, int C,
     return dv >= 0 ? dv : dh;
 }
 
-__device__ __forceinline__ int next_edge(int a, int o, int R, int C, const int32_t *exit_id) {
-    int nb = nbr(a, o, R, C);
-    return nb >= 0 ? nb * 4 + opp(o) : 4 * R * C + exit_id[a * 4 + o];
+__device__ __forceinline__ int next_edge(const Topo &T, int a, int o) {
+    int nb = T.nbr(a, o);
+    return nb >= 0 ? nb * 4 + opp(o) : 4 * T.A + T.exit_id[a * 4 + o];
 }
 
 // Lane index for movement m on incoming edge e: right -> 0, left/U -> 2,
@@ -86,57 +124,71 @@ __device__ __forceinline__ int lane_for_move(int m, int e, const int32_t *cnt) {
 }
 
 // Lane a vehicle takes when entering edge e2 from lane index kf.
-__device__ __forceinline__ int lane_for(int e2, int kf, int dst, const int32_t *cnt, int A,
-                                        int R, int C, const int32_t *exit_ao) {
-    if (e2 >= 4 * A || e2 == dst) return kf;  // connections keep the lane index
+__device__ __forceinline__ int lane_for(const Topo &T, int e2, int kf, int dst,
+                                        const int32_t *cnt) {
+    if (e2 >= 4 * T.A || e2 == dst) return kf;  // connections keep the lane index
     int h2 = opp(e2 & 3);
-    int o2 = route_out(e2 >> 2, h2, dst, R, C, exit_ao);
+    int o2 = route_out(T, e2 >> 2, h2, dst);
     return lane_for_move(movement(h2, o2), e2, cnt);
 }
 
-// The 5 lanes that can feed edge e2 (in approach order n,s,e,w, lane order).
-// Returns false for fringe-in edges (nothing upstream).
-__device__ __forceinline__ bool feeders(int e2, int A, int R, int C, const int32_t *exit_ao,
-                                        int fl[5]) {
-    int as, o;
-    if (e2 < 4 * A) {
-        as = nbr(e2 >> 2, e2 & 3, R, C);
-        if (as < 0) return false;
+// Upstream junction `as` and out-direction `o` of the movements that feed edge
+// e2; false for fringe-in edges (nothing upstream).
+__device__ __forceinline__ bool feed_src(const Topo &T, int e2, int &as, int &o) {
+    if (e2 < 4 * T.A) {
+        as = T.nbr(e2 >> 2, e2 & 3);
         o = opp(e2 & 3);
-    } else {
-        int x = e2 - 4 * A;
-        as = exit_ao[2 * x];
-        o = exit_ao[2 * x + 1];
+        return as >= 0;
     }
-    int n = 0;
+    const int x = e2 - 4 * T.A;
+    as = T.exit_ao[2 * x];
+    o = T.exit_ao[2 * x + 1];
+    return true;
+}
+
+// The i-th of the 5 lanes that feed edge e2 (approach order n,s,e,w, lane
+// order within an approach): the straight approach d = opp(o) contributes
+// lanes 0 and 1, right turns lane 0, left / U-turns lane 2.  A function of a
+// compile-time i (callers unroll), so no per-thread array is indexed.
+__device__ __forceinline__ int feeder(int as, int o, int i) {
+    int pos = 0, out = 0;
+#pragma unroll
     for (int d = 0; d < 4; d++) {
-        int m = movement(opp(d), o), base = (as * 4 + d) * 3;
+        const int m = movement(opp(d), o), base = (as * 4 + d) * 3;
         if (m == MV_S) {
-            fl[n++] = base;
-            fl[n++] = base + 1;
-        } else if (m == MV_R) {
-            fl[n++] = base;
+            if (pos == i) out = base;
+            if (pos + 1 == i) out = base + 1;
+            pos += 2;
         } else {
-            fl[n++] = base + 2;
+            if (pos == i) out = base + (m == MV_R ? 0 : 2);
+            pos += 1;
         }
     }
-    return true;
+    return out;
 }
 
 // IDM (Treiber): a [1 - (v/v0)^4 - (s*/s)^2], s* = s0 + max(0, vT + v dv/(2 sqrt(ab))).
 // Fixed evaluation order (mirrored by oracle/oracle_sim.c).
-__device__ __forceinline__ float idm_free(float v, const dmdqn_idm &P) {
-    float r = v / P.vmax;
+// dmdqn_idm plus the f32 reciprocals of its two constant divisors, computed
+// once per launch (oracle_sim.c does the same divisions: bit-identical).
+struct IdmK : dmdqn_idm {
+    float inv_vmax, inv_two_sqrt_ab;
+    __device__ explicit IdmK(const dmdqn_idm &p)
+        : dmdqn_idm(p), inv_vmax(1.0f / p.vmax), inv_two_sqrt_ab(1.0f / p.two_sqrt_ab) {}
+};
+
+__device__ __forceinline__ float idm_free(float v, const IdmK &P) {
+    float r = v * P.inv_vmax;
     float r2 = r * r;
     float r4 = r2 * r2;
     return P.accel * (1.0f - r4);
 }
 
-__device__ __forceinline__ float idm_acc(float v, float s, float dv, const dmdqn_idm &P) {
-    float r = v / P.vmax;
+__device__ __forceinline__ float idm_acc(float v, float s, float dv, const IdmK &P) {
+    float r = v * P.inv_vmax;
     float r2 = r * r;
     float r4 = r2 * r2;
-    float ss = v * P.tau + (v * dv) / P.two_sqrt_ab;
+    float ss = v * P.tau + (v * dv) * P.inv_two_sqrt_ab;
     if (ss < 0.0f) ss = 0.0f;
     float sstar = P.min_gap + ss;
     if (s < 0.01f) s = 0.01f;
@@ -145,7 +197,7 @@ __device__ __forceinline__ float idm_acc(float v, float s, float dv, const dmdqn
     return P.accel * (t1 - q * q);
 }
 
-__device__ __forceinline__ float clamp_speed(float v, const dmdqn_idm &P) {
+__device__ __forceinline__ float clamp_speed(float v, const IdmK &P) {
     if (v < 0.0f) return 0.0f;
     if (v > P.vmax) return P.vmax;
     return v;

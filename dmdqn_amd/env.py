@@ -83,7 +83,7 @@ class CSim(C.Structure):
                 ("period_ms", C.c_int32), ("nveh", C.c_int32)] + [
         (n, C.c_void_p) for n in ["x", "v", "dst", "head", "cnt", "req", "gfrom", "fx", "fv",
                                   "tl_phase", "tl_ts", "qptr", "q_off", "q_ids", "vdst",
-                                  "exit_id", "exit_ao", "stats"]]
+                                  "exit_id", "exit_ao", "stats", "q_dst"]]
 
 
 class CIdm(C.Structure):
@@ -136,6 +136,8 @@ class TrafficEnv:
         self.t_q_off = torch.from_numpy(q_off).to(dev)
         self.t_q_ids = torch.from_numpy(q_ids.view(np.int16)).to(dev)
         self.t_vdst = torch.from_numpy(vdst.view(np.int16)).to(dev)
+        q_dst = np.take_along_axis(vdst, q_ids.astype(np.int64), axis=1)  # queue order
+        self.t_q_dst = torch.from_numpy(np.ascontiguousarray(q_dst).view(np.int16)).to(dev)
         self.t_exit_id = torch.from_numpy(g.exit_id.reshape(-1).copy()).to(dev)
         self.t_exit_ao = torch.from_numpy(g.exit_ao.reshape(-1).copy()).to(dev)
         self.t_stats = z32(E, 4)
@@ -144,7 +146,7 @@ class TrafficEnv:
                                    self.t_req, self.t_gfrom, self.t_fx, self.t_fv,
                                    self.t_phase_state, self.t_ts, self.t_qptr, self.t_q_off,
                                    self.t_q_ids, self.t_vdst, self.t_exit_id, self.t_exit_ao,
-                                   self.t_stats]])
+                                   self.t_stats, self.t_q_dst]])
         self.cidm = cfg.idm.c_struct()
         # observation buffers
         self.halt = z32(E, A, 12)

@@ -125,6 +125,8 @@ typedef struct dmdqn_sim {
     const int32_t *exit_id;      /* [A*4] exit id of (a, out-dir) or -1        */
     const int32_t *exit_ao;      /* [X][2] (a, out-dir) of exit x              */
     int32_t *stats;              /* [E][4] inserted, arrived, running, pending */
+    const uint16_t *q_dst;       /* [E][nveh] vdst[q_ids[i]]: destination of the
+                                    vehicle at queue position i                */
 } dmdqn_sim;
 
 /* Car-following / geometry constants (SUMO passenger defaults + grid_3x3

@@ -114,17 +114,19 @@ static int feeders(const orc_env *g, int e2, int fl[5]) {
 }
 
 /* IDM, same operation order as sim.hpp */
+/* The IDM divides by the constants vmax and 2 sqrt(ab) through their f32
+ * reciprocals (one rounding each, as the HIP kernel does: sim.hpp IdmK). */
 static float idm_free(const orc_idm *P, float v) {
-    float r = v / P->vmax;
+    float r = v * (1.0f / P->vmax);
     float r2 = r * r;
     float r4 = r2 * r2;
     return P->accel * (1.0f - r4);
 }
 static float idm_acc(const orc_idm *P, float v, float s, float dv) {
-    float r = v / P->vmax;
+    float r = v * (1.0f / P->vmax);
     float r2 = r * r;
     float r4 = r2 * r2;
-    float ss = v * P->tau + (v * dv) / P->two_sqrt_ab;
+    float ss = v * P->tau + (v * dv) * (1.0f / P->two_sqrt_ab);
     if (ss < 0.0f) ss = 0.0f;
     float sstar = P->min_gap + ss;
     if (s < 0.01f) s = 0.01f;

@@ -1,0 +1,25 @@
+"""Diagnostic (needs a DMDQN_SIM_PROFILE build): per-pass time of k_sim_step,
+thread 0's view, averaged over envs and steps, in microseconds."""
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from dmdqn_amd.env import EnvConfig, TrafficEnv  # noqa: E402
+
+R, C, E = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (4, 4, 1024)
+env = TrafficEnv(EnvConfig(rows=R, cols=C, num_envs=E, seed=3))
+env.reset()
+g = torch.Generator(device="cuda").manual_seed(0)
+acc = np.zeros(8)
+n = 0
+for step in range(120):
+    a = torch.randint(0, 4, (E, env.A), device="cuda", generator=g, dtype=torch.int32)
+    env.step(a)
+    if step >= 60:
+        acc += env.halt.reshape(E, -1)[:, :8].double().mean(0).cpu().numpy() / 100.0
+        n += 1
+names = ["TL", "A front decide", "B grant", "C advance", "D append", "E insert", "staging",
+         "halt+writeback"]
+print({k: round(v / n, 2) for k, v in zip(names, acc)}, "us per launch (substep passes summed over K)")
