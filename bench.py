@@ -78,12 +78,22 @@ def read_traffic(workload_key):
         return None
 
 
-def _sim_roofline(E, K, vbar, sim_ms, traffic):
+def sim_state_fits_lds(rows, cols, cap=24):
+    """Mirror of sim.hip's path choice (state image + topology tables <= LDS)."""
+    A, X = rows * cols, 2 * rows + 2 * cols
+    NL = 3 * (4 * A + X)
+    state = NL * cap * 12 + NL * 24 + A * 24 + 16 + (4 * A + 1) * 4
+    topo = (A + (4 * A + X) + 4 * A + 2 * X + (4 * A + X)) * 4
+    return state + topo <= 160 * 1024 - 64
+
+
+def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
     """Sim-only HBM figure: 20*K*V-bar algorithmic bytes per env
     step over the average k_sim_step duration (HIP events, timed region)."""
     t = float(np.mean(sim_ms)) / 1e3
     b = E * SIM_BYTES_PER_VEH_SUBSTEP * K * vbar
-    return {"kernel": "k_sim_step (K IDM substeps per launch, env state staged in LDS)",
+    where = "env state staged in LDS" if in_lds else "env state in HBM (exceeds LDS)"
+    return {"kernel": f"k_sim_step (K IDM substeps per launch, {where})",
             "bound": "hbm", "achieved": round(b / t / 1e9, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 5),
             "traffic": traffic, "bytes_per_launch": int(b), "mean_running_vehicles": round(vbar, 1),
@@ -244,9 +254,11 @@ def main():
             "cpu_baseline": cpu,
             # secondary figures SURVEY 8d asks for next to the headline roofline
             "sim_roofline": _sim_roofline(E, tr.env.cfg.step_duration, vbar, sim_ms,
-                                          read_traffic(f"{wl}_sim")),
+                                          read_traffic(f"{wl}_sim"),
+                                          sim_state_fits_lds(args.rows, args.cols)),
             "mfma": {
-                "kernel": "k_learn_f16 (Q-net forward/backward, v_mfma_f32_16x16x32_f16)",
+                "kernel": ("k_learn_shared_f16" if args.shared else "k_learn_f16") +
+                          " (Q-net forward/backward, v_mfma_f32_16x16x32_f16)",
                 "flop_per_launch": NA * LEARN_FLOP_PER_AGENT,
                 "achieved": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12, 2),
                 "peak": MFMA_F16_DENSE_TFLOPS,
