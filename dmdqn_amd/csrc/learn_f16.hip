@@ -195,50 +195,59 @@ __device__ __forceinline__ half4v relu_h4(f32x4 acc, float4 b) {
     return hv;
 }
 
-// Forward of one 128-row batch X (in R2); Q -> qout[128][4] (f32 of the f16
-// output, as Keras' mixed policy emits f16 from the last Dense).
-//   KEEPX = false: H1 stays in R1, H2 goes to R2 over X (the training forward:
-//                  backward needs H1 and H2).
-//   KEEPX = true : H2 overwrites H1 in R1 after a barrier and X survives in R2
-//                  for a second forward on the same batch.
-// after_l1 / after_l2 run once the layer's MFMAs no longer need f.w1 / f.w2:
-// they may start loading the next network's fragments into f (the output
-// layer of THIS network is read through pointers captured before after_l2).
-template <bool KEEPX, typename H1k = NoHook, typename H2k = NoHook>
-__device__ void forward(Frags &f, const OutL o, _Float16 *R1, _Float16 *R2, float *qout,
-                        H1k after_l1 = {}, H2k after_l2 = {}) {
+struct NoHook0 {
+    __device__ void operator()() const {}
+};
+
+// Forward with explicit buffers: X (rows, stride DP) -> H1b -> H2b -> qout.
+//   HOLD = true : H2b == H1b -- layer 2 keeps its 8 output tiles in registers
+//                 across a barrier before overwriting H1 (X survives).
+//   HOLD = false: H2b != H1b -- each layer-2 tile is written as soon as it is
+//                 computed (H2b may be X's buffer: X is dead after layer 1).
+// Hooks: after_l1(f) / after_l2(f) as in forward(); after_sync2() runs after
+// the barrier that follows layer 2 (every wave is done reading H1b).
+template <bool HOLD, typename H1k = NoHook, typename H2k = NoHook, typename S2k = NoHook0>
+__device__ void forward_x(Frags &f, const OutL o, const _Float16 *X, _Float16 *H1b, _Float16 *H2b,
+                          float *qout, H1k after_l1 = {}, H2k after_l2 = {},
+                          S2k after_sync2 = {}) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
     const int n = 16 * w + 4 * lg;
-    // layer 1: K = 96 (3 k-steps), B = X rows
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row(R2, DP, 16 * t, 32 * s), c);
-        *reinterpret_cast<half4v *>(R1 + (16 * t + lr) * H + n) = relu_h4(c, f.b1);
+        for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row(X, DP, 16 * t, 32 * s), c);
+        *reinterpret_cast<half4v *>(H1b + (16 * t + lr) * H + n) = relu_h4(c, f.b1);
     }
     after_l1(f);
     __syncthreads();
-    // layer 2: K = 128, B = H1 rows (R1)
-    _Float16 *H2 = KEEPX ? R1 : R2;
-    {
+    if constexpr (HOLD) {
         f32x4 acc[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row(R1, H, 16 * t, 32 * s), c);
+            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row(H1b, H, 16 * t, 32 * s), c);
             acc[t] = c;
         }
         const float4 b2 = f.b2;
         after_l2(f);
-        if (KEEPX) __syncthreads();  // every wave has read H1
+        __syncthreads();  // every wave has read H1
 #pragma unroll
         for (int t = 0; t < 8; t++)
-            *reinterpret_cast<half4v *>(H2 + (16 * t + lr) * H + n) = relu_h4(acc[t], b2);
+            *reinterpret_cast<half4v *>(H2b + (16 * t + lr) * H + n) = relu_h4(acc[t], b2);
+    } else {
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row(H1b, H, 16 * t, 32 * s), c);
+            *reinterpret_cast<half4v *>(H2b + (16 * t + lr) * H + n) = relu_h4(c, f.b2);
+        }
+        after_l2(f);
     }
     __syncthreads();
-    // layer 3: Q^T[a][b] = W3T[a][k] . H2[b][k]; wave w -> batch tile w
+    after_sync2();
     {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -248,7 +257,7 @@ __device__ void forward(Frags &f, const OutL o, _Float16 *R1, _Float16 *R2, floa
             else
 #pragma unroll
                 for (int e = 0; e < 8; e++) a3[e] = (_Float16)0.0f;
-            acc = mfma(a3, frag_row(H2, H, 16 * w, 32 * s), acc);
+            acc = mfma(a3, frag_row(H2b, H, 16 * w, 32 * s), acc);
         }
         if (lg == 0) {
             float4 q;
@@ -679,21 +688,25 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     // target forward keeps X(S') in R2; the online net's fragments (reused by
     // both online forwards) load layer by layer as the target's die
     const float *Wpc = Wp;
-    forward<true>(fr, tg, R1, R2, S.z3, [Wpc](Frags &f) { load_w1(Wpc, f); },
-                  [Wpc](Frags &f) { load_w2(Wpc, f); });
+    // Buffer plan: target X=R2 -> H1 R1 -> H2 R1 (hold; X survives) ;
+    // online S': X=R2 -> H1 R1 -> H2 R2 over the dead X (no hold), the S rows
+    // issued after layer 1 land in R1 once layer 2 is done ; training forward:
+    // X=R1 -> H1 R2 -> H2 R1 over X (no hold).  The backward then finds H1 in R2
+    // and H2 in R1: it runs on the swapped pair (P1, P2) = (R2, R1).
+    forward_x<true>(fr, tg, R2, R1, R1, S.z3, [Wpc](Frags &f) { load_w1(Wpc, f); },
+                    [Wpc](Frags &f) { load_w2(Wpc, f); });
     STAMP(3);
-    // online(S'): X(S') is dead after layer 1, so the S rows for the training
-    // forward load during layers 1-2 and land in R2 while H2 sits in R1
-    float *qo = (float *)DQ;  // 2 KB; DQ is not needed until after the S forward
+    float *qo = (float *)DQ;
     Rows gs;
-    forward<true>(fr, on, R1, R2, qo, [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); },
-                  [&](Frags &) { gather_commit(R2, gs); });
+    forward_x<false>(fr, on, R2, R1, R2, qo,
+                     [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); }, NoHook{},
+                     [&]() { gather_commit(R1, gs); });
     STAMP(4);
     STAMP(5);
     ddqn_target(a, qo, S);
-    // ---- online(S), activations kept: H1 in R1, H2 in R2 ; q, loss, DQ
     STAMP(6);
-    forward<false>(fr, on, R1, R2, S.z3);
+    forward_x<false>(fr, on, R1, R2, R1, S.z3);
+    _Float16 *const P1 = R2, *const P2 = R1;
     STAMP(7);
     loss_dq<QSTATS>(a, agent, DQ, S);
 
@@ -704,7 +717,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
             half8 dqf = frag_tr(DQ, 16, b0, 0);
-            acc = mfma(frag_tr(R2, H, b0, 16 * w), dqf, acc);
+            acc = mfma(frag_tr(P2, H, b0, 16 * w), dqf, acc);
             gb = mfma(ones, dqf, gb);  // every wave (no MFMA under divergent control)
         }
         if (lr < NACT) {
@@ -715,9 +728,9 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();  // dW3 read H2; dZ2 overwrites it
     STAMP(8);
-    bwd_dz2(R2, on, S);
+    bwd_dz2(P2, on, S);
     STAMP(9);
-    h1_mask(R1, mask);  // the DQ region is free now
+    h1_mask(P1, mask);  // the DQ region is free now
     // ---- dW2[j][k] = H1^T . dZ2 (wave w: j-tile w, 8 k-tiles) ; db2 (k-tile w) ; Adam
     {
         f32x4 g2[8], gb = {0.f, 0.f, 0.f, 0.f};
@@ -725,15 +738,15 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         for (int t = 0; t < 8; t++) g2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 av = frag_tr(R1, H, b0, 16 * w);
-            gb = mfma(ones, frag_tr(R2, H, b0, 16 * w), gb);
+            const half8 av = frag_tr(P1, H, b0, 16 * w);
+            gb = mfma(ones, frag_tr(P2, H, b0, 16 * w), gb);
 #pragma unroll
-            for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr(R2, H, b0, 16 * t), g2[t]);
+            for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr(P2, H, b0, 16 * t), g2[t]);
         }
-        // H1 fully consumed (dW2, mask): R1 becomes the W2^T image now, from
+        // H1 fully consumed (dW2, mask): P1 becomes the W2^T image now, from
         // the register copy of old W2 (fr.w2), which is then dead during Adam
         __syncthreads();
-        w2t_image(R1, fr);
+        w2t_image(P1, fr);
         // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3]
         adam_pipe<4, 2>(Wp, Mp, Vp, Tp,
                         [&](int t) { return (size_t)L::oW2T + (size_t)(16 * t + lr) * H + 16 * w + 4 * lg; },
@@ -742,14 +755,14 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();  // W2^T image complete
     f32x4 d1[8];
-    bwd_dh1_from_image(R1, R2, d1);
+    bwd_dh1_from_image(P1, P2, d1);
     {
-        Rows gx;  // X(S) again for dW1 (R2 is free)
+        Rows gx;  // X(S) again for dW1 (P2 is free)
         gather_issue(a.ring_s, a, agent, S.slot, gx);
-        gather_commit(R2, gx);
+        gather_commit(P2, gx);
     }
     STAMP(10);
-    bwd_dz1(R1, mask, d1);
+    bwd_dz1(P1, mask, d1);
     __syncthreads();
     STAMP(11);
     // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
@@ -759,10 +772,10 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         for (int t = 0; t < 6; t++) g1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 bv = frag_tr(R1, H, b0, 16 * w);
+            const half8 bv = frag_tr(P1, H, b0, 16 * w);
             gb = mfma(ones, bv, gb);
 #pragma unroll
-            for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr(R2, DP, b0, 16 * t), bv, g1[t]);
+            for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr(P2, DP, b0, 16 * t), bv, g1[t]);
         }
         // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; padded
         // features 89..95 have zero weight and zero gradient and stay zero
@@ -820,60 +833,63 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
             gather_commit(R2, gn);
         }
         __syncthreads();
-        forward<true>(fr, tg, R1, R2, S.z3, [Wp](Frags &f) { load_w1(Wp, f); },
-                      [Wp](Frags &f) { load_w2(Wp, f); });  // X(S') stays in R2
+        // buffer plan of k_learn_f16: the backward runs on (P1, P2) = (R2, R1)
+        forward_x<true>(fr, tg, R2, R1, R1, S.z3, [Wp](Frags &f) { load_w1(Wp, f); },
+                        [Wp](Frags &f) { load_w2(Wp, f); });  // X(S') stays in R2
         float *qo = (float *)DQ;
         Rows gs;
-        forward<true>(fr, on, R1, R2, qo, [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); },
-                      [&](Frags &) { gather_commit(R2, gs); });
+        forward_x<false>(fr, on, R2, R1, R2, qo,
+                         [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); }, NoHook{},
+                         [&]() { gather_commit(R1, gs); });
         ddqn_target(a, qo, S);
-        forward<false>(fr, on, R1, R2, S.z3);
+        forward_x<false>(fr, on, R1, R2, R1, S.z3);
+        _Float16 *const P1 = R2, *const P2 = R1;
         loss_dq<QSTATS>(a, agent, DQ, S);
         // dW3 / db3
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
             const half8 dqf = frag_tr(DQ, 16, b0, 0);
-            G3 = mfma(frag_tr(R2, H, b0, 16 * w), dqf, G3);
+            G3 = mfma(frag_tr(P2, H, b0, 16 * w), dqf, G3);
             GB3 = mfma(ones, dqf, GB3);
         }
         __syncthreads();
-        bwd_dz2(R2, on, S);
-        h1_mask(R1, mask);
+        bwd_dz2(P2, on, S);
+        h1_mask(P1, mask);
         // dW2 / db2 (tile by tile, accumulating into the LDS accumulators)
         {
             half8 av[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                av[q] = frag_tr(R1, H, 32 * q, 16 * w);
-                GB2 = mfma(ones, frag_tr(R2, H, 32 * q, 16 * w), GB2);
+                av[q] = frag_tr(P1, H, 32 * q, 16 * w);
+                GB2 = mfma(ones, frag_tr(P2, H, 32 * q, 16 * w), GB2);
             }
 #pragma unroll
             for (int t = 0; t < 8; t++) {
                 f32x4 c = G2L[(w * 8 + t) * 64 + l];
 #pragma unroll
-                for (int q = 0; q < 4; q++) c = mfma(av[q], frag_tr(R2, H, 32 * q, 16 * t), c);
+                for (int q = 0; q < 4; q++) c = mfma(av[q], frag_tr(P2, H, 32 * q, 16 * t), c);
                 G2L[(w * 8 + t) * 64 + l] = c;
             }
         }
         __syncthreads();
         f32x4 d1[8];
-        bwd_dh1(R1, R2, fr, d1);
+        bwd_dh1(P1, P2, fr, d1);
         {
             Rows gx;
             gather_issue(a.ring_s, a, agent, S.slot, gx);
-            gather_commit(R2, gx);
+            gather_commit(P2, gx);
         }
-        bwd_dz1(R1, mask, d1);
+        bwd_dz1(P1, mask, d1);
         __syncthreads();
         // dW1 / db1
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 bv = frag_tr(R1, H, b0, 16 * w);
+            const half8 bv = frag_tr(P1, H, b0, 16 * w);
             GB1 = mfma(ones, bv, GB1);
 #pragma unroll
-            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr(R2, DP, b0, 16 * t), bv, G1[t]);
+            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr(P2, DP, b0, 16 * t), bv, G1[t]);
         }
-        __syncthreads();  // R1 / R2 / scratch are rewritten by the next agent
+        __syncthreads();  // P1 / P2 / scratch are rewritten by the next agent
     }
     // partial sums of this workgroup, kernel layout (every index written once)
     float *G = slab + (size_t)blockIdx.x * L::P;
