@@ -37,7 +37,7 @@ class CLearn(C.Structure):
                                   "params", "adam_m", "adam_v", "target", "target_h",
                                   "loss"]] + [
         (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]] + [
-        ("stamps", C.c_void_p), ("qstats", C.c_void_p)]
+        ("stamps", C.c_void_p), ("qstats", C.c_void_p), ("params_h", C.c_void_p)]
 
 
 _lib.register({
@@ -48,8 +48,9 @@ _lib.register({
                               C.c_void_p, C.c_void_p],
     "dmdqn_learn_shared_grad": [C.POINTER(CLearn), C.c_void_p, C.c_int, C.c_void_p, C.c_float,
                                 C.c_void_p],
-    "dmdqn_adam": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
-                   C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_void_p],
+    "dmdqn_adam": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                   C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
+                   C.c_int, C.c_void_p],
 })
 
 PRECISIONS = {"fp32": 0, "fp16": 1}
@@ -198,10 +199,17 @@ class BatchedDQN:
         self.target = self.params.clone()
         # fp16 path: the target forward reads an f16 copy (padded row stride Ph)
         self.Ph = (self.P + 7) // 8 * 8
-        self.target_h = None
+        self.target_h = self.params_h = None
         if cfg.precision == "fp16":
+            # f16 copies the forwards read (Keras casts the f32 variables to f16);
+            # the online copy only for the shared net, whose Adam is a separate
+            # pass (fused into the per-agent learn, the extra stores cost more
+            # than the halved fragment reads save)
             self.target_h = torch.zeros((NW, self.Ph), dtype=torch.float16, device=dev)
             self._refresh_target_h()
+            if self.shared:
+                self.params_h = torch.zeros((NW, self.Ph), dtype=torch.float16, device=dev)
+                self._refresh_params_h()
         if self.shared:
             # one partial gradient per persistent workgroup (one per CU)
             n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -295,7 +303,8 @@ class BatchedDQN:
                                self.target_h, self.loss]],
                    np.float32(cfg.gamma), alpha, c1, c2, eps,
                    None if self.stamps is None else self.stamps.data_ptr(),
-                   self.qstats.zero_().data_ptr() if collect_stats else None)
+                   self.qstats.zero_().data_ptr() if collect_stats else None,
+                   None if self.params_h is None else self.params_h.data_ptr())
         self._last_args = a  # keeps the struct (and what it points at) inspectable
         if self.learn_hook:
             self.learn_hook(True)
@@ -334,8 +343,13 @@ class BatchedDQN:
             if world > 1:
                 dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)  # one flat 114 KB buffer
         call("dmdqn_adam", ptr(self.params), ptr(self.adam_m), ptr(self.adam_v), ptr(self.target),
-             ptr(self.target_h), ptr(self.grad), self.P, C.c_float(1.0 / world), C.c_float(alpha),
+             ptr(self.target_h), ptr(self.params_h), ptr(self.grad), self.P, C.c_float(1.0 / world),
+             C.c_float(alpha),
              C.c_float(c1), C.c_float(c2), C.c_float(eps), int(sync), st)
+
+    def _refresh_params_h(self):
+        if self.params_h is not None:
+            self.params_h[:, :self.P].copy_(self.params.to(torch.float16))
 
     def _refresh_target_h(self):
         if self.target_h is not None:
@@ -367,6 +381,7 @@ class BatchedDQN:
         agent = 0 if self.shared else agent
         self.params[agent].copy_(torch.from_numpy(keras_to_kernel(flat, self.H)))
         self.target[agent].copy_(self.params[agent])
+        self._refresh_params_h()
         self._refresh_target_h()
 
     def state_dict(self):
@@ -378,6 +393,7 @@ class BatchedDQN:
     def load_state_dict(self, sd):
         for k in ["params", "target", "adam_m", "adam_v"]:
             getattr(self, k).copy_(sd[k].to(self.device))
+        self._refresh_params_h()
         self._refresh_target_h()
         self.learn_step_counter = int(sd["learn_step_counter"])
         self.global_step_count = int(sd["global_step_count"])

@@ -7,7 +7,8 @@ This module keeps that naming for the exported weights and adds what a resume
 needs, so that load + K steps reproduces an uninterrupted run bit-exactly
 (every kernel on the path is deterministic):
 
-  nets      params / target (+ its f16 shadow) / Adam m, v, learn counters
+  nets      params / target (+ its f16 shadow) / Adam m, v, learn counters;
+            the online net's f16 copy is rebuilt from params on load
   replay    the filled part of every ring + the host counter
   streams   both device MT19937 streams per env (numpy act stream, CPython
             sample stream)
@@ -94,6 +95,7 @@ def load(path, tr):
     env.t, env.episode = c["env_t"], c["env_episode"]
     tr.episode, tr.step_count, tr.total_steps = c["episode"], c["step_count"], c["total_steps"]
     ag.ring.total = c["ring_total"]
+    ag._refresh_params_h()  # the f16 online copy is derived, not stored
     if "replay" in st:
         n = st["replay"]["s"].shape[1]
         for k, v in st["replay"].items():

@@ -806,6 +806,7 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
     const float *Wp = a.params;
     const _Float16 *TH = a.target_h ? reinterpret_cast<const _Float16 *>(a.target_h) : nullptr;
+    const _Float16 *WH = reinterpret_cast<const _Float16 *>(a.params_h);
     Frags fr;
     stage_out(Wp, W3L, B3L);
     if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
@@ -834,8 +835,8 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
         }
         __syncthreads();
         // buffer plan of k_learn_f16: the backward runs on (P1, P2) = (R2, R1)
-        forward_x<true>(fr, tg, R2, R1, R1, S.z3, [Wp](Frags &f) { load_w1(Wp, f); },
-                        [Wp](Frags &f) { load_w2(Wp, f); });  // X(S') stays in R2
+        forward_x<true>(fr, tg, R2, R1, R1, S.z3, [WH](Frags &f) { load_w1(WH, f); },
+                        [WH](Frags &f) { load_w2(WH, f); });  // X(S') stays in R2
         float *qo = (float *)DQ;
         Rows gs;
         forward_x<false>(fr, on, R2, R1, R2, qo,
@@ -931,7 +932,8 @@ __global__ void __launch_bounds__(256) k_reduce_slabs(const float *slab, int nw,
 // Keras-3 Adam over n flat parameters (A-11) with g = gscale * grad; on a
 // target sync also writes the target copy and its f16 shadow.
 __global__ void __launch_bounds__(256) k_adam(float *W, float *M, float *V, float *T,
-                                              _Float16 *TH, const float *G, int n, float gscale,
+                                              _Float16 *TH, _Float16 *WH, const float *G, int n,
+                                              float gscale,
                                               float alpha, float c1, float c2, float eps, int sync) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
@@ -943,6 +945,7 @@ __global__ void __launch_bounds__(256) k_adam(float *W, float *M, float *V, floa
     M[i] = m;
     V[i] = v;
     W[i] = w;
+    if (WH) WH[i] = (_Float16)w;
     if (sync) {
         T[i] = w;
         if (TH) TH[i] = (_Float16)w;
@@ -973,7 +976,7 @@ extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, i
                   "dmdqn_learn_shared_grad: fp16 precision with hidden=128 (P=%d) only",
                   f16k::L::P);
     DMDQN_REQUIRE(a->ring_s && a->ring_n && a->ring_a && a->ring_d && a->ring_r && a->idx &&
-                      a->params && a->target,
+                      a->params && a->target && a->params_h,
                   "dmdqn_learn_shared_grad: null array");
     DMDQN_REQUIRE(n_slabs >= 1, "dmdqn_learn_shared_grad: n_slabs must be >= 1");
     hipStream_t s = as_stream(stream);
@@ -990,12 +993,14 @@ extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, i
 }
 
 extern "C" int dmdqn_adam(float *params, float *adam_m, float *adam_v, float *target,
-                          uint16_t *target_h, const float *grad, int n, float gscale, float alpha,
-                          float c1, float c2, float eps, int sync, void *stream) {
+                          uint16_t *target_h, uint16_t *params_h, const float *grad, int n,
+                          float gscale, float alpha, float c1, float c2, float eps, int sync,
+                          void *stream) {
     DMDQN_REQUIRE(params && adam_m && adam_v && grad && n > 0, "dmdqn_adam: bad args");
     DMDQN_REQUIRE(!sync || target, "dmdqn_adam: target required on a sync");
     hipLaunchKernelGGL(k_adam, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), params,
-                       adam_m, adam_v, target, reinterpret_cast<_Float16 *>(target_h), grad, n,
+                       adam_m, adam_v, target, reinterpret_cast<_Float16 *>(target_h),
+                       reinterpret_cast<_Float16 *>(params_h), grad, n,
                        gscale, alpha, c1, c2, eps, sync);
     DMDQN_LAUNCH_CHECK("k_adam");
     return DMDQN_OK;

@@ -185,6 +185,11 @@ typedef struct dmdqn_learn_args {
                                         sum Q(S)^2 over the batch's 128x4
                                         online values, counts of actions 0..3
                                         (dqn_agent.py:361-363); zero it first */
+    uint16_t *params_h;              /* shared net only (dmdqn_learn_shared_grad,
+                                        required there): [Ph] f16 copy of the
+                                        online net (Keras' f16 cast of the f32
+                                        variables) the forwards read; dmdqn_adam
+                                        rewrites it.  Ignored by dmdqn_learn. */
 } dmdqn_learn_args;
 
 int dmdqn_learn(const dmdqn_learn_args *args, void *stream);
@@ -216,11 +221,12 @@ int dmdqn_learn_shared_grad(const dmdqn_learn_args *args, float *slab, int n_sla
                             float scale, void *stream);
 
 /* Keras-3 Adam (dqn_agent.py:357, A-11) on n flat parameters with gradient
- * gscale * grad[i]; sync != 0 also copies params to target (and its f16 shadow
- * target_h, when not NULL) -- the hard target sync of dqn_agent.py:376-387. */
+ * gscale * grad[i]; params_h (when not NULL) receives the f16 copy of every
+ * updated parameter; sync != 0 also copies params to target (and its f16
+ * shadow target_h, when not NULL) -- the hard target sync of dqn_agent.py:376-387. */
 int dmdqn_adam(float *params, float *adam_m, float *adam_v, float *target, uint16_t *target_h,
-               const float *grad, int n, float gscale, float alpha, float c1, float c2, float eps,
-               int sync, void *stream);
+               uint16_t *params_h, const float *grad, int n, float gscale, float alpha, float c1,
+               float c2, float eps, int sync, void *stream);
 
 #ifdef __cplusplus
 }

@@ -73,7 +73,7 @@ def _shared_worker(rank, ws, port, q):
     fake = SimpleNamespace(NA=4, n_slabs=2, P=P, device="cpu",
                            slab=torch.zeros((2, P)), grad=torch.zeros(P),
                            params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
-                           target=torch.zeros(P), target_h=None)
+                           target=torch.zeros(P), target_h=None, params_h=None)
     seen = {}
 
     def fake_call(name, *args):
@@ -82,8 +82,8 @@ def _shared_worker(rank, ws, port, q):
             seen["scale"] = args[4].value
         elif name == "dmdqn_adam":
             seen["grad"] = fake.grad.tolist()
-            seen["gscale"] = args[7].value
-            seen["sync"] = args[12]
+            seen["gscale"] = args[8].value
+            seen["sync"] = args[13]
         return 0
 
     AG.call, AG.stream_of = fake_call, (lambda *a: None)

@@ -103,6 +103,7 @@ def test_shared_many_agents_across_slabs():
     # are split over slabs: recompute (pre-Adam weights) with a single slab
     g1 = ag.grad.clone()
     ag.params.copy_(p0)
+    ag._refresh_params_h()
     from dmdqn_amd._lib import call, ptr, stream_of
     import ctypes as C
     slab1 = torch.empty((1, ag.P), dtype=torch.float32, device=DEV)

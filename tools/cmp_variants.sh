@@ -1,5 +1,6 @@
 # A/B kernel variants in one GPU call (same box):
 #   bash tools/cmp_variants.sh "-DFOO" "-DBAR=2" "file:tools/_base_learn_f16.hip"
+# BENCH_ARGS (env) is appended to the bench command line.
 # A "file:" variant builds with that file in place of csrc/learn_f16.hip.
 set -e
 SRC=dmdqn_amd/csrc/learn_f16.hip
@@ -11,6 +12,6 @@ for v in "$@"; do
     cp /tmp/_cur_learn_f16.hip $SRC; flags="$v"
   fi
   DMDQN_EXTRA_FLAGS="$flags -DDMDQN_VARIANT" python3 -m dmdqn_amd.build > gpurun_out/build.log 2>&1
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(\"$v\", d[\"value\"], d[\"roofline\"][\"avg_launch_ms\"], d[\"roofline\"][\"frac\"])"
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline $BENCH_ARGS | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(\"$v\", d[\"value\"], d[\"roofline\"][\"avg_launch_ms\"], d[\"roofline\"][\"frac\"])"
 done
 cp /tmp/_cur_learn_f16.hip $SRC
