@@ -78,6 +78,43 @@ __device__ __forceinline__ half8 frag_tr(const _Float16 *img, int ld, int r0, in
     return r;
 }
 
+// The [128][128] activation images (H1, H2, dZ2, dZ1, the W2^T image) are
+// stored in 8-row x 32-column blocks of 512 B (a band of 8 rows is 2 KB),
+// row r's 16-byte chunks within a block XOR-permuted by 2*((r>>3)&1):
+//   * row-fragment reads (ds_read_b128 of rows r0..r0+15, chunk 4s+lg): each
+//     16-lane bank group {0-3,12-15 | 20-27} covers all 16 bank slots;
+//   * transposed reads (ds_read_b64_tr_b16 of rows r0+8g+q, chunks 2c..2c+1):
+//     each 32-lane half covers all 32 eight-byte slots;
+// so both are conflict-free (the plain 256-B rows were 8-way on both), and
+// every address is a lane constant plus an immediate.
+__device__ __forceinline__ int hoff(int r, int c) {
+    const int ch = c >> 3;
+    return 1024 * (r >> 3) + 256 * (ch >> 2) + 32 * (r & 7) + 8 * ((ch & 3) ^ ((r >> 2) & 2)) +
+           (c & 7);
+}
+
+// frag_row on a blocked image (r0 a multiple of 16, k0 of 32).
+__device__ __forceinline__ half8 frag_row_h(const _Float16 *img, int r0, int k0) {
+    const int l = threadIdx.x & 63;
+    return *reinterpret_cast<const half8 *>(img + hoff(r0 + (l & 15), k0 + 8 * (l >> 4)));
+}
+
+// frag_tr on a blocked image (r0 a multiple of 8, c0 of 16); rows +4 share
+// the row's permutation and sit 128 elements further.
+__device__ __forceinline__ half8 frag_tr_h(const _Float16 *img, int r0, int c0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const _Float16 *p0 = img + hoff(r0 + 8 * g + (i >> 2), c0 + 4 * (i & 3));
+    v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)p0);
+    v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(p0 + 128));
+    half8 r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        r[e] = __builtin_bit_cast(_Float16, (short)t0[e]);
+        r[e + 4] = __builtin_bit_cast(_Float16, (short)t1[e]);
+    }
+    return r;
+}
+
 // A-fragment of a transposed f32 weight matrix WT[N][ld] straight from HBM:
 // WT[n0 + (l&15)][k0 + 8(l>>4) + e] -> f16.  nvalid masks padded rows.
 __device__ __forceinline__ half8 wfrag(const float *WT, int ld, int n0, int k0, int nvalid = 16) {
@@ -217,7 +254,7 @@ __device__ void forward_x(Frags &f, const OutL o, const _Float16 *X, _Float16 *H
         f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row(X, DP, 16 * t, 32 * s), c);
-        *reinterpret_cast<half4v *>(H1b + (16 * t + lr) * H + n) = relu_h4(c, f.b1);
+        *reinterpret_cast<half4v *>(H1b + hoff(16 * t + lr, n)) = relu_h4(c, f.b1);
     }
     after_l1(f);
     __syncthreads();
@@ -227,7 +264,7 @@ __device__ void forward_x(Frags &f, const OutL o, const _Float16 *X, _Float16 *H
         for (int t = 0; t < 8; t++) {
             f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row(H1b, H, 16 * t, 32 * s), c);
+            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row_h(H1b, 16 * t, 32 * s), c);
             acc[t] = c;
         }
         const float4 b2 = f.b2;
@@ -235,14 +272,14 @@ __device__ void forward_x(Frags &f, const OutL o, const _Float16 *X, _Float16 *H
         __syncthreads();  // every wave has read H1
 #pragma unroll
         for (int t = 0; t < 8; t++)
-            *reinterpret_cast<half4v *>(H2b + (16 * t + lr) * H + n) = relu_h4(acc[t], b2);
+            *reinterpret_cast<half4v *>(H2b + hoff(16 * t + lr, n)) = relu_h4(acc[t], b2);
     } else {
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row(H1b, H, 16 * t, 32 * s), c);
-            *reinterpret_cast<half4v *>(H2b + (16 * t + lr) * H + n) = relu_h4(c, f.b2);
+            for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row_h(H1b, 16 * t, 32 * s), c);
+            *reinterpret_cast<half4v *>(H2b + hoff(16 * t + lr, n)) = relu_h4(c, f.b2);
         }
         after_l2(f);
     }
@@ -257,7 +294,7 @@ __device__ void forward_x(Frags &f, const OutL o, const _Float16 *X, _Float16 *H
             else
 #pragma unroll
                 for (int e = 0; e < 8; e++) a3[e] = (_Float16)0.0f;
-            acc = mfma(a3, frag_row(H2b, H, 16 * w, 32 * s), acc);
+            acc = mfma(a3, frag_row_h(H2b, 16 * w, 32 * s), acc);
         }
         if (lg == 0) {
             float4 q;
@@ -544,7 +581,7 @@ __device__ __forceinline__ void loss_dq(const dmdqn_learn_args &a, int agent, _F
 __device__ __forceinline__ void bwd_dz2(_Float16 *R2, const OutL on, const Scratch &S) {
     for (int t = threadIdx.x; t < B_ * (H / 8); t += 512) {
         const int b = t >> 4, k8 = (t & 15) * 8, ac = S.act[b];
-        half8 *p = reinterpret_cast<half8 *>(R2 + b * H + k8);
+        half8 *p = reinterpret_cast<half8 *>(R2 + hoff(b, k8));
         half8 h = *p, o;
         const half8 wv = *reinterpret_cast<const half8 *>(on.w3 + ac * H + k8);
         const float dq = S.dq[b];
@@ -559,11 +596,10 @@ __device__ __forceinline__ void bwd_dz2(_Float16 *R2, const OutL on, const Scrat
 // ReLU mask of H1 (R1) as bits: mask[b][j/32] (128 x 4 words).
 __device__ __forceinline__ void h1_mask(const _Float16 *R1, uint32_t *mask) {
     const int tid = threadIdx.x, b = tid >> 2, q = tid & 3;
-    const half8 *hp = reinterpret_cast<const half8 *>(R1 + b * H + 32 * q);
     uint32_t bits = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-        const half8 hv = hp[c];
+        const half8 hv = *reinterpret_cast<const half8 *>(R1 + hoff(b, 32 * q + 8 * c));
 #pragma unroll
         for (int e = 0; e < 8; e++) bits |= ((float)hv[e] > 0.0f ? 1u : 0u) << (8 * c + e);
     }
@@ -578,7 +614,7 @@ __device__ __forceinline__ void w2t_image(_Float16 *R1, const Frags &fr) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
 #pragma unroll
     for (int s2 = 0; s2 < 4; s2++)
-        *reinterpret_cast<half8 *>(R1 + (16 * w + lr) * H + 32 * s2 + 8 * lg) = fr.w2[s2];
+        *reinterpret_cast<half8 *>(R1 + hoff(16 * w + lr, 32 * s2 + 8 * lg)) = fr.w2[s2];
 }
 
 __device__ __forceinline__ void bwd_dh1_from_image(const _Float16 *R1, const _Float16 *R2,
@@ -588,9 +624,9 @@ __device__ __forceinline__ void bwd_dh1_from_image(const _Float16 *R1, const _Fl
     for (int t = 0; t < 8; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s2 = 0; s2 < 4; s2++) {
-        const half8 av = frag_tr(R1, H, 32 * s2, 16 * w);
+        const half8 av = frag_tr_h(R1, 32 * s2, 16 * w);
 #pragma unroll
-        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(R2, H, 16 * t, 32 * s2), d1[t]);
+        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row_h(R2, 16 * t, 32 * s2), d1[t]);
     }
     __syncthreads();
 }
@@ -600,15 +636,15 @@ __device__ __forceinline__ void bwd_dh1(_Float16 *R1, const _Float16 *R2, const 
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
 #pragma unroll
     for (int s2 = 0; s2 < 4; s2++)
-        *reinterpret_cast<half8 *>(R1 + (16 * w + lr) * H + 32 * s2 + 8 * lg) = fr.w2[s2];
+        *reinterpret_cast<half8 *>(R1 + hoff(16 * w + lr, 32 * s2 + 8 * lg)) = fr.w2[s2];
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < 8; t++) d1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s2 = 0; s2 < 4; s2++) {
-        const half8 av = frag_tr(R1, H, 32 * s2, 16 * w);
+        const half8 av = frag_tr_h(R1, 32 * s2, 16 * w);
 #pragma unroll
-        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row(R2, H, 16 * t, 32 * s2), d1[t]);
+        for (int t = 0; t < 8; t++) d1[t] = mfma(av, frag_row_h(R2, 16 * t, 32 * s2), d1[t]);
     }
     __syncthreads();
 }
@@ -624,7 +660,7 @@ __device__ __forceinline__ void bwd_dz1(_Float16 *R1, const uint32_t *mask, cons
         half4v o;
 #pragma unroll
         for (int e = 0; e < 4; e++) o[e] = ((bits >> e) & 1u) ? (_Float16)d1[t][e] : (_Float16)0.0f;
-        *reinterpret_cast<half4v *>(R1 + b * H + j) = o;
+        *reinterpret_cast<half4v *>(R1 + hoff(b, j)) = o;
     }
 }
 
@@ -717,7 +753,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
             half8 dqf = frag_tr(DQ, 16, b0, 0);
-            acc = mfma(frag_tr(P2, H, b0, 16 * w), dqf, acc);
+            acc = mfma(frag_tr_h(P2, b0, 16 * w), dqf, acc);
             gb = mfma(ones, dqf, gb);  // every wave (no MFMA under divergent control)
         }
         if (lr < NACT) {
@@ -738,10 +774,10 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         for (int t = 0; t < 8; t++) g2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 av = frag_tr(P1, H, b0, 16 * w);
-            gb = mfma(ones, frag_tr(P2, H, b0, 16 * w), gb);
+            const half8 av = frag_tr_h(P1, b0, 16 * w);
+            gb = mfma(ones, frag_tr_h(P2, b0, 16 * w), gb);
 #pragma unroll
-            for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr(P2, H, b0, 16 * t), g2[t]);
+            for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr_h(P2, b0, 16 * t), g2[t]);
         }
         // H1 fully consumed (dW2, mask): P1 becomes the W2^T image now, from
         // the register copy of old W2 (fr.w2), which is then dead during Adam
@@ -772,7 +808,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         for (int t = 0; t < 6; t++) g1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 bv = frag_tr(P1, H, b0, 16 * w);
+            const half8 bv = frag_tr_h(P1, b0, 16 * w);
             gb = mfma(ones, bv, gb);
 #pragma unroll
             for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr(P2, DP, b0, 16 * t), bv, g1[t]);
@@ -850,7 +886,7 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
             const half8 dqf = frag_tr(DQ, 16, b0, 0);
-            G3 = mfma(frag_tr(P2, H, b0, 16 * w), dqf, G3);
+            G3 = mfma(frag_tr_h(P2, b0, 16 * w), dqf, G3);
             GB3 = mfma(ones, dqf, GB3);
         }
         __syncthreads();
@@ -861,14 +897,14 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
             half8 av[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                av[q] = frag_tr(P1, H, 32 * q, 16 * w);
-                GB2 = mfma(ones, frag_tr(P2, H, 32 * q, 16 * w), GB2);
+                av[q] = frag_tr_h(P1, 32 * q, 16 * w);
+                GB2 = mfma(ones, frag_tr_h(P2, 32 * q, 16 * w), GB2);
             }
 #pragma unroll
             for (int t = 0; t < 8; t++) {
                 f32x4 c = G2L[(w * 8 + t) * 64 + l];
 #pragma unroll
-                for (int q = 0; q < 4; q++) c = mfma(av[q], frag_tr(P2, H, 32 * q, 16 * t), c);
+                for (int q = 0; q < 4; q++) c = mfma(av[q], frag_tr_h(P2, 32 * q, 16 * t), c);
                 G2L[(w * 8 + t) * 64 + l] = c;
             }
         }
@@ -885,7 +921,7 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
         // dW1 / db1
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 bv = frag_tr(P1, H, b0, 16 * w);
+            const half8 bv = frag_tr_h(P1, b0, 16 * w);
             GB1 = mfma(ones, bv, GB1);
 #pragma unroll
             for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr(P2, DP, b0, 16 * t), bv, G1[t]);
