@@ -78,32 +78,38 @@ __device__ __forceinline__ half8 frag_tr(const _Float16 *img, int ld, int r0, in
     return r;
 }
 
-// The [128][128] activation images (H1, H2, dZ2, dZ1, the W2^T image) are
-// stored in 8-row x 32-column blocks of 512 B (a band of 8 rows is 2 KB),
+// The activation images -- [128][128] H1, H2, dZ2, dZ1, the W2^T image and
+// the [128][96] X -- are stored in 8-row x 32-column blocks of 512 B (a band
+// of 8 rows is LD/32 blocks, a multiple of 256 B),
 // row r's 16-byte chunks within a block XOR-permuted by 2*((r>>3)&1):
 //   * row-fragment reads (ds_read_b128 of rows r0..r0+15, chunk 4s+lg): each
 //     16-lane bank group {0-3,12-15 | 20-27} covers all 16 bank slots;
 //   * transposed reads (ds_read_b64_tr_b16 of rows r0+8g+q, chunks 2c..2c+1):
 //     each 32-lane half covers all 32 eight-byte slots;
 // so both are conflict-free (the plain 256-B rows were 8-way on both), and
-// every address is a lane constant plus an immediate.
+// every address is a lane constant plus an immediate.  (The 2-way conflicts
+// of the 192-B X rows go too.)
+template <int LD = H>
 __device__ __forceinline__ int hoff(int r, int c) {
+    static_assert(LD % 32 == 0, "whole blocks per band");
     const int ch = c >> 3;
-    return 1024 * (r >> 3) + 256 * (ch >> 2) + 32 * (r & 7) + 8 * ((ch & 3) ^ ((r >> 2) & 2)) +
+    return 8 * LD * (r >> 3) + 256 * (ch >> 2) + 32 * (r & 7) + 8 * ((ch & 3) ^ ((r >> 2) & 2)) +
            (c & 7);
 }
 
 // frag_row on a blocked image (r0 a multiple of 16, k0 of 32).
+template <int LD = H>
 __device__ __forceinline__ half8 frag_row_h(const _Float16 *img, int r0, int k0) {
     const int l = threadIdx.x & 63;
-    return *reinterpret_cast<const half8 *>(img + hoff(r0 + (l & 15), k0 + 8 * (l >> 4)));
+    return *reinterpret_cast<const half8 *>(img + hoff<LD>(r0 + (l & 15), k0 + 8 * (l >> 4)));
 }
 
 // frag_tr on a blocked image (r0 a multiple of 8, c0 of 16); rows +4 share
 // the row's permutation and sit 128 elements further.
+template <int LD = H>
 __device__ __forceinline__ half8 frag_tr_h(const _Float16 *img, int r0, int c0) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    const _Float16 *p0 = img + hoff(r0 + 8 * g + (i >> 2), c0 + 4 * (i & 3));
+    const _Float16 *p0 = img + hoff<LD>(r0 + 8 * g + (i >> 2), c0 + 4 * (i & 3));
     v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)p0);
     v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(p0 + 128));
     half8 r;
@@ -253,7 +259,7 @@ __device__ void forward_x(Frags &f, const OutL o, const _Float16 *X, _Float16 *H
     for (int t = 0; t < 8; t++) {
         f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row(X, DP, 16 * t, 32 * s), c);
+        for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row_h<DP>(X, 16 * t, 32 * s), c);
         *reinterpret_cast<half4v *>(H1b + hoff(16 * t + lr, n)) = relu_h4(c, f.b1);
     }
     after_l1(f);
@@ -472,7 +478,7 @@ __device__ __forceinline__ void gather_commit(_Float16 *R2, const Rows &g) {
             hv[e] = (_Float16)(float)(int8_t)(g.v[i].x >> (8 * e));
             hv[e + 4] = (_Float16)(float)(int8_t)(g.v[i].y >> (8 * e));
         }
-        *reinterpret_cast<half8 *>(R2 + b * DP + 8 * q) = hv;
+        *reinterpret_cast<half8 *>(R2 + hoff<DP>(b, 8 * q)) = hv;
     }
 }
 
@@ -811,7 +817,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
             const half8 bv = frag_tr_h(P1, b0, 16 * w);
             gb = mfma(ones, bv, gb);
 #pragma unroll
-            for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr(P2, DP, b0, 16 * t), bv, g1[t]);
+            for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr_h<DP>(P2, b0, 16 * t), bv, g1[t]);
         }
         // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; padded
         // features 89..95 have zero weight and zero gradient and stay zero
@@ -924,7 +930,7 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
             const half8 bv = frag_tr_h(P1, b0, 16 * w);
             GB1 = mfma(ones, bv, GB1);
 #pragma unroll
-            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr(P2, DP, b0, 16 * t), bv, G1[t]);
+            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr_h<DP>(P2, b0, 16 * t), bv, G1[t]);
         }
         __syncthreads();  // P1 / P2 / scratch are rewritten by the next agent
     }
