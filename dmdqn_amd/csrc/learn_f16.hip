@@ -81,20 +81,23 @@ __device__ __forceinline__ half8 frag_tr(const _Float16 *img, int ld, int r0, in
 // The activation images -- [128][128] H1, H2, dZ2, dZ1, the W2^T image and
 // the [128][96] X -- are stored in 8-row x 32-column blocks of 512 B (a band
 // of 8 rows is LD/32 blocks, a multiple of 256 B),
-// row r's 16-byte chunks within a block XOR-permuted by 2*((r>>3)&1):
+// row r's 16-byte chunks within a block XOR-permuted by bit 1 and bit 3 of r
+// (a search over the linear permutations of row bits 0, 1, 3):
 //   * row-fragment reads (ds_read_b128 of rows r0..r0+15, chunk 4s+lg): each
 //     16-lane bank group {0-3,12-15 | 20-27} covers all 16 bank slots;
 //   * transposed reads (ds_read_b64_tr_b16 of rows r0+8g+q, chunks 2c..2c+1):
 //     each 32-lane half covers all 32 eight-byte slots;
-// so both are conflict-free (the plain 256-B rows were 8-way on both), and
+// so both are conflict-free (the plain 256-B rows were 8-way on both), the
+// 8-byte MFMA-output stores are 2-way (the least any permutation of whole
+// 16-byte chunks allows for 16 rows at one column), and
 // every address is a lane constant plus an immediate.  (The 2-way conflicts
 // of the 192-B X rows go too.)
 template <int LD = H>
 __device__ __forceinline__ int hoff(int r, int c) {
     static_assert(LD % 32 == 0, "whole blocks per band");
     const int ch = c >> 3;
-    return 8 * LD * (r >> 3) + 256 * (ch >> 2) + 32 * (r & 7) + 8 * ((ch & 3) ^ ((r >> 2) & 2)) +
-           (c & 7);
+    return 8 * LD * (r >> 3) + 256 * (ch >> 2) + 32 * (r & 7) +
+           8 * ((ch & 3) ^ (((r >> 1) & 1) | ((r >> 2) & 2))) + (c & 7);
 }
 
 // frag_row on a blocked image (r0 a multiple of 16, k0 of 32).
