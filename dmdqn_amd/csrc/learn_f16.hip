@@ -374,10 +374,23 @@ __device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, c
 // Each batch's loads are pinned together by a scheduling barrier (without it
 // the scheduler, under the 128-VGPR cap, sinks loads to their uses).  Measured
 // (one box): W2 4x2 + W1 2x3 tiles, 4.18 ms vs 4.36 ms for the plain order.
-template <int NB, int NT, typename Index>
+// `grad()` runs after the first batch's loads are issued and produces g[]:
+// the w, m, v loads do not depend on the gradient, so their latency hides
+// behind the gradient MFMAs.
+// Issue the first Adam batch before the gradient MFMAs: for W1 (measured
+// 1-2 % faster); not for W2, where the 24 extra live VGPRs next to the dW2
+// accumulators and the W2 fragments spill (10 -> 28) and cost 10 %.
+#ifndef DMDQN_EARLY_W2
+#define DMDQN_EARLY_W2 0
+#endif
+#ifndef DMDQN_EARLY_W1
+#define DMDQN_EARLY_W1 1
+#endif
+template <int NB, int NT, bool EARLY, typename Index, typename Grad>
 __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T, Index ix,
-                                          const f32x4 *g, const AdamC &k) {
+                                          const f32x4 *g, const AdamC &k, Grad grad) {
     float4 w[2][NT], m[2][NT], v[2][NT];
+    if constexpr (!EARLY) grad();
 #pragma unroll
     for (int q = 0; q < NT; q++) {
         const size_t i = ix(q);
@@ -386,6 +399,10 @@ __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T
         v[0][q] = *reinterpret_cast<const float4 *>(V + i);
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (EARLY) {
+        grad();
+        __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int h = 0; h < NB; h++) {
         const int c = h & 1, n = c ^ 1;
@@ -779,23 +796,25 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     // ---- dW2[j][k] = H1^T . dZ2 (wave w: j-tile w, 8 k-tiles) ; db2 (k-tile w) ; Adam
     {
         f32x4 g2[8], gb = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 8; t++) g2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 av = frag_tr_h(P1, b0, 16 * w);
-            gb = mfma(ones, frag_tr_h(P2, b0, 16 * w), gb);
-#pragma unroll
-            for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr_h(P2, b0, 16 * t), g2[t]);
-        }
-        // H1 fully consumed (dW2, mask): P1 becomes the W2^T image now, from
-        // the register copy of old W2 (fr.w2), which is then dead during Adam
-        __syncthreads();
-        w2t_image(P1, fr);
         // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3]
-        adam_pipe<4, 2>(Wp, Mp, Vp, Tp,
-                        [&](int t) { return (size_t)L::oW2T + (size_t)(16 * t + lr) * H + 16 * w + 4 * lg; },
-                        g2, AK);
+        adam_pipe<4, 2, DMDQN_EARLY_W2>(
+            Wp, Mp, Vp, Tp,
+            [&](int t) { return (size_t)L::oW2T + (size_t)(16 * t + lr) * H + 16 * w + 4 * lg; }, g2,
+            AK, [&]() {
+#pragma unroll
+                for (int t = 0; t < 8; t++) g2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int b0 = 0; b0 < B_; b0 += 32) {
+                    const half8 av = frag_tr_h(P1, b0, 16 * w);
+                    gb = mfma(ones, frag_tr_h(P2, b0, 16 * w), gb);
+#pragma unroll
+                    for (int t = 0; t < 8; t++) g2[t] = mfma(av, frag_tr_h(P2, b0, 16 * t), g2[t]);
+                }
+                // H1 fully consumed (dW2, mask): P1 becomes the W2^T image now,
+                // from the register copy of old W2 (fr.w2), dead during Adam
+                __syncthreads();
+                w2t_image(P1, fr);
+            });
         if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob2 + 16 * w + lr, gb[0], AK);
     }
     __syncthreads();  // W2^T image complete
@@ -813,21 +832,23 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
     {
         f32x4 g1[6], gb = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 6; t++) g1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 bv = frag_tr_h(P1, b0, 16 * w);
-            gb = mfma(ones, bv, gb);
-#pragma unroll
-            for (int t = 0; t < 6; t++) g1[t] = mfma(frag_tr_h<DP>(P2, b0, 16 * t), bv, g1[t]);
-        }
         // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; padded
         // features 89..95 have zero weight and zero gradient and stay zero
-        adam_pipe<2, 3>(
+        adam_pipe<2, 3, DMDQN_EARLY_W1>(
             Wp, Mp, Vp, Tp,
             [&](int t) { return (size_t)L::oW1T + (size_t)(16 * w + lr) * DP + 16 * t + 4 * lg; }, g1,
-            AK);
+            AK, [&]() {
+#pragma unroll
+                for (int t = 0; t < 6; t++) g1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int b0 = 0; b0 < B_; b0 += 32) {
+                    const half8 bv = frag_tr_h(P1, b0, 16 * w);
+                    gb = mfma(ones, bv, gb);
+#pragma unroll
+                    for (int t = 0; t < 6; t++)
+                        g1[t] = mfma(frag_tr_h<DP>(P2, b0, 16 * t), bv, g1[t]);
+                }
+            });
         if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob1 + 16 * w + lr, gb[0], AK);
     }
     if (a.stamps) {
