@@ -72,6 +72,25 @@ def n_params(hidden, n_actions=N_ACTIONS):
     return H * D_PAD + H * H + n_actions * H + 2 * H + n_actions
 
 
+def tile_wt(WT):
+    """[..., N, K] row-major W^T -> [..., N*K] tiled device order (qnet_layout.hpp
+    qn_wt): 16 x 16 tiles in row-major tile order, each [K%16 / 8][N%16][K%8]."""
+    lead, (N, K) = WT.shape[:-2], WT.shape[-2:]
+    t = WT.reshape(lead + (N // 16, 16, K // 16, 2, 8))
+    n = len(lead)
+    t = np.moveaxis(t, [n + 0, n + 2, n + 3, n + 1, n + 4], list(range(n, n + 5)))
+    return t.reshape(lead + (N * K,))
+
+
+def untile_wt(flat, N, K):
+    """Inverse of tile_wt: [..., N*K] tiled -> [..., N, K] row-major."""
+    lead = flat.shape[:-1]
+    n = len(lead)
+    t = flat.reshape(lead + (N // 16, K // 16, 2, 16, 8))
+    t = np.moveaxis(t, list(range(n, n + 5)), [n + 0, n + 2, n + 3, n + 1, n + 4])
+    return t.reshape(lead + (N, K))
+
+
 def keras_to_kernel(flat, hidden):
     """[..., P_keras] Keras get_weights order -> [..., P_kernel] device layout."""
     H = hidden
@@ -86,7 +105,7 @@ def keras_to_kernel(flat, hidden):
     b3 = flat[..., o:o + N_ACTIONS]
     W1T = np.zeros(lead + (H, D_PAD), np.float32)
     W1T[..., :D_IN] = np.swapaxes(W1, -1, -2)
-    parts = [W1T.reshape(lead + (-1,)), np.swapaxes(W2, -1, -2).reshape(lead + (-1,)),
+    parts = [tile_wt(W1T), tile_wt(np.swapaxes(W2, -1, -2)),
              np.swapaxes(W3, -1, -2).reshape(lead + (-1,)), b1, b2, b3]
     return np.concatenate(parts, axis=-1)
 
@@ -97,8 +116,8 @@ def kernel_to_keras(flat, hidden):
     flat = np.asarray(flat, dtype=np.float32)
     lead = flat.shape[:-1]
     o = 0
-    W1T = flat[..., o:o + H * D_PAD].reshape(lead + (H, D_PAD)); o += H * D_PAD
-    W2T = flat[..., o:o + H * H].reshape(lead + (H, H)); o += H * H
+    W1T = untile_wt(flat[..., o:o + H * D_PAD], H, D_PAD); o += H * D_PAD
+    W2T = untile_wt(flat[..., o:o + H * H], H, H); o += H * H
     W3T = flat[..., o:o + N_ACTIONS * H].reshape(lead + (N_ACTIONS, H)); o += N_ACTIONS * H
     b1 = flat[..., o:o + H]; o += H
     b2 = flat[..., o:o + H]; o += H

@@ -54,7 +54,7 @@ struct Scratch {
 };
 
 // Y[b][n] = act(X[b][:] . W[:][n] + bias[n]) for the wave's 16-column tile.
-// X rows come from LDS (f16 or f32), W^T [N][KS] from global memory.
+// X rows come from LDS (f16 or f32), W^T [N][KS] (tiled, qn_wt) from global memory.
 template <int H, int K, typename TX, bool RELU, int KS>
 __device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *WT, const float *bias,
                                            float *Y, int ldy, int n0, int nvalid) {
@@ -65,7 +65,7 @@ __device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *WT
     const int n = n0 + lr;
     for (int k0 = 0; k0 < K; k0 += 4) {
         const int kk = k0 + lk;
-        const float bv = (kk < K && lr < nvalid) ? WT[(size_t)n * KS + kk] : 0.0f;
+        const float bv = (kk < K && lr < nvalid) ? WT[qn_wt(n, kk, KS)] : 0.0f;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const float av = (float)X[(16 * t + lr) * ldx + kk];
@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
             const int k = k0 + lk;
             const float av = H2[(16 * w + lr) * H + k];
 #pragma unroll
-            for (int t = 0; t < NT; t++) d1[t] = mfma4(av, W2T[(size_t)k * H + 16 * t + lr], d1[t]);
+            for (int t = 0; t < NT; t++) d1[t] = mfma4(av, W2T[qn_wt(k, 16 * t + lr, H)], d1[t]);
         }
     }
     __syncthreads();  // everyone done reading H1 (dW2) and old W2 (dH1)
@@ -342,7 +342,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
             for (int t = 0; t < NT; t++)
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    size_t i = L::oW2T + (size_t)(16 * t + lr) * H + 16 * jt + 4 * lk + j;
+                    size_t i = L::oW2T + qn_wt(16 * t + lr, 16 * jt + 4 * lk + j, H);
                     adam_el(Wp, Mp, Vp, Tp, i, g2[q][t][j], AK, sync);
                 }
     }
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     int i = 16 * t + 4 * lk + j;
-                    if (i < D_) adam_el(Wp, Mp, Vp, Tp, L::oW1T + (size_t)(16 * jt + lr) * QN_DP + i,
+                    if (i < D_) adam_el(Wp, Mp, Vp, Tp, L::oW1T + qn_wt(16 * jt + lr, i, QN_DP),
                                         g1[t][j], AK, sync);
                 }
         }
@@ -400,14 +400,14 @@ __global__ void __launch_bounds__(256) k_q_argmax(const float *params, size_t ps
     __syncthreads();
     for (int j = tid; j < H; j += blockDim.x) {
         float s = 0.0f;
-        for (int i = 0; i < D_; i++) s += x[i] * Wp[L::oW1T + j * QN_DP + i];
+        for (int i = 0; i < D_; i++) s += x[i] * Wp[L::oW1T + qn_wt(j, i, QN_DP)];
         s += Wp[L::ob1 + j];
         h1[j] = s > 0.0f ? s : 0.0f;
     }
     __syncthreads();
     for (int k = tid; k < H; k += blockDim.x) {
         float s = 0.0f;
-        for (int j = 0; j < H; j++) s += h1[j] * Wp[L::oW2T + k * H + j];
+        for (int j = 0; j < H; j++) s += h1[j] * Wp[L::oW2T + qn_wt(k, j, H)];
         s += Wp[L::ob2 + k];
         h2[k] = s > 0.0f ? s : 0.0f;
     }

@@ -124,13 +124,14 @@ __device__ __forceinline__ half8 frag_tr_h(const _Float16 *img, int r0, int c0) 
     return r;
 }
 
-// A-fragment of a transposed f32 weight matrix WT[N][ld] straight from HBM:
-// WT[n0 + (l&15)][k0 + 8(l>>4) + e] -> f16.  nvalid masks padded rows.
+// A-fragment of a transposed f32 weight matrix WT[N][ld] (tiled, qn_wt)
+// straight from HBM: WT[n0 + (l&15)][k0 + 8(l>>4) + e] -> f16, 32 contiguous
+// bytes per lane.  nvalid masks padded rows.
 __device__ __forceinline__ half8 wfrag(const float *WT, int ld, int n0, int k0, int nvalid = 16) {
     const int l = threadIdx.x & 63, lr = l & 15;
     half8 r;
     if (lr < nvalid) {
-        const float4 *p = reinterpret_cast<const float4 *>(WT + (size_t)(n0 + lr) * ld + k0 + 8 * (l >> 4));
+        const float4 *p = reinterpret_cast<const float4 *>(WT + qn_wt(n0 + lr, k0 + 8 * (l >> 4), ld));
         float4 x = p[0], y = p[1];
         r[0] = (_Float16)x.x; r[1] = (_Float16)x.y; r[2] = (_Float16)x.z; r[3] = (_Float16)x.w;
         r[4] = (_Float16)y.x; r[5] = (_Float16)y.y; r[6] = (_Float16)y.z; r[7] = (_Float16)y.w;
@@ -146,7 +147,7 @@ __device__ __forceinline__ half8 wfrag(const _Float16 *WT, int ld, int n0, int k
     const int l = threadIdx.x & 63, lr = l & 15;
     half8 r;
     if (lr < nvalid) {
-        r = *reinterpret_cast<const half8 *>(WT + (size_t)(n0 + lr) * ld + k0 + 8 * (l >> 4));
+        r = *reinterpret_cast<const half8 *>(WT + qn_wt(n0 + lr, k0 + 8 * (l >> 4), ld));
     } else {
 #pragma unroll
         for (int e = 0; e < 8; e++) r[e] = (_Float16)0.0f;
@@ -380,6 +381,12 @@ __device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, c
 // Issue the first Adam batch before the gradient MFMAs: for W1 (measured
 // 1-2 % faster); not for W2, where the 24 extra live VGPRs next to the dW2
 // accumulators and the W2 fragments spill (10 -> 28) and cost 10 %.
+#ifndef DMDQN_EARLY_W3
+#define DMDQN_EARLY_W3 0
+#endif
+#ifndef DMDQN_GX_EARLY
+#define DMDQN_GX_EARLY 0
+#endif
 #ifndef DMDQN_EARLY_W2
 #define DMDQN_EARLY_W2 0
 #endif
@@ -770,9 +777,54 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     forward_x<false>(fr, on, R1, R2, R1, S.z3);
     _Float16 *const P1 = R2, *const P2 = R1;
     STAMP(7);
-    loss_dq<QSTATS>(a, agent, DQ, S);
-
     const half8 ones = ones8();
+#if DMDQN_EARLY_W3
+    // ---- dW3[k][a] = H2^T . DQ (wave w: k-tile w) ; db3 (wave 0).  W3's
+    // Adam loads (lanes lr < 4: rows k = 16w + 4lg + e, column a -> W3T[a][k..k+3])
+    // are issued before the loss, so their latency hides behind it.
+    {
+        const size_t i3 = L::oW3T + (size_t)(lr & 3) * H + 16 * w + 4 * lg;
+        float4 w3 = {}, m3 = {}, v3 = {};
+        if (lr < NACT) {
+            w3 = *reinterpret_cast<const float4 *>(Wp + i3);
+            m3 = *reinterpret_cast<const float4 *>(Mp + i3);
+            v3 = *reinterpret_cast<const float4 *>(Vp + i3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        loss_dq<QSTATS>(a, agent, DQ, S);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f}, gb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b0 = 0; b0 < B_; b0 += 32) {
+            half8 dqf = frag_tr(DQ, 16, b0, 0);
+            acc = mfma(frag_tr_h(P2, b0, 16 * w), dqf, acc);
+            gb = mfma(ones, dqf, gb);  // every wave (no MFMA under divergent control)
+        }
+        if (lr < NACT) {
+            float *pw = &w3.x, *pm = &m3.x, *pv = &v3.x;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const float ge = acc[e];
+                pm[e] = pm[e] + (ge - pm[e]) * AK.c1;
+                pv[e] = pv[e] + (ge * ge - pv[e]) * AK.c2;
+                pw[e] = pw[e] - (pm[e] * AK.alpha) / (sqrtf(pv[e]) + AK.eps);
+            }
+            *reinterpret_cast<float4 *>(Wp + i3) = w3;
+            *reinterpret_cast<float4 *>(Mp + i3) = m3;
+            *reinterpret_cast<float4 *>(Vp + i3) = v3;
+            if (SYNC) {
+                *reinterpret_cast<float4 *>(Tp + i3) = w3;
+                if (TH) {
+                    half4v hv;
+                    hv[0] = (_Float16)w3.x; hv[1] = (_Float16)w3.y;
+                    hv[2] = (_Float16)w3.z; hv[3] = (_Float16)w3.w;
+                    *reinterpret_cast<half4v *>(TH + i3) = hv;
+                }
+            }
+            if (w == 0 && lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob3 + lr, gb[0], AK);
+        }
+    }
+#else
+    loss_dq<QSTATS>(a, agent, DQ, S);
     // ---- dW3[k][a] = H2^T . DQ (wave w: k-tile w) ; db3 (wave 0)
     {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f}, gb = {0.f, 0.f, 0.f, 0.f};
@@ -788,6 +840,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
             if (w == 0 && lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob3 + lr, gb[0], AK);
         }
     }
+#endif
     __syncthreads();  // dW3 read H2; dZ2 overwrites it
     STAMP(8);
     bwd_dz2(P2, on, S);
@@ -799,7 +852,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         // rows j = 16w + 4lg + e, column k = 16t + lr  ->  W2T[k][j..j+3]
         adam_pipe<4, 2, DMDQN_EARLY_W2>(
             Wp, Mp, Vp, Tp,
-            [&](int t) { return (size_t)L::oW2T + (size_t)(16 * t + lr) * H + 16 * w + 4 * lg; }, g2,
+            [&](int t) { return (size_t)L::oW2T + qn_wt(16 * t + lr, 16 * w + 4 * lg, H); }, g2,
             AK, [&]() {
 #pragma unroll
                 for (int t = 0; t < 8; t++) g2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -819,12 +872,22 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
     }
     __syncthreads();  // W2^T image complete
     f32x4 d1[8];
+#if DMDQN_GX_EARLY
+    {
+        Rows gx;  // X(S) again for dW1: issued before dH1, lands in P2 once dZ2 is consumed
+        gather_issue(a.ring_s, a, agent, S.slot, gx);
+        __builtin_amdgcn_sched_barrier(0);
+        bwd_dh1_from_image(P1, P2, d1);
+        gather_commit(P2, gx);
+    }
+#else
     bwd_dh1_from_image(P1, P2, d1);
     {
         Rows gx;  // X(S) again for dW1 (P2 is free)
         gather_issue(a.ring_s, a, agent, S.slot, gx);
         gather_commit(P2, gx);
     }
+#endif
     STAMP(10);
     bwd_dz1(P1, mask, d1);
     __syncthreads();
@@ -836,7 +899,7 @@ __global__ void __launch_bounds__(512, 4) k_learn_f16(dmdqn_learn_args a) {
         // features 89..95 have zero weight and zero gradient and stay zero
         adam_pipe<2, 3, DMDQN_EARLY_W1>(
             Wp, Mp, Vp, Tp,
-            [&](int t) { return (size_t)L::oW1T + (size_t)(16 * w + lr) * DP + 16 * t + 4 * lg; }, g1,
+            [&](int t) { return (size_t)L::oW1T + qn_wt(16 * w + lr, 16 * t + 4 * lg, DP); }, g1,
             AK, [&]() {
 #pragma unroll
                 for (int t = 0; t < 6; t++) g1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -968,13 +1031,13 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         const f32x4 c = G2L[(w * 8 + t) * 64 + l];
-        *reinterpret_cast<float4 *>(G + L::oW2T + (16 * t + lr) * H + 16 * w + 4 * lg) =
+        *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(16 * t + lr, 16 * w + 4 * lg, H)) =
             make_float4(c[0], c[1], c[2], c[3]);
     }
     if (lg == 0) G[L::ob2 + 16 * w + lr] = GB2[0];
 #pragma unroll
     for (int t = 0; t < 6; t++)
-        *reinterpret_cast<float4 *>(G + L::oW1T + (16 * w + lr) * DP + 16 * t + 4 * lg) =
+        *reinterpret_cast<float4 *>(G + L::oW1T + qn_wt(16 * w + lr, 16 * t + 4 * lg, DP)) =
             make_float4(G1[t][0], G1[t][1], G1[t][2], G1[t][3]);
     if (lg == 0) G[L::ob1 + 16 * w + lr] = GB1[0];
 }

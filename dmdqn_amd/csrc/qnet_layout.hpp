@@ -5,12 +5,17 @@
 // its target copy and Adam m / v) are stored TRANSPOSED, [fan_out][fan_in],
 // with the 89 input features padded to 96:
 //   W1T[H][96] | W2T[H][H] | W3T[4][H] | b1[H] | b2[H] | b3[4]
-// so that (a) a forward MFMA A-fragment (8 consecutive fan-in values of one
-// neuron) is 32 contiguous bytes, and (b) a weight-gradient tile C[in][out]
-// produced by MFMA holds 4 consecutive fan-in values per lane -> one 16-byte
-// read-modify-write per lane in Adam.  Padding entries (features 89..95) have
-// zero weights and receive zero gradients, so Adam keeps them at zero.
-// Host helpers (dmdqn_amd/agent.py) convert to/from the Keras get_weights order.
+// W1T and W2T are TILED (qn_wt): 16 x 16 (fan-out x fan-in) tiles of 1 KB in
+// row-major tile order, each stored as [fan-in / 8 (2)][fan-out (16)][fan-in % 8 (8)]:
+//   (a) a forward MFMA A-fragment (8 consecutive fan-in values of one neuron)
+//       is 32 contiguous bytes;
+//   (b) a weight-gradient tile C[in][out] produced by MFMA holds 4 consecutive
+//       fan-in values per lane, and the 64 lanes' 16-byte Adam accesses cover
+//       the tile's 1 KB contiguously (row-major [fan_out][fan_in] gave 16
+//       separate 64-byte pieces per wave-instruction: 17 % slower learn).
+// W3T stays row-major.  Padding entries (features 89..95) have zero weights
+// and receive zero gradients, so Adam keeps them at zero.  Host helpers
+// (dmdqn_amd/agent.py) convert to/from the Keras get_weights order.
 #pragma once
 
 namespace dmdqn {
@@ -18,6 +23,13 @@ namespace dmdqn {
 constexpr int QN_D = 89;    // observation dim (order_lanes.py:554)
 constexpr int QN_DP = 96;   // padded fan-in of layer 1
 constexpr int QN_NA = 4;    // actions
+
+// Offset of W^T[out][in] in a tiled [N][K] block (K = padded fan-in, N and K
+// multiples of 16).
+__host__ __device__ constexpr int qn_wt(int out, int in, int K) {
+    return (((out >> 4) * (K >> 4) + (in >> 4)) << 8) + (((in >> 3) & 1) << 7) + ((out & 15) << 3) +
+           (in & 7);
+}
 
 template <int H>
 struct QL {

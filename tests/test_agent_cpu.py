@@ -5,7 +5,7 @@ import yaml
 
 from conftest import ROOT
 from dmdqn_amd.agent import (AgentConfig, keras_adam_consts, keras_to_kernel, kernel_to_keras,
-                             n_params, n_params_keras)
+                             n_params, n_params_keras, tile_wt, untile_wt)
 
 
 def test_param_counts():
@@ -22,9 +22,27 @@ def test_layout_roundtrip():
         assert kk.shape == (3, n_params(H))
         np.testing.assert_array_equal(kernel_to_keras(kk, H), k)
         # feature padding of W1T is zero
-        W1T = kk[:, :H * 96].reshape(3, H, 96)
+        W1T = untile_wt(kk[:, :H * 96], H, 96)
         assert (W1T[:, :, 89:] == 0).all()
         np.testing.assert_array_equal(W1T[:, :, :89], np.swapaxes(k[:, :89 * H].reshape(3, 89, H), 1, 2))
+
+
+def _qn_wt(o, i, K):  # qnet_layout.hpp qn_wt
+    return (((o >> 4) * (K >> 4) + (i >> 4)) << 8) + (((i >> 3) & 1) << 7) + ((o & 15) << 3) + (i & 7)
+
+
+def test_tiled_weight_layout_matches_device_formula():
+    rng = np.random.RandomState(1)
+    for N, K in ((128, 96), (128, 128), (64, 96), (64, 64)):
+        W = rng.normal(size=(2, N, K)).astype(np.float32)
+        t = tile_wt(W)
+        idx = np.array([[_qn_wt(o, i, K) for i in range(K)] for o in range(N)])
+        np.testing.assert_array_equal(t[:, idx], W)
+        np.testing.assert_array_equal(untile_wt(t, N, K), W)
+        # one Adam wave-instruction (lane l = lr + 16 lg owns W^T[16t + lr][16w + 4lg .. +3])
+        # covers one contiguous 1 KB tile
+        offs = sorted(_qn_wt(16 + (l & 15), 16 + 4 * (l >> 4) + e, K) for l in range(64) for e in range(4))
+        assert offs == list(range(offs[0], offs[0] + 256))
 
 
 def test_keras_adam_constants():
