@@ -102,6 +102,9 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
                     "20 B per vehicle-substep as SURVEY 8d defines them"}
 
 
+VBAR_EVERY = 5  # V-bar sampling stride (steps)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +122,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=60,
                     help="timed RL steps per replica of the CPU baseline")
+    ap.add_argument("--overlap", action="store_true",
+                    help="act/sim/observe/sample of step t+1 on a side stream, overlapped with "
+                         "learn t (bit-identical; +2-3 %% steps/s, but the learn kernel shares "
+                         "the GPU, so its timed duration grows ~6 %%); default: one stream")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo; only barrier + timing use it")
     args = ap.parse_args()
@@ -140,14 +147,14 @@ def main():
 
     # all work on one dedicated stream: HIP events recorded on the legacy null
     # stream block the host and would inflate the timed region
-    work = torch.cuda.Stream(dev)
+    work = torch.cuda.Stream(dev, priority=int(os.environ.get("DMDQN_WORK_PRIO", "0")))
     torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
     # independent nets are seeded per rank; the shared net must start identical on every rank
     agent_cfg = AgentConfig(precision=args.precision, seed=1000 if args.shared else 1000 + rank,
                             shared_params=args.shared)
-    tr = Trainer(env_cfg, agent_cfg, device=dev)
+    tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap)
     E, A = tr.env.E, tr.env.A
     NA = E * A
     for _ in range(agent_cfg.batch_size - 1):  # replay fill (no learn yet)
@@ -166,14 +173,17 @@ def main():
 
     sim_starts, sim_ends = [], []
 
+    # running vehicles per env after every VBAR_EVERY-th step, summed on the
+    # device (V-bar for the sim's algorithmic bytes); one tiny elementwise add,
+    # on the stream the sim runs on (the hook runs in its stream context)
+    vsum = torch.zeros(E, dtype=torch.int64, device=dev)
+
     def sim_hook(before):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream(dev))
         (sim_starts if before else sim_ends).append(ev)
-
-    # running vehicles per env after each step, summed on the device (V-bar for
-    # the sim's algorithmic bytes); one tiny elementwise add per step
-    vsum = torch.zeros(E, dtype=torch.int64, device=dev)
+        if not before and (len(sim_ends) - 1) % VBAR_EVERY == 0:
+            vsum.add_(tr.env.t_stats[:, 2])
     learn_before = tr.agent.learn_launches
     D.barrier()
     torch.cuda.synchronize(dev)
@@ -182,14 +192,13 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.step()
-        vsum += tr.env.t_stats[:, 2]
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     D.barrier()
     tr.agent.learn_hook = None
     tr.env.sim_hook = None
     sim_ms = [s.elapsed_time(e) for s, e in zip(sim_starts, sim_ends)]
-    vbar = float(vsum.double().mean().item()) / args.steps
+    vbar = float(vsum.double().mean().item()) / len(range(0, args.steps, VBAR_EVERY))
     n_learn = tr.agent.learn_launches - learn_before
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
@@ -237,6 +246,8 @@ def main():
                 "parallelism": (f"env-shard x{world}" + (" + RCCL all-reduce of the 114 KB "
                                 "gradient" if args.shared and world > 1 else " (no collectives)")),
                 "precision": args.precision,
+                "schedule": ("one stream" if not args.overlap else
+                             "two streams: act/sim/observe/sample of step t+1 overlap learn t"),
             },
             "roofline": {
                 "kernel": ("k_learn_shared_f16 + k_reduce_slabs + k_adam" if args.shared else

@@ -247,11 +247,21 @@ class BatchedDQN:
                      else np.asarray(env_seeds))
             self.np_state = K.seed_streams(seeds, "np", dev)
             self.py_state = K.seed_streams(seeds, "py", dev)
-        self.idx = torch.empty((NA, cfg.batch_size), dtype=torch.int32, device=dev)
+        # two index buffers: presample() may draw the next learn's batch (on
+        # another stream) while the current learn still reads its own
+        self._idx_bufs = [torch.empty((NA, cfg.batch_size), dtype=torch.int32, device=dev)
+                          for _ in range(2)]
+        self.idx = self._idx_bufs[0]
+        self._presampled = None  # (n, buffer) drawn ahead by presample()
         self.loss = torch.zeros(NA, dtype=torch.float32, device=dev)
         self.qstats = torch.zeros((NA, 6), dtype=torch.float32, device=dev)
-        self.actions = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
+        # alternating action buffers: a caller may still read step t's actions on
+        # its stream while the trainer's side stream writes step t+1's
+        self._act_bufs = [torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
+                          for _ in range(2)]
+        self.actions = self._act_bufs[0]
         self.greedy = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
+        self._done_flags = [torch.full((NA,), v, dtype=torch.uint8, device=dev) for v in (0, 1)]
         self.global_step_count = 0
         self.learn_step_counter = 0
         self.epsilon = cfg.epsilon_start
@@ -280,6 +290,7 @@ class BatchedDQN:
                  self.NA, self.P, self.H, ptr(obs.reshape(self.NA, D_IN)), ptr(self.greedy), None,
                  stream_of(self.device))
             greedy = self.greedy
+        self.actions = self._act_bufs[1] if self.actions is self._act_bufs[0] else self._act_bufs[0]
         return K.act(self.np_state, self.A, eps=eps, n_actions=N_ACTIONS, greedy=greedy,
                      out=self.actions)
 
@@ -289,7 +300,7 @@ class BatchedDQN:
         actions [E,A] int32, rewards [E,A] f64, done: bool or uint8 [E]."""
         NA = self.NA
         if isinstance(done, (bool, np.bool_, int)):
-            d = torch.full((NA,), int(bool(done)), dtype=torch.uint8, device=self.device)
+            d = self._done_flags[int(bool(done))]  # constant [NA] u8 (no per-step fill)
         else:
             d = done.to(torch.uint8).reshape(self.E, 1).expand(self.E, self.A).reshape(NA).contiguous()
         self.ring.store(obs.reshape(NA, D_IN), next_obs.reshape(NA, D_IN),
@@ -310,7 +321,14 @@ class BatchedDQN:
         if n < self.cfg.batch_size:
             return None
         cfg = self.cfg
-        K.replay_sample(self.py_state, self.A, n, cfg.batch_size, out=self.idx)
+        if self._presampled is not None:
+            pn, buf = self._presampled
+            self._presampled = None
+            if pn != n:
+                raise RuntimeError(f"presample drew for n={pn}, the ring holds {n}")
+            self.idx = buf
+        else:
+            K.replay_sample(self.py_state, self.A, n, cfg.batch_size, out=self.idx)
         self.learn_step_counter += 1
         alpha, c1, c2, eps = keras_adam_consts(self.learn_step_counter, cfg.learning_rate)
         sync = self.learn_step_counter % cfg.target_update_frequency == 0
@@ -335,6 +353,22 @@ class BatchedDQN:
             self.learn_hook(False)
         self.learn_launches += 1
         return self.loss
+
+    def presample(self, n):
+        """Draw the next learn's replay indices now (ReplayBuffer.sample,
+        dqn_agent.py:59-63) for a ring of n transitions, into the index buffer
+        the current learn does not read, on the current stream.  The draws
+        depend only on the CPython stream and n, never on the ring contents, so
+        they may run before the store that brings the ring to n (trainer
+        overlap).  The next learn() must see len(ring) == n."""
+        if n < self.cfg.batch_size:
+            return False
+        if self._presampled is not None:
+            raise RuntimeError("presample called twice before a learn")
+        buf = self._idx_bufs[1] if self.idx is self._idx_bufs[0] else self._idx_bufs[0]
+        K.replay_sample(self.py_state, self.A, n, self.cfg.batch_size, out=buf)
+        self._presampled = (n, buf)
+        return True
 
     def learn_metrics(self):
         """The scalars dqn_agent.py:361-370 logs, from the last learn(collect_stats=True):

@@ -103,6 +103,7 @@ def load(path, tr):
     tr.obs = st["obs"].to(env.device)
     # the observation the env hands back is a view of its own buffer
     env.obs = tr.obs
+    tr.join_streams()  # the restore ran on the caller's stream
     return st
 
 

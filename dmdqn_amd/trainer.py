@@ -3,8 +3,29 @@
 One `step()` is one iteration of the loop body for every agent of every env
 replica:  act (select_action) -> env step (setPhase, K substeps) -> observe /
 reward -> remember -> replay (learn), in the reference's order.  All of it is
-kernel launches on one HIP stream; the host keeps only counters.
+kernel launches; the host keeps only counters.
+
+Two HIP streams (overlap=True, the default on a device).  The reference loop
+is sequential, but its data flow is not: with the reference's epsilon (1.0 on
+the training path, A-1) the next act, the env step and the next batch's replay
+draws need nothing from the learn.  So step t+1's act -> sim -> observe ->
+sample run on a side stream while learn t runs on the caller's stream; only
+remember (which overwrites ring slots learn t may read) waits for learn t, and
+the side stream waits for remember t before reusing its buffers.  Every kernel
+sees exactly the inputs of the sequential order, so results are bit-identical
+(tests/test_gpu_overlap.py).  A greedy act (epsilon < 1) also waits for the
+learn, whose weights it reads.
+
+  side:  [wait store t-1] act_t  sim_t  observe_t  sample_t  (ev_obs)
+  main:                     [wait ev_obs] store_t (ev_store) learn_t
+
+What a step returns or exposes per step (obs, reward, loss, agent.actions) is
+fresh or double-buffered, so the caller may read it on its own stream between
+steps.  Persistent env/agent state (sim arrays, RNG streams) is advanced by the
+next step's side stream without waiting for such reads: read it host-blocking
+(.cpu()), and call join_streams() after writing it.
 """
+import os
 from dataclasses import dataclass
 
 import torch
@@ -20,8 +41,15 @@ class StepStats:
 
 
 class Trainer:
-    def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda"):
+    def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
+                 overlap=True):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
+        self.overlap = overlap
+        self.side = (torch.cuda.Stream(self.env.device,
+                                       priority=int(os.environ.get("DMDQN_SIDE_PRIO", "0")))
+                     if overlap else None)
+        self._ev_store = self._ev_learn = None
+        self._join = True  # the side stream's first work waits for everything before it
         self.agent = BatchedDQN(self.env.E, self.env.A, agent_cfg or AgentConfig(), device=device,
                                 env_seeds=self.env.seeds)
         self.obs = self.env.reset()
@@ -34,6 +62,8 @@ class Trainer:
     def step(self, collect_stats=False):
         """One loop iteration for every replica; collect_stats makes the learn
         also produce the metrics of dqn_agent.py:361-370 (agent.learn_metrics)."""
+        if self.overlap:
+            return self._step_overlap(collect_stats)
         env, agent = self.env, self.agent
         actions = agent.act(self.obs)                          # train.py:211-222
         next_obs, reward, done, info = env.step(actions)       # train.py:225-270
@@ -49,6 +79,52 @@ class Trainer:
         else:
             self.obs = next_obs
         return StepStats(loss is not None, done)
+
+    def _step_overlap(self, collect_stats):
+        env, agent, side = self.env, self.agent, self.side
+        main = torch.cuda.current_stream(env.device)
+        if self._join:  # first step, or the caller touched state on its stream
+            side.wait_stream(main)
+            self._join = False
+        elif self._ev_store is not None:
+            side.wait_event(self._ev_store)  # remember t-1 has read obs/actions/reward
+        if agent.current_epsilon() < 1.0 and self._ev_learn is not None:
+            side.wait_event(self._ev_learn)  # greedy act reads the updated weights
+        with torch.cuda.stream(side):
+            actions = agent.act(self.obs)                          # train.py:211-222
+            next_obs, reward, done, info = env.step(actions)       # train.py:225-270
+            agent.presample(min(agent.ring.total + 1, agent.ring.cap))
+            ev_obs = torch.cuda.Event()
+            ev_obs.record(side)
+        main.wait_event(ev_obs)
+        for t in (self.obs, next_obs, reward, env.local):
+            t.record_stream(main)  # side-allocated, read on main
+        agent.remember(self.obs, actions, reward, next_obs, done)  # train.py:274-282
+        self._ev_store = torch.cuda.Event()
+        self._ev_store.record(main)
+        loss = agent.learn(collect_stats=collect_stats)
+        self._ev_learn = torch.cuda.Event()
+        self._ev_learn.record(main)
+        self.last_loss, self.last_reward = loss, reward
+        self.step_count += 1
+        self.total_steps += 1
+        if done:                                               # train.py:188-190
+            self.episode += 1
+            self.step_count = 0
+            with torch.cuda.stream(side):
+                self.obs = env.reset()
+            main.wait_stream(side)
+            self.obs.record_stream(main)
+            env.local.record_stream(main)
+        else:
+            self.obs = next_obs
+        return StepStats(loss is not None, done)
+
+    def join_streams(self):
+        """Call after changing trainer state on the caller's stream between
+        steps (checkpoint restore, weight loads): the next step's side-stream
+        work then waits for it."""
+        self._join = True
 
     def agent_env_steps(self, n_steps):
         return n_steps * self.env.E * self.env.A
