@@ -89,7 +89,10 @@ def sim_state_fits_lds(rows, cols, cap=24):
 
 def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
     """Sim-only HBM figure: 20*K*V-bar algorithmic bytes per env
-    step over the average k_sim_step duration (HIP events, timed region)."""
+    step over the average k_sim_step duration (HIP events over the
+    SIM_PROBE_STEPS untimed steps that follow the timed region)."""
+    if not sim_ms:
+        return None
     t = float(np.mean(sim_ms)) / 1e3
     b = E * SIM_BYTES_PER_VEH_SUBSTEP * K * vbar
     where = "env state staged in LDS" if in_lds else "env state in HBM (exceeds LDS)"
@@ -98,11 +101,12 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
             "unit": "GB/s", "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 5),
             "traffic": traffic, "bytes_per_launch": int(b), "mean_running_vehicles": round(vbar, 1),
             "avg_launch_ms": round(t * 1e3, 4),
+            "timed_over": f"{SIM_PROBE_STEPS} steps after the timed region",
             "note": "latency-bound: the per-env working set is cache-resident; bytes are "
                     "20 B per vehicle-substep as SURVEY 8d defines them"}
 
 
-VBAR_EVERY = 5  # V-bar sampling stride (steps)
+SIM_PROBE_STEPS = 10  # untimed steps after the timed region that time the sim
 
 
 def main():
@@ -122,10 +126,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=60,
                     help="timed RL steps per replica of the CPU baseline")
-    ap.add_argument("--overlap", action="store_true",
-                    help="act/sim/observe/sample of step t+1 on a side stream, overlapped with "
-                         "learn t (bit-identical; +2-3 %% steps/s, but the learn kernel shares "
-                         "the GPU, so its timed duration grows ~6 %%); default: one stream")
+    ap.add_argument("--overlap", default="none", choices=["none", "sample", "full"],
+                    help="stream schedule (dmdqn_amd/trainer.py; all bit-identical): none = one "
+                         "stream; sample = replay draws on a side stream beside act/sim/observe/"
+                         "store; full = step t+1's act/sim/observe/sample beside learn t")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo; only barrier + timing use it")
     args = ap.parse_args()
@@ -147,7 +151,7 @@ def main():
 
     # all work on one dedicated stream: HIP events recorded on the legacy null
     # stream block the host and would inflate the timed region
-    work = torch.cuda.Stream(dev, priority=int(os.environ.get("DMDQN_WORK_PRIO", "0")))
+    work = torch.cuda.Stream(dev)
     torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
@@ -163,43 +167,57 @@ def main():
         tr.step()
     assert tr.agent.learn_launches > 0 or args.warmup == 0
 
-    # HIP events bracketing each learn launch, on the stream it runs on
+    # HIP events bracketing each learn launch, on the stream it runs on.
+    # Created (and recorded once) before the timed region: a torch Event
+    # creates its HIP event lazily at the first record.
+    pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+    for ev in pool:
+        ev.record(work)
+    torch.cuda.synchronize(dev)
+    pool_it = iter(pool)
     starts, ends = [], []
 
     def hook(before):
-        ev = torch.cuda.Event(enable_timing=True)
+        ev = next(pool_it)
         ev.record(torch.cuda.current_stream(dev))
         (starts if before else ends).append(ev)
 
-    sim_starts, sim_ends = [], []
+    learn_before = tr.agent.learn_launches
+    D.barrier()
+    torch.cuda.synchronize(dev)
+    tr.agent.learn_hook = hook
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    D.barrier()
+    tr.agent.learn_hook = None
+    n_learn = tr.agent.learn_launches - learn_before
 
-    # running vehicles per env after every VBAR_EVERY-th step, summed on the
-    # device (V-bar for the sim's algorithmic bytes); one tiny elementwise add,
-    # on the stream the sim runs on (the hook runs in its stream context)
+    # Sim probe, after the timed region: k_sim_step durations (HIP events on the
+    # stream the sim runs on) and the running vehicles per env after each step
+    # (V-bar for the sim's algorithmic bytes).  Kept out of the timed region:
+    # the extra records and the per-step reduction around the sim cost
+    # 0.1-0.6 ms per step there (measured).
+    sim_starts, sim_ends = [], []
     vsum = torch.zeros(E, dtype=torch.int64, device=dev)
 
     def sim_hook(before):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream(dev))
         (sim_starts if before else sim_ends).append(ev)
-        if not before and (len(sim_ends) - 1) % VBAR_EVERY == 0:
+        if not before:
             vsum.add_(tr.env.t_stats[:, 2])
-    learn_before = tr.agent.learn_launches
-    D.barrier()
-    torch.cuda.synchronize(dev)
-    tr.agent.learn_hook = hook
+
     tr.env.sim_hook = sim_hook
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(SIM_PROBE_STEPS):
         tr.step()
     torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    D.barrier()
-    tr.agent.learn_hook = None
     tr.env.sim_hook = None
     sim_ms = [s.elapsed_time(e) for s, e in zip(sim_starts, sim_ends)]
-    vbar = float(vsum.double().mean().item()) / len(range(0, args.steps, VBAR_EVERY))
-    n_learn = tr.agent.learn_launches - learn_before
+    vbar = float(vsum.double().mean().item()) / SIM_PROBE_STEPS
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     el_max = D.max_over_ranks(el, device=dev)
@@ -210,7 +228,7 @@ def main():
         P = n_params_keras(tr.agent.H)  # the reference's 28,548 parameters
         # independent = NA * (128*721 + 28P); shared (C5) = NA*128*721 + 28P
         bpl = (NA * 128 * REPLAY_ROW_BYTES + 28 * P) if args.shared else NA * learn_bytes_per_agent(P)
-        avg_learn_s = float(np.mean(learn_ms)) / 1e3
+        avg_learn_s = float(np.mean(learn_ms)) / 1e3 if learn_ms else float("nan")
         achieved = bpl / avg_learn_s / 1e9
         wl = f"{args.rows}x{args.cols}x{args.envs}"
         traffic = read_traffic(f"{wl}_{args.precision}")
@@ -229,6 +247,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el_max / args.steps * 1e3, 4),
+            "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -246,8 +265,9 @@ def main():
                 "parallelism": (f"env-shard x{world}" + (" + RCCL all-reduce of the 114 KB "
                                 "gradient" if args.shared and world > 1 else " (no collectives)")),
                 "precision": args.precision,
-                "schedule": ("one stream" if not args.overlap else
-                             "two streams: act/sim/observe/sample of step t+1 overlap learn t"),
+                "schedule": {"none": "one stream",
+                             "sample": "replay draws on a side stream beside act/sim/observe/store",
+                             "full": "act/sim/observe/sample of step t+1 beside learn t"}[args.overlap],
             },
             "roofline": {
                 "kernel": ("k_learn_shared_f16 + k_reduce_slabs + k_adam" if args.shared else

@@ -5,33 +5,43 @@ replica:  act (select_action) -> env step (setPhase, K substeps) -> observe /
 reward -> remember -> replay (learn), in the reference's order.  All of it is
 kernel launches; the host keeps only counters.
 
-Two HIP streams (overlap=True, the default on a device).  The reference loop
-is sequential, but its data flow is not: with the reference's epsilon (1.0 on
-the training path, A-1) the next act, the env step and the next batch's replay
-draws need nothing from the learn.  So step t+1's act -> sim -> observe ->
-sample run on a side stream while learn t runs on the caller's stream; only
-remember (which overwrites ring slots learn t may read) waits for learn t, and
-the side stream waits for remember t before reusing its buffers.  Every kernel
-sees exactly the inputs of the sequential order, so results are bit-identical
-(tests/test_gpu_overlap.py).  A greedy act (epsilon < 1) also waits for the
-learn, whose weights it reads.
+Schedules (`overlap`).  The reference loop is sequential, but its data flow
+is not: the replay draws of a step depend only on the CPython stream and the
+ring length (never on the ring contents), and with the reference's epsilon
+(1.0 on the training path, A-1) the next act and env step need nothing from
+the learn.  Every schedule gives each kernel exactly the inputs of the
+sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
 
-  side:  [wait store t-1] act_t  sim_t  observe_t  sample_t  (ev_obs)
-  main:                     [wait ev_obs] store_t (ev_store) learn_t
+  "none"    (default) one stream: act, sim, observe, store, sample, learn.
+  "sample"  the replay draws of step t run on a side stream beside
+            act/sim/observe/store of step t (all latency-bound, low occupancy);
+            the side stream waits for learn t-1, so nothing shares the GPU
+            with a learn.
+              side:  [wait learn t-1] sample_t (ev_s)
+              main:  act_t sim_t observe_t store_t [wait ev_s] learn_t
+  "full"    step t+1's act -> sim -> observe -> sample run on the side stream
+            while learn t runs; only remember (which overwrites ring slots
+            learn t may read) waits for learn t.  A greedy act (epsilon < 1)
+            also waits for the learn, whose weights it reads.  The learn then
+            shares the GPU with the sim, so its own duration grows.
+              side:  [wait store t-1] act_t sim_t observe_t sample_t (ev_obs)
+              main:                  [wait ev_obs] store_t (ev_store) learn_t
 
-What a step returns or exposes per step (obs, reward, loss, agent.actions) is
-fresh or double-buffered, so the caller may read it on its own stream between
-steps.  Persistent env/agent state (sim arrays, RNG streams) is advanced by the
-next step's side stream without waiting for such reads: read it host-blocking
-(.cpu()), and call join_streams() after writing it.
+What a step returns or exposes per step (obs, reward, loss, agent.actions,
+agent.idx) is fresh or double-buffered, so the caller may read it on its own
+stream between steps.  Persistent env/agent state (sim arrays, RNG streams) is
+advanced by the next step's side stream without waiting for such reads: read
+it host-blocking (.cpu()), and call join_streams() after writing it.
 """
-import os
 from dataclasses import dataclass
 
 import torch
 
 from .agent import AgentConfig, BatchedDQN
 from .env import EnvConfig, TrafficEnv
+
+
+SCHEDULES = ("none", "sample", "full")
 
 
 @dataclass
@@ -42,12 +52,14 @@ class StepStats:
 
 class Trainer:
     def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
-                 overlap=True):
+                 overlap="none"):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
+        if overlap is True or overlap is False:
+            overlap = "full" if overlap else "none"
+        if overlap not in SCHEDULES:
+            raise ValueError(f"overlap must be one of {SCHEDULES}")
         self.overlap = overlap
-        self.side = (torch.cuda.Stream(self.env.device,
-                                       priority=int(os.environ.get("DMDQN_SIDE_PRIO", "0")))
-                     if overlap else None)
+        self.side = torch.cuda.Stream(self.env.device) if overlap != "none" else None
         self._ev_store = self._ev_learn = None
         self._join = True  # the side stream's first work waits for everything before it
         self.agent = BatchedDQN(self.env.E, self.env.A, agent_cfg or AgentConfig(), device=device,
@@ -62,13 +74,47 @@ class Trainer:
     def step(self, collect_stats=False):
         """One loop iteration for every replica; collect_stats makes the learn
         also produce the metrics of dqn_agent.py:361-370 (agent.learn_metrics)."""
-        if self.overlap:
+        if self.overlap == "full":
             return self._step_overlap(collect_stats)
+        if self.overlap == "sample":
+            return self._step_side_sample(collect_stats)
         env, agent = self.env, self.agent
         actions = agent.act(self.obs)                          # train.py:211-222
         next_obs, reward, done, info = env.step(actions)       # train.py:225-270
         agent.remember(self.obs, actions, reward, next_obs, done)  # train.py:274-282
         loss = agent.learn(collect_stats=collect_stats)
+        self.last_loss, self.last_reward = loss, reward
+        self.step_count += 1
+        self.total_steps += 1
+        if done:                                               # train.py:188-190
+            self.episode += 1
+            self.step_count = 0
+            self.obs = env.reset()
+        else:
+            self.obs = next_obs
+        return StepStats(loss is not None, done)
+
+    def _step_side_sample(self, collect_stats):
+        env, agent, side = self.env, self.agent, self.side
+        main = torch.cuda.current_stream(env.device)
+        if self._join:
+            side.wait_stream(main)
+            self._join = False
+        elif self._ev_learn is not None:
+            side.wait_event(self._ev_learn)  # learn t-1 done: nothing beside the next learn
+        ev_s = None
+        with torch.cuda.stream(side):
+            if agent.presample(min(agent.ring.total + 1, agent.ring.cap)):
+                ev_s = torch.cuda.Event()
+                ev_s.record(side)
+        actions = agent.act(self.obs)                          # train.py:211-222
+        next_obs, reward, done, info = env.step(actions)       # train.py:225-270
+        agent.remember(self.obs, actions, reward, next_obs, done)  # train.py:274-282
+        if ev_s is not None:
+            main.wait_event(ev_s)
+        loss = agent.learn(collect_stats=collect_stats)
+        self._ev_learn = torch.cuda.Event()
+        self._ev_learn.record(main)
         self.last_loss, self.last_reward = loss, reward
         self.step_count += 1
         self.total_steps += 1

@@ -35,11 +35,12 @@ def _run(tr, n):
     return out
 
 
+@pytest.mark.parametrize("mode", ["sample", "full"])
 @pytest.mark.parametrize("precision,shared,greedy", [
     ("fp16", False, False), ("fp32", False, False), ("fp16", True, False), ("fp16", False, True)])
-def test_overlap_matches_sequential(precision, shared, greedy):
-    ref = _trainer(False, precision, shared, greedy)
-    ovl = _trainer(True, precision, shared, greedy)
+def test_overlap_matches_sequential(mode, precision, shared, greedy):
+    ref = _trainer("none", precision, shared, greedy)
+    ovl = _trainer(mode, precision, shared, greedy)
     assert ovl.side is not None and ref.side is None
     a, b = _run(ref, 170), _run(ovl, 170)   # 3 episodes of 50 steps, learn from step 128
     assert sum(x[4] for x in a) == 3 and ref.episode == ovl.episode == 3
