@@ -41,7 +41,18 @@ def learn_bytes_per_agent(P, batch=128):
 # Q-net FLOPs of one agent's learn: B*(4F + F') with
 # F = 2(89*128 + 128*128 + 128*4), F' = 2(128*128 + 128*4) -> 33.3 MFLOP
 LEARN_FLOP_PER_AGENT = 128 * (4 * 2 * (89 * 128 + 128 * 128 + 128 * 4) + 2 * (128 * 128 + 128 * 4))
-MFMA_F16_DENSE_TFLOPS = 2500.0  # MI355X dense F16/BF16 MFMA peak (MI355X_MICROARCH.md)
+# MI355X dense MFMA peaks per operand type (MI355X_MICROARCH.md: F16/BF16 2.5
+# PFLOP/s dense, F32 matrix 157.3 TFLOP/s)
+MFMA_PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2500.0, "bf16": 2500.0}
+METRIC = "agent-env steps/sec (whole node), 16-intersection\u00d71024 envs, 1/2/4/8 MI355X"
+DTYPES = {"fp32": "f32",
+          "fp16": "f16 (mixed_float16 as the reference: f16 MFMA operands, f32 accumulate, "
+                  "f32 master weights + Adam)",
+          "bf16": "bf16 (mixed_bfloat16: bf16 MFMA operands, f32 accumulate, "
+                  "f32 master weights + Adam)"}
+LEARN_KERNELS = {"fp32": "k_learn_f32", "fp16": "k_learn_f16", "bf16": "k_learn_bf16"}
+MFMA_OPS = {"fp32": "v_mfma_f32_16x16x4_f32", "fp16": "v_mfma_f32_16x16x32_f16",
+            "bf16": "v_mfma_f32_16x16x32_bf16"}
 SIM_BYTES_PER_VEH_SUBSTEP = 20  # read x, v, lane cursor (12 B) + write x, v (8 B)
 
 
@@ -117,9 +128,10 @@ def main():
     ap.add_argument("--envs", type=int, default=1024, help="env replicas per GPU")
     ap.add_argument("--rows", type=int, default=4)
     ap.add_argument("--cols", type=int, default=4)
-    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
+    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16", "bf16"],
                     help="fp16 = the reference's mixed_float16 policy (f16 MFMA operands, "
-                         "f32 accumulate, f32 master weights + Adam); fp32 = strict path")
+                         "f32 accumulate, f32 master weights + Adam); bf16 = the same with "
+                         "bf16 operands (BASELINE config C2); fp32 = strict path")
     ap.add_argument("--shared", action="store_true",
                     help="C5: one shared network (mean per-agent loss, RCCL gradient "
                          "all-reduce across ranks); use with --rows 8 --cols 8")
@@ -240,7 +252,7 @@ def main():
                       + (", RCCL gradient all-reduce" if world > 1 else "") + ") + one Adam"
                       if args.shared else "Double-DQN learn + Adam")
         out = {
-            "metric": "agent-env steps/sec (whole node), 16-intersection x 1024 envs",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "agent-env steps/s",
             "n_gpus": world,
@@ -251,9 +263,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": ("f32" if args.precision == "fp32" else
-                      "f16 (mixed_float16 as the reference: f16 MFMA operands, f32 accumulate, "
-                      "f32 master weights + Adam)"),
+            "dtype": DTYPES[args.precision],
             "data": f"synthetic ({args.rows}x{args.cols} grid, randomTrips-style demand, "
                     "Keras-style random init)",
             "config": {
@@ -288,13 +298,14 @@ def main():
                                           read_traffic(f"{wl}_sim"),
                                           sim_state_fits_lds(args.rows, args.cols)),
             "mfma": {
-                "kernel": ("k_learn_shared_f16" if args.shared else "k_learn_f16") +
-                          " (Q-net forward/backward, v_mfma_f32_16x16x32_f16)",
+                "kernel": ("k_learn_shared_f16" if args.shared else LEARN_KERNELS[args.precision]) +
+                          f" (Q-net forward/backward, {MFMA_OPS[args.precision]})",
                 "flop_per_launch": NA * LEARN_FLOP_PER_AGENT,
                 "achieved": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12, 2),
-                "peak": MFMA_F16_DENSE_TFLOPS,
+                "peak": MFMA_PEAK_TFLOPS[args.precision],
                 "unit": "TFLOP/s",
-                "frac": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12 / MFMA_F16_DENSE_TFLOPS, 4),
+                "frac": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12 /
+                              MFMA_PEAK_TFLOPS[args.precision], 4),
             },
         }
         print(json.dumps(out))

@@ -53,7 +53,9 @@ _lib.register({
                    C.c_int, C.c_void_p],
 })
 
-PRECISIONS = {"fp32": 0, "fp16": 1}
+PRECISIONS = {"fp32": 0, "fp16": 1, "bf16": 2}
+# dtype of the 16-bit operand copies (target shadow, shared online copy)
+H16_DTYPES = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
 
 D_PAD = 96  # layer-1 fan-in padded for 32-byte MFMA fragments (qnet_layout.hpp)
@@ -172,7 +174,7 @@ class AgentConfig:
     target_update_frequency: int = 500
     nn_layers: List[int] = field(default_factory=lambda: [128, 128])
     # build-only knobs (additive)
-    precision: str = "fp32"          # "fp32" | "fp16" (mixed, the reference's policy)
+    precision: str = "fp32"          # "fp32" | "fp16" (mixed, the reference's policy) | "bf16"
     count_env_steps: bool = False    # True fixes A-1 (epsilon decays); False = reference
     seed: int = 0
     # C5 (not in the reference): ONE network shared by every agent,
@@ -216,18 +218,20 @@ class BatchedDQN:
         w = torch.as_tensor(init.reshape(NW, self.P))
         self.params = w.to(dev).contiguous()
         self.target = self.params.clone()
-        # fp16 path: the target forward reads an f16 copy (padded row stride Ph)
+        # fp16 / bf16 paths: the target forward reads a 16-bit copy (padded row
+        # stride Ph) in the MFMA operand type
         self.Ph = (self.P + 7) // 8 * 8
         self.target_h = self.params_h = None
-        if cfg.precision == "fp16":
+        h16 = H16_DTYPES.get(cfg.precision)
+        if h16 is not None:
             # f16 copies the forwards read (Keras casts the f32 variables to f16);
             # the online copy only for the shared net, whose Adam is a separate
             # pass (fused into the per-agent learn, the extra stores cost more
             # than the halved fragment reads save)
-            self.target_h = torch.zeros((NW, self.Ph), dtype=torch.float16, device=dev)
+            self.target_h = torch.zeros((NW, self.Ph), dtype=h16, device=dev)
             self._refresh_target_h()
             if self.shared:
-                self.params_h = torch.zeros((NW, self.Ph), dtype=torch.float16, device=dev)
+                self.params_h = torch.zeros((NW, self.Ph), dtype=h16, device=dev)
                 self._refresh_params_h()
         if self.shared:
             # one partial gradient per persistent workgroup (one per CU)
@@ -402,11 +406,11 @@ class BatchedDQN:
 
     def _refresh_params_h(self):
         if self.params_h is not None:
-            self.params_h[:, :self.P].copy_(self.params.to(torch.float16))
+            self.params_h[:, :self.P].copy_(self.params.to(self.params_h.dtype))
 
     def _refresh_target_h(self):
         if self.target_h is not None:
-            self.target_h[:, :self.P].copy_(self.target.to(torch.float16))
+            self.target_h[:, :self.P].copy_(self.target.to(self.target_h.dtype))
 
     def update_target_network(self):
         self.target.copy_(self.params)

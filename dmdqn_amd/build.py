@@ -25,6 +25,7 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
 PER_FILE = {
     "learn.hip": ["-ffp-contract=fast"],
     "learn_f16.hip": ["-ffp-contract=fast"],
+    "learn_bf16.hip": ["-ffp-contract=fast"],
 }
 DEFAULT_FP = ["-ffp-contract=off"]
 # experiment hook: extra flags for every file (e.g. -D switches while tuning)

@@ -428,7 +428,8 @@ __global__ void __launch_bounds__(256) k_q_argmax(const float *params, size_t ps
     }
 }
 
-int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s);  // learn_f16.hip
+int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s);   // learn_f16.hip
+int launch_learn_bf16(const dmdqn_learn_args *a, hipStream_t s);  // learn_bf16.hip
 
 }  // namespace dmdqn
 
@@ -442,9 +443,10 @@ extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
     DMDQN_REQUIRE(a->ring_s && a->ring_n && a->ring_a && a->ring_d && a->ring_r && a->idx &&
                       a->params && a->adam_m && a->adam_v && a->target,
                   "dmdqn_learn: null pointer");
-    DMDQN_REQUIRE(a->precision == 0 || a->precision == 1, "dmdqn_learn: precision %d",
+    DMDQN_REQUIRE(a->precision >= 0 && a->precision <= 2, "dmdqn_learn: precision %d",
                   a->precision);
     if (a->precision == 1) return launch_learn_f16(a, as_stream(stream));
+    if (a->precision == 2) return launch_learn_bf16(a, as_stream(stream));
     if (a->hidden == 128) {
         DMDQN_REQUIRE(a->P == Lay<128>::P, "dmdqn_learn: P=%d != %d", a->P, Lay<128>::P);
         hipLaunchKernelGGL(k_learn_f32<128>, dim3(a->NA), dim3(512), 0, as_stream(stream), *a);

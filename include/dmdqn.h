@@ -161,7 +161,8 @@ int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *ac
  * kernels transposed, fan-in padded to 96 (P floats, row stride P; the host
  * converts to / from the Keras get_weights() order).
  * precision: 0 = fp32 MFMA (exact f32 products), 1 = fp16 MFMA with fp32
- * accumulation and fp32 master weights (the reference's mixed_float16). */
+ * accumulation and fp32 master weights (the reference's mixed_float16),
+ * 2 = the same with bf16 MFMA operands (mixed_bfloat16; BASELINE config C2). */
 typedef struct dmdqn_learn_args {
     int32_t NA, cap, start, batch, hidden, precision, sync_target, P;
     const int8_t *ring_s, *ring_n;   /* [NA][cap][96]                        */
@@ -170,7 +171,7 @@ typedef struct dmdqn_learn_args {
     const int32_t *idx;              /* [NA][batch] deque positions          */
     float *params, *adam_m, *adam_v; /* [NA][P] online weights + Adam slots  */
     float *target;                   /* [NA][P] target network               */
-    uint16_t *target_h;              /* precision 1: [NA][Ph] f16 copy of the
+    uint16_t *target_h;              /* precision 1 / 2: [NA][Ph] f16 / bf16 copy of the
                                         target (Ph = P rounded up to 8) used by
                                         the target forward -- Keras casts the
                                         f32 target to f16 for its matmuls, so

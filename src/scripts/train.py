@@ -186,7 +186,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batched", action="store_true")
     ap.add_argument("--envs", type=int, default=1024)
-    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"])
+    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16", "bf16"])
     ap.add_argument("--metrics", default=None, help="offline JSONL metrics (replaces wandb)")
     ap.add_argument("--scenario", default=None,
                     help="SUMO scenario: a .sumocfg or a .npz from sumo_scenario (default for the "

@@ -52,7 +52,7 @@ def test_graft_smoke():
     __graft_entry__.smoke()
 
 
-@pytest.mark.parametrize("precision,rtol", [("fp32", 1e-4), ("fp16", 2e-2)])
+@pytest.mark.parametrize("precision,rtol", [("fp32", 1e-4), ("fp16", 2e-2), ("bf16", 5e-2)])
 def test_learn_metrics_match_host(precision, rtol):
     """qstats (dqn_agent.py:361-363) vs the host: action histogram exact, Q
     moments of the online net on the sampled S within the precision's tolerance."""

@@ -32,7 +32,8 @@ def _run(tr, n):
     return out
 
 
-@pytest.mark.parametrize("precision,shared", [("fp32", False), ("fp16", False), ("fp16", True)])
+@pytest.mark.parametrize("precision,shared", [("fp32", False), ("fp16", False), ("bf16", False),
+                                              ("fp16", True)])
 def test_resume_is_bit_exact(tmp_path, precision, shared):
     tr = _trainer(precision, shared)
     _run(tr, 140)                       # learn active, a target sync behind us

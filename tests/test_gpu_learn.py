@@ -103,14 +103,28 @@ def test_learn_gate_and_q_argmax():
 
 
 # ---------------------------------------------------------------------------
-# fp16 (mixed_float16) path
+# fp16 (mixed_float16) and bf16 (mixed_bfloat16) paths
+def _f16r(x):
+    return np.asarray(x, np.float32).astype(np.float16).astype(np.float32)
+
+
+def _bf16r(x):
+    """f32 -> bf16 -> f32, round to nearest even (v_cvt_pk_bf16_f32; finite inputs)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32)
+
+
+ROUND = {"fp16": _f16r, "bf16": _bf16r}
+
+
 def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e-3,
-                     w3_dz2=None):
-    """numpy restatement of the kernel's rounding points: f16 operands, f32
-    accumulation, f16 activations / Q / activation-gradients, f32 Adam.
-    w3_dz2 overrides the W3 [H][4] that backprop uses for dZ2 (test hook: the
-    correct value is the pre-update W3)."""
-    f16, f32 = np.float16, np.float32
+                     w3_dz2=None, rnd=_f16r):
+    """numpy restatement of the kernel's rounding points: 16-bit operands (rnd:
+    f16 or bf16), f32 accumulation, 16-bit activations / Q / activation-gradients,
+    f32 Adam.  w3_dz2 overrides the W3 [H][4] that backprop uses for dZ2 (test
+    hook: the correct value is the pre-update W3)."""
+    f32 = np.float32
 
     def split(w):
         sizes = [89 * H, H, H * H, H, H * 4, 4]
@@ -119,14 +133,13 @@ def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e
             out.append(w[o:o + s])
             o += s
         W1, b1, W2, b2, W3, b3 = out
-        return (W1.reshape(89, H).astype(f16).astype(f32), b1, W2.reshape(H, H).astype(f16).astype(f32),
-                b2, W3.reshape(H, 4).astype(f16).astype(f32), b3)
+        return (rnd(W1.reshape(89, H)), b1, rnd(W2.reshape(H, H)), b2, rnd(W3.reshape(H, 4)), b3)
 
     def fwd(ws, X):
         W1, b1, W2, b2, W3, b3 = ws
-        h1 = np.maximum(X @ W1 + b1, 0).astype(f16).astype(f32)
-        h2 = np.maximum(h1 @ W2 + b2, 0).astype(f16).astype(f32)
-        q = (h2 @ W3 + b3).astype(f16).astype(f32)
+        h1 = rnd(np.maximum(X @ W1 + b1, 0))
+        h2 = rnd(np.maximum(h1 @ W2 + b2, 0))
+        q = rnd(h2 @ W3 + b3)
         return h1, h2, q
 
     wo, wt = split(p), split(tgt)
@@ -138,17 +151,17 @@ def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e
     pred = q[np.arange(128), Aa]
     dq = (2.0 * (pred - y) / 128).astype(f32)
     loss = np.mean((y - pred) ** 2)
-    dq16 = dq.astype(f16).astype(f32)
+    dq16 = rnd(dq)
     DQ = np.zeros((128, 4), f32)
     DQ[np.arange(128), Aa] = dq16
     W1, b1, W2, b2, W3, b3 = wo
     gW3 = h2.T @ DQ
     gb3 = DQ.sum(0)
-    W3b = W3 if w3_dz2 is None else w3_dz2.astype(f16).astype(f32)
-    dz2 = np.where(h2 > 0, (dq16[:, None] * W3b[:, Aa].T), 0).astype(f16).astype(f32)
+    W3b = W3 if w3_dz2 is None else rnd(w3_dz2)
+    dz2 = rnd(np.where(h2 > 0, (dq16[:, None] * W3b[:, Aa].T), 0))
     gb2 = dz2.sum(0)
     gW2 = h1.T @ dz2
-    dz1 = np.where(h1 > 0, dz2 @ W2.T, 0).astype(f16).astype(f32)
+    dz1 = rnd(np.where(h1 > 0, dz2 @ W2.T, 0))
     gb1 = dz1.sum(0)
     gW1 = S.T @ dz1
     g = np.concatenate([gW1.ravel(), gb1, gW2.ravel(), gb2, gW3.ravel(), gb3]).astype(f32)
@@ -159,9 +172,20 @@ def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e
     return loss, g, p2, m2, v2
 
 
-def test_learn_fp16_matches_mixed_emulation_and_fp32_oracle():
+# per precision: (loss rtol vs the emulation, gradient abs tol x max|g|, gradient
+# rel tol, share of bias / W3 entries within it, loss rtol vs the fp32 oracle).
+# bf16 keeps 8 mantissa bits to f16's 11, so a rounding-boundary flip moves a
+# value 8x further.
+TOL16 = {"fp16": (2e-3, 2e-3, 1e-2, 0.97, 2e-2),
+         "bf16": (1.6e-2, 1.6e-2, 8e-2, 0.95, 2e-2)}
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_learn_h16_matches_mixed_emulation_and_fp32_oracle(precision):
     E, A = 2, 4
-    cfg = AgentConfig(replay_buffer_size=300, target_update_frequency=2, seed=5, precision="fp16")
+    cfg = AgentConfig(replay_buffer_size=300, target_update_frequency=2, seed=5, precision=precision)
+    rnd = ROUND[precision]
+    tl, ta, tr, tshare, t32 = TOL16[precision]
     ag = BatchedDQN(E, A, cfg)
     rng = np.random.RandomState(2)
     _fill(ag, 200, rng)
@@ -174,32 +198,33 @@ def test_learn_fp16_matches_mixed_emulation_and_fp32_oracle():
     for j in range(ag.NA):
         S, Aa, Rn, S2, D = _host_batch(ag, j, idx[j])
         zero = np.zeros_like(p0[j])
-        l_e, g_e, p_e, m_e, v_e = _mixed_emulation(p0[j], t0[j], zero, zero.copy(), S, Aa, Rn, S2, D, 1)
+        l_e, g_e, p_e, m_e, v_e = _mixed_emulation(p0[j], t0[j], zero, zero.copy(), S, Aa, Rn, S2, D, 1,
+                                                   rnd=rnd)
         # tight: same rounding points.  What remains is accumulation order: an
         # f16 ulp here and there, and ReLU-boundary flips (a pre-activation within
         # rounding of 0 lands on opposite sides), each of which moves one column
         # of dW1 or one row of dW2 -- a few dozen entries per agent.
-        np.testing.assert_allclose(loss[j], l_e, rtol=2e-3)
+        np.testing.assert_allclose(loss[j], l_e, rtol=tl)
         g_g = m_g[j] / np.float32(0.1)
         assert np.isfinite(g_g).all()
         gs = np.abs(g_e).max()
-        close = np.abs(g_g - g_e) <= 2e-3 * gs + 1e-2 * np.abs(g_e)
+        close = np.abs(g_g - g_e) <= ta * gs + tr * np.abs(g_e)
         assert close.mean() > 0.99, f"agent {j}: {np.sum(~close)} gradient entries off"
         H = 128
         o_b1, o_b2, o_w3 = 89 * H, 89 * H + H + H * H, 89 * H + H + H * H + H
         for lo, hi in [(o_b1, o_b1 + H), (o_b2, o_b2 + H), (o_w3, o_w3 + 4 * H + 4)]:
-            assert close[lo:hi].mean() > 0.97, (lo, hi)
+            assert close[lo:hi].mean() > tshare, (lo, hi)
         # stated tolerance vs the fp32 oracle (rtol 2e-2 on the loss)
         p1, m1, v1 = p0[j].copy(), zero.copy(), zero.copy()
         l32 = O.learn(p1, t0[j], m1, v1, S, Aa, Rn, S2, D, 1)
-        np.testing.assert_allclose(loss[j], l32, rtol=2e-2)
+        np.testing.assert_allclose(loss[j], l32, rtol=t32)
         # backprop must use the PRE-update W3 (Adam on W3 runs first in the
         # kernel): the gradients of W1/b1/W2/b2 sit far closer to that emulation
         # than to one using the post-update W3 (a ~1% relative shift)
         o_w3e = o_w3 + 4 * H
         w3_new = p_e[o_w3:o_w3e].reshape(H, 4)
         _, g_bad, _, _, _ = _mixed_emulation(p0[j], t0[j], zero, zero.copy(), S, Aa, Rn, S2, D, 1,
-                                             w3_dz2=w3_new)
+                                             w3_dz2=w3_new, rnd=rnd)
         big = np.abs(g_e[:o_w3]) > 0.1 * np.abs(g_e[:o_w3]).max()
         err_ok = np.median(np.abs(g_g[:o_w3] - g_e[:o_w3])[big] / np.abs(g_e[:o_w3])[big])
         err_bad = np.median(np.abs(g_g[:o_w3] - g_bad[:o_w3])[big] / np.abs(g_bad[:o_w3])[big])
@@ -209,4 +234,7 @@ def test_learn_fp16_matches_mixed_emulation_and_fp32_oracle():
     # second learn triggers the target sync (frequency 2)
     ag.learn()
     np.testing.assert_array_equal(ag.target.cpu().numpy(), ag.params.cpu().numpy())
+    # ... and its 16-bit shadow (the target forward's operand) is the RNE rounding
+    th = ag.target_h[:, :ag.P].float().cpu().numpy()
+    np.testing.assert_array_equal(th, rnd(ag.target.cpu().numpy()))
 

@@ -2,15 +2,15 @@
 #   bash tools/cmp_variants.sh "-DFOO" "-DBAR=2" "file:tools/_base_learn_f16.hip"
 # BENCH_ARGS (env) is appended to the bench command line; LEARN_ONLY=1 times
 # the learn kernel alone (tools/learn_bench.py, median/min of 60 launches).
-# A "file:" variant builds with that file in place of csrc/learn_f16.hip.
+# A "file:" variant builds with that file in place of csrc/learn_h16.hpp.
 set -e
-SRC=dmdqn_amd/csrc/learn_f16.hip
-cp $SRC /tmp/_cur_learn_f16.hip
+SRC=dmdqn_amd/csrc/learn_h16.hpp
+cp $SRC /tmp/_cur_learn_h16.hpp
 for v in "$@"; do
   if [[ "$v" == file:* ]]; then
     cp "${v#file:}" $SRC; flags=""
   else
-    cp /tmp/_cur_learn_f16.hip $SRC; flags="$v"
+    cp /tmp/_cur_learn_h16.hpp $SRC; flags="$v"
   fi
   DMDQN_EXTRA_FLAGS="$flags -DDMDQN_VARIANT" python3 -m dmdqn_amd.build > gpurun_out/build.log 2>&1
   if [ -n "$LEARN_ONLY" ]; then
@@ -19,5 +19,5 @@ for v in "$@"; do
     timeout -k 10 300 python3 bench.py --no-cpu-baseline $BENCH_ARGS | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(\"$v\", d[\"value\"], d[\"roofline\"][\"avg_launch_ms\"], d[\"roofline\"][\"frac\"])"
   fi
 done
-cp /tmp/_cur_learn_f16.hip $SRC
+cp /tmp/_cur_learn_h16.hpp $SRC
 DMDQN_EXTRA_FLAGS="" python3 -m dmdqn_amd.build > gpurun_out/build.log 2>&1  # leave the current source built

@@ -1,7 +1,7 @@
-"""Diagnostic: the fp16 learn kernel alone at C3 size (16 agents x 1024 envs)
+"""Diagnostic: the fp16 (or --bf16) learn kernel alone at C3 size (16 agents x 1024 envs)
 on random replay contents, timed with HIP events on one stream.  Prints the
 median and min of N launches (ms) -- a tighter A/B signal than bench.py.
-usage: python tools/learn_bench.py [N] [--shared]"""
+usage: python tools/learn_bench.py [N] [--shared] [--bf16]"""
 import json
 import sys
 
@@ -13,8 +13,9 @@ from dmdqn_amd.agent import AgentConfig, BatchedDQN  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 40
 shared = "--shared" in sys.argv
+prec = "bf16" if "--bf16" in sys.argv else "fp16"
 E, A = 1024, 16
-ag = BatchedDQN(E, A, AgentConfig(precision="fp16", seed=0, shared_params=shared,
+ag = BatchedDQN(E, A, AgentConfig(precision=prec, seed=0, shared_params=shared,
                                   replay_buffer_size=1000))
 g = torch.Generator(device="cuda").manual_seed(0)
 for t in range(200):
@@ -34,4 +35,4 @@ for _ in range(N):
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1))
 print(json.dumps({"median_ms": round(float(np.median(ts)), 4), "min_ms": round(float(min(ts)), 4),
-                  "n": N, "shared": shared}))
+                  "n": N, "shared": shared, "precision": prec}))
