@@ -58,7 +58,8 @@ PRECISIONS = {"fp32": 0, "fp16": 1, "bf16": 2}
 H16_DTYPES = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
 
-D_PAD = 96  # layer-1 fan-in padded for 32-byte MFMA fragments (qnet_layout.hpp)
+D_PAD = 96  # feature stride of an observation row in the replay ring (qnet_layout.hpp)
+D_TILED = 88  # layer-1 features held in 16x16 tiles; feature 88 is a separate column
 
 
 def n_params_keras(hidden, n_actions=N_ACTIONS):
@@ -69,9 +70,10 @@ def n_params_keras(hidden, n_actions=N_ACTIONS):
 
 def n_params(hidden, n_actions=N_ACTIONS):
     """Floats per agent in the device layout (qnet_layout.hpp):
-    W1T[H][96] | W2T[H][H] | W3T[4][H] | b1[H] | b2[H] | b3[4]."""
+    W1T[H][0..87] | W1T[H][88] | W2T[H][H] | W3T[4][H] | b1[H] | b2[H] | b3[4]
+    -- the Keras parameter count, no padding."""
     H = hidden
-    return H * D_PAD + H * H + n_actions * H + 2 * H + n_actions
+    return H * D_IN + H * H + n_actions * H + 2 * H + n_actions
 
 
 def tile_wt(WT):
@@ -93,6 +95,31 @@ def untile_wt(flat, N, K):
     return t.reshape(lead + (N, K))
 
 
+def tile_w1(W1T):
+    """[..., H, 89] row-major W1^T -> [..., 89*H] device order (qnet_layout.hpp
+    qn_w1): per 16 neurons the tiles of features 0..79 and the first half
+    (80..87) of the next, then the column of feature 88."""
+    lead, H = W1T.shape[:-2], W1T.shape[-2]
+    pad = np.zeros(lead + (H, D_PAD), np.float32)
+    pad[..., :D_IN] = W1T
+    t = tile_wt(pad).reshape(lead + (H // 16, 6, 2, 16, 8))
+    blk = np.concatenate([t[..., :5, :, :, :].reshape(lead + (H // 16, 1280)),
+                          t[..., 5, 0, :, :].reshape(lead + (H // 16, 128))], axis=-1)
+    return np.concatenate([blk.reshape(lead + (H * D_TILED,)), W1T[..., D_TILED]], axis=-1)
+
+
+def untile_w1(flat, H):
+    """Inverse of tile_w1: [..., 89*H] -> [..., H, 89]."""
+    lead = flat.shape[:-1]
+    blk = flat[..., :H * D_TILED].reshape(lead + (H // 16, D_TILED * 16))
+    t = np.zeros(lead + (H // 16, 6, 2, 16, 8), np.float32)
+    t[..., :5, :, :, :] = blk[..., :1280].reshape(lead + (H // 16, 5, 2, 16, 8))
+    t[..., 5, 0, :, :] = blk[..., 1280:].reshape(lead + (H // 16, 16, 8))
+    W1T = untile_wt(t.reshape(lead + (H * D_PAD,)), H, D_PAD)[..., :D_IN].copy()
+    W1T[..., D_TILED] = flat[..., H * D_TILED:H * D_IN]
+    return W1T
+
+
 def keras_to_kernel(flat, hidden):
     """[..., P_keras] Keras get_weights order -> [..., P_kernel] device layout."""
     H = hidden
@@ -105,26 +132,24 @@ def keras_to_kernel(flat, hidden):
     b2 = flat[..., o:o + H]; o += H
     W3 = flat[..., o:o + H * N_ACTIONS].reshape(lead + (H, N_ACTIONS)); o += H * N_ACTIONS
     b3 = flat[..., o:o + N_ACTIONS]
-    W1T = np.zeros(lead + (H, D_PAD), np.float32)
-    W1T[..., :D_IN] = np.swapaxes(W1, -1, -2)
-    parts = [tile_wt(W1T), tile_wt(np.swapaxes(W2, -1, -2)),
+    parts = [tile_w1(np.swapaxes(W1, -1, -2)), tile_wt(np.swapaxes(W2, -1, -2)),
              np.swapaxes(W3, -1, -2).reshape(lead + (-1,)), b1, b2, b3]
     return np.concatenate(parts, axis=-1)
 
 
 def kernel_to_keras(flat, hidden):
-    """Inverse of keras_to_kernel (drops the zero feature padding)."""
+    """Inverse of keras_to_kernel."""
     H = hidden
     flat = np.asarray(flat, dtype=np.float32)
     lead = flat.shape[:-1]
     o = 0
-    W1T = untile_wt(flat[..., o:o + H * D_PAD], H, D_PAD); o += H * D_PAD
+    W1T = untile_w1(flat[..., o:o + H * D_IN], H); o += H * D_IN
     W2T = untile_wt(flat[..., o:o + H * H], H, H); o += H * H
     W3T = flat[..., o:o + N_ACTIONS * H].reshape(lead + (N_ACTIONS, H)); o += N_ACTIONS * H
     b1 = flat[..., o:o + H]; o += H
     b2 = flat[..., o:o + H]; o += H
     b3 = flat[..., o:o + N_ACTIONS]
-    parts = [np.swapaxes(W1T[..., :D_IN], -1, -2).reshape(lead + (-1,)), b1,
+    parts = [np.swapaxes(W1T, -1, -2).reshape(lead + (-1,)), b1,
              np.swapaxes(W2T, -1, -2).reshape(lead + (-1,)), b2,
              np.swapaxes(W3T, -1, -2).reshape(lead + (-1,)), b3]
     return np.concatenate(parts, axis=-1)

@@ -54,7 +54,8 @@ struct Scratch {
 };
 
 // Y[b][n] = act(X[b][:] . W[:][n] + bias[n]) for the wave's 16-column tile.
-// X rows come from LDS (f16 or f32), W^T [N][KS] (tiled, qn_wt) from global memory.
+// X rows come from LDS (f16 or f32), W^T [N][KS] (tiled, qn_wt; KS = 0: the
+// layer-1 block, qn_w1) from global memory.
 template <int H, int K, typename TX, bool RELU, int KS>
 __device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *WT, const float *bias,
                                            float *Y, int ldy, int n0, int nvalid) {
@@ -65,7 +66,8 @@ __device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *WT
     const int n = n0 + lr;
     for (int k0 = 0; k0 < K; k0 += 4) {
         const int kk = k0 + lk;
-        const float bv = (kk < K && lr < nvalid) ? WT[qn_wt(n, kk, KS)] : 0.0f;
+        const float bv =
+            (kk < K && lr < nvalid) ? WT[KS == 0 ? qn_w1<H>(n, kk) : qn_wt(n, kk, KS)] : 0.0f;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const float av = (float)X[(16 * t + lr) * ldx + kk];
@@ -92,7 +94,7 @@ __device__ void forward(const float *P, const _Float16 *X, float *H1, float *H2,
     const int w = threadIdx.x >> 6;
     constexpr int NT = H / 16;  // column tiles per layer
     for (int nt = w; nt < NT; nt += 8)
-        dense_tile<H, D_, _Float16, true, QN_DP>(X, DP, P + L::oW1T, P + L::ob1, H1, H, 16 * nt, 16);
+        dense_tile<H, D_, _Float16, true, 0>(X, DP, P + L::oW1T, P + L::ob1, H1, H, 16 * nt, 16);
     __syncthreads();
     for (int nt = w; nt < NT; nt += 8)
         dense_tile<H, H, float, true, H>(H1, H, P + L::oW2T, P + L::ob2, H2, H, 16 * nt, 16);
@@ -373,7 +375,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     int i = 16 * t + 4 * lk + j;
-                    if (i < D_) adam_el(Wp, Mp, Vp, Tp, L::oW1T + qn_wt(16 * jt + lr, i, QN_DP),
+                    if (i < D_) adam_el(Wp, Mp, Vp, Tp, L::oW1T + qn_w1<H>(16 * jt + lr, i),
                                         g1[t][j], AK, sync);
                 }
         }
@@ -400,7 +402,7 @@ __global__ void __launch_bounds__(256) k_q_argmax(const float *params, size_t ps
     __syncthreads();
     for (int j = tid; j < H; j += blockDim.x) {
         float s = 0.0f;
-        for (int i = 0; i < D_; i++) s += x[i] * Wp[L::oW1T + qn_wt(j, i, QN_DP)];
+        for (int i = 0; i < D_; i++) s += x[i] * Wp[L::oW1T + qn_w1<H>(j, i)];
         s += Wp[L::ob1 + j];
         h1[j] = s > 0.0f ? s : 0.0f;
     }

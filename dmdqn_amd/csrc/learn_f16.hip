@@ -125,9 +125,11 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
     if (lg == 0) G[L::ob2 + 16 * w + lr] = GB2[0];
 #pragma unroll
     for (int t = 0; t < 6; t++)
-        *reinterpret_cast<float4 *>(G + L::oW1T + qn_wt(16 * w + lr, 16 * t + 4 * lg, DP)) =
-            make_float4(G1[t][0], G1[t][1], G1[t][2], G1[t][3]);
+        if (t < 5 || lg < 2)  // tile 5: features 80..87 (89..95 do not exist)
+            *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(16 * w + lr, 16 * t + 4 * lg)) =
+                make_float4(G1[t][0], G1[t][1], G1[t][2], G1[t][3]);
     if (lg == 0) G[L::ob1 + 16 * w + lr] = GB1[0];
+    if (lg == 2) G[L::oW1X + 16 * w + lr] = G1[5][0];  // feature 88
 }
 
 // grad[i] = scale * sum_w slab[w][i]  (fixed order over workgroups)

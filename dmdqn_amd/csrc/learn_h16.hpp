@@ -179,6 +179,39 @@ __device__ __forceinline__ half8 wfrag(const h16 *WT, int ld, int n0, int k0, in
     return r;
 }
 
+// Layer-1 A-fragment s (features 32s..32s+31) of neurons n0..n0+15 from the
+// W1 block (qn_w1): 8 consecutive features per lane.  Fragment 2's lanes
+// lg = 3 cover features 88..95, of which only 88 exists (the W1T column;
+// 89..95 are zero weights, not stored).
+__device__ __forceinline__ half8 w1frag(const float *W1, int n0, int s) {
+    const int l = threadIdx.x & 63, lg = l >> 4, n = n0 + (l & 15);
+    half8 r;
+    if (s < 2 || lg < 3) {
+        const float4 *p = reinterpret_cast<const float4 *>(W1 + qn_w1<H>(n, 32 * s + 8 * lg));
+        float4 x = p[0], y = p[1];
+        r[0] = (h16)x.x; r[1] = (h16)x.y; r[2] = (h16)x.z; r[3] = (h16)x.w;
+        r[4] = (h16)y.x; r[5] = (h16)y.y; r[6] = (h16)y.z; r[7] = (h16)y.w;
+    } else {
+#pragma unroll
+        for (int e = 1; e < 8; e++) r[e] = (h16)0.0f;
+        r[0] = (h16)W1[qn_w1<H>(n, QN_DT)];
+    }
+    return r;
+}
+
+__device__ __forceinline__ half8 w1frag(const h16 *W1, int n0, int s) {
+    const int l = threadIdx.x & 63, lg = l >> 4, n = n0 + (l & 15);
+    half8 r;
+    if (s < 2 || lg < 3) {
+        r = *reinterpret_cast<const half8 *>(W1 + qn_w1<H>(n, 32 * s + 8 * lg));
+    } else {
+#pragma unroll
+        for (int e = 1; e < 8; e++) r[e] = (h16)0.0f;
+        r[0] = W1[qn_w1<H>(n, QN_DT)];
+    }
+    return r;
+}
+
 __device__ __forceinline__ float4 ld_bias4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ float4 ld_bias4(const h16 *p) {
     const half4v h = *reinterpret_cast<const half4v *>(p);
@@ -221,7 +254,7 @@ template <typename T>
 __device__ __forceinline__ void load_w1(const T *Wg, Frags &f) {
     const int w = threadIdx.x >> 6, lg = (threadIdx.x & 63) >> 4;
 #pragma unroll
-    for (int s = 0; s < 3; s++) f.w1[s] = wfrag(Wg + L::oW1T, DP, 16 * w, 32 * s);
+    for (int s = 0; s < 3; s++) f.w1[s] = w1frag(Wg + L::oW1T, 16 * w, s);
     f.b1 = ld_bias4(Wg + L::ob1 + 16 * w + 4 * lg);
 }
 
@@ -417,17 +450,28 @@ __device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, c
 #ifndef DMDQN_EARLY_W1
 #define DMDQN_EARLY_W1 1
 #endif
-template <int NB, int NT, bool EARLY, typename Index, typename Grad>
+// `valid(tile)` says whether the lane's 4 parameters of that tile exist (the
+// W1 block stores only features 0..88; a lane with nothing to update keeps its
+// registers and touches no memory).
+struct AllValid {
+    __device__ constexpr bool operator()(int) const { return true; }
+};
+
+template <int NB, int NT, bool EARLY, typename Index, typename Grad, typename Valid = AllValid>
 __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T, Index ix,
-                                          const f32x4 *g, const AdamC &k, Grad grad) {
+                                          const f32x4 *g, const AdamC &k, Grad grad,
+                                          Valid valid = {}) {
     float4 w[2][NT], m[2][NT], v[2][NT];
     if constexpr (!EARLY) grad();
 #pragma unroll
     for (int q = 0; q < NT; q++) {
         const size_t i = ix(q);
-        w[0][q] = *reinterpret_cast<const float4 *>(W + i);
-        m[0][q] = *reinterpret_cast<const float4 *>(M + i);
-        v[0][q] = *reinterpret_cast<const float4 *>(V + i);
+        w[0][q] = m[0][q] = v[0][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (valid(q)) {
+            w[0][q] = *reinterpret_cast<const float4 *>(W + i);
+            m[0][q] = *reinterpret_cast<const float4 *>(M + i);
+            v[0][q] = *reinterpret_cast<const float4 *>(V + i);
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (EARLY) {
@@ -441,9 +485,12 @@ __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T
 #pragma unroll
             for (int q = 0; q < NT; q++) {
                 const size_t i = ix((h + 1) * NT + q);
-                w[n][q] = *reinterpret_cast<const float4 *>(W + i);
-                m[n][q] = *reinterpret_cast<const float4 *>(M + i);
-                v[n][q] = *reinterpret_cast<const float4 *>(V + i);
+                w[n][q] = m[n][q] = v[n][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (valid((h + 1) * NT + q)) {
+                    w[n][q] = *reinterpret_cast<const float4 *>(W + i);
+                    m[n][q] = *reinterpret_cast<const float4 *>(M + i);
+                    v[n][q] = *reinterpret_cast<const float4 *>(V + i);
+                }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -462,6 +509,7 @@ __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T
 #pragma unroll
         for (int q = 0; q < NT; q++) {
             const size_t i = ix(h * NT + q);
+            if (!valid(h * NT + q)) continue;
             *reinterpret_cast<float4 *>(W + i) = w[c][q];
             *reinterpret_cast<float4 *>(M + i) = m[c][q];
             *reinterpret_cast<float4 *>(V + i) = v[c][q];
@@ -919,12 +967,14 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
     // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
     {
         f32x4 g1[6], gb = {0.f, 0.f, 0.f, 0.f};
-        // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; padded
-        // features 89..95 have zero weight and zero gradient and stay zero
+        // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; tile 5
+        // holds features 80..95: lanes lg < 2 (80..87) update in the pipe, lane
+        // lg = 2's first row is feature 88 (the W1T column, below), the rest
+        // (89..95) do not exist
         adam_pipe<2, 3, DMDQN_EARLY_W1>(
             Wp, Mp, Vp, Tp,
-            [&](int t) { return (size_t)L::oW1T + qn_wt(16 * w + lr, 16 * t + 4 * lg, DP); }, g1,
-            AK, [&]() {
+            [&](int t) { return (size_t)L::oW1T + qn_w1<H>(16 * w + lr, t < 5 || lg < 2 ? 16 * t + 4 * lg : 0); },
+            g1, AK, [&]() {
 #pragma unroll
                 for (int t = 0; t < 6; t++) g1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -935,8 +985,13 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
                     for (int t = 0; t < 6; t++)
                         g1[t] = mfma(frag_tr_h<DP>(P2, b0, 16 * t), bv, g1[t]);
                 }
-            });
-        if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob1 + 16 * w + lr, gb[0], AK);
+            },
+            [&](int t) { return t < 5 || lg < 2; });
+        // b1[j] (lanes lg = 0: every row of the ones-MFMA holds the column sum)
+        // and W1T[j][88] (lanes lg = 2, row 88 of tile 5)
+        if (lg == 0 || lg == 2)
+            adam1(Wp, Mp, Vp, Tp, (lg == 0 ? L::ob1 : L::oW1X) + 16 * w + lr,
+                  lg == 0 ? gb[0] : g1[5][0], AK);
     }
     if (a.stamps) {
         __syncthreads();

@@ -11,7 +11,7 @@ from dmdqn_amd.agent import (AgentConfig, keras_adam_consts, keras_to_kernel, ke
 def test_param_counts():
     assert n_params_keras(128) == 28548  # P = 28,548 for [128,128]
     assert n_params_keras(256) == 89860
-    assert n_params(128) == 29444 and n_params(128) % 4 == 0
+    assert n_params(128) == 28548 == n_params_keras(128) and n_params(128) % 4 == 0
 
 
 def test_layout_roundtrip():
@@ -21,10 +21,17 @@ def test_layout_roundtrip():
         kk = keras_to_kernel(k, H)
         assert kk.shape == (3, n_params(H))
         np.testing.assert_array_equal(kernel_to_keras(kk, H), k)
-        # feature padding of W1T is zero
-        W1T = untile_wt(kk[:, :H * 96], H, 96)
-        assert (W1T[:, :, 89:] == 0).all()
-        np.testing.assert_array_equal(W1T[:, :, :89], np.swapaxes(k[:, :89 * H].reshape(3, 89, H), 1, 2))
+        # W1T sits at the device formula's offsets (qnet_layout.hpp qn_w1)
+        W1T = np.swapaxes(k[:, :89 * H].reshape(3, 89, H), 1, 2)
+        idx = np.array([[_qn_w1(o, i, H) for i in range(89)] for o in range(H)])
+        np.testing.assert_array_equal(kk[:, idx], W1T)
+        assert sorted(idx.ravel().tolist()) == list(range(89 * H))  # no gaps, no padding
+
+
+def _qn_w1(o, i, H):  # qnet_layout.hpp qn_w1
+    if i < 88:
+        return (o >> 4) * 1408 + ((i >> 4) << 8) + (((i >> 3) & 1) << 7) + ((o & 15) << 3) + (i & 7)
+    return 88 * H + o
 
 
 def _qn_wt(o, i, K):  # qnet_layout.hpp qn_wt
