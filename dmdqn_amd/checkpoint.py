@@ -26,7 +26,7 @@ import os
 import numpy as np
 import torch
 
-FORMAT = "dmdqn-ckpt-3"  # 3: unpadded tiled W1T (89*H floats) / tiled W2T (qnet_layout.hpp)
+FORMAT = "dmdqn-ckpt-4"  # 4: 128-B replay rows (s' rows carry a, done, r); unpadded W1T (qnet_layout.hpp)
 
 _ENV_TENSORS = ["t_x", "t_v", "t_dst", "t_head", "t_cnt", "t_phase_state", "t_ts", "t_qptr",
                 "t_stats", "halt", "phase", "tspent", "done_u8"]

@@ -23,7 +23,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int B_ = 128;     // batch (dqn_agent.py: batch_size 128)
 constexpr int D_ = 89;      // observation dim
-constexpr int DP = 96;      // padded feature stride of X (replay row bytes)
+constexpr int DP = 96;      // padded feature stride of the X image in LDS
 constexpr int NACT = 4;
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
         for (int t = tid; t < B_ * (DP / 4); t += 512) {
             int b = t / (DP / 4), q = t - b * (DP / 4);
             const char4 c = reinterpret_cast<const char4 *>(
-                ring + ((size_t)agent * a.cap + S.slot[b]) * DP)[q];
+                ring + ((size_t)agent * a.cap + S.slot[b]) * DMDQN_ROW_BYTES)[q];
             _Float16 *dst = X + b * DP + 4 * q;
             dst[0] = (_Float16)(float)c.x;
             dst[1] = (_Float16)(float)c.y;

@@ -44,13 +44,7 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
         // the independent kernel does from HBM) rather than pin 72 VGPRs
         if (TH) load_frags(TH, fr);
         else load_frags(a.target, fr);
-        batch_meta(a, agent, S);
-        {
-            Rows gn;
-            gather_issue(a.ring_n, a, agent, S.slot, gn);
-            gather_commit(R2, gn);
-        }
-        __syncthreads();
+        batch_head(a, agent, R2, S);  // X(S') in R2, metadata, z-score
         // buffer plan of k_learn_f16: the backward runs on (P1, P2) = (R2, R1)
         forward_x<true>(fr, tg, R2, R1, R1, S.z3, [WH](Frags &f) { load_w1(WH, f); },
                         [WH](Frags &f) { load_w2(WH, f); });  // X(S') stays in R2

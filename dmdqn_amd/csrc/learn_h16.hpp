@@ -553,16 +553,18 @@ __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, si
 
 struct Rows { uint2 v[3]; };
 
-// Replay rows (int8) of one agent's batch -> X f16 [128][96] in R2, in two
-// halves so the loads can be in flight across other work: issue (3 x 8 bytes
-// per thread into registers), then commit (convert + LDS store) once R2 is free.
+// Replay rows (int8, DMDQN_ROW_BYTES = one 128-B line each) of one agent's
+// batch -> X f16 [128][96] in R2, in two halves so the loads can be in flight
+// across other work: issue (3 x 8 bytes per thread into registers), then
+// commit (convert + LDS store) once R2 is free.
 __device__ __forceinline__ void gather_issue(const int8_t *ring, const dmdqn_learn_args &a,
                                              int agent, const int *slot, Rows &g) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
-        g.v[i] = reinterpret_cast<const uint2 *>(ring + ((size_t)agent * a.cap + slot[b]) * DP)[q];
+        g.v[i] = reinterpret_cast<const uint2 *>(ring + ((size_t)agent * a.cap + slot[b]) *
+                                                            DMDQN_ROW_BYTES)[q];
     }
 }
 
@@ -581,21 +583,44 @@ __device__ __forceinline__ void gather_commit(h16 *R2, const Rows &g) {
     }
 }
 
-// Batch metadata (ring slots, actions, dones) and the reward z-score of
-// ReplayBuffer.sample (dqn_agent.py:64-69): f64 mean and population std over
-// the 128 rewards in numpy's pairwise order (8 partial sums of 16), + 1e-8.
-__device__ __forceinline__ void batch_meta(const dmdqn_learn_args &a, int agent, const Scratch &S) {
+// Ring slots of the batch (deque positions -> slots).  Ends with a barrier.
+__device__ __forceinline__ void batch_slots(const dmdqn_learn_args &a, int agent, const Scratch &S) {
     const int tid = threadIdx.x;
     if (tid < B_) {
-        int pos = a.idx[(size_t)agent * B_ + tid];
-        int s = a.start + pos;
+        int s = a.start + a.idx[(size_t)agent * B_ + tid];
         if (s >= a.cap) s -= a.cap;
-        size_t r = (size_t)agent * a.cap + s;
         S.slot[tid] = s;
-        S.act[tid] = a.ring_a[r];
-        S.r64[tid] = a.ring_r[r];
-        S.dn[tid] = a.ring_d[r] ? 1.0f : 0.0f;
     }
+    __syncthreads();
+}
+
+// The transition metadata (a, done, r) from the s' rows (bytes 96..111 of the
+// line gather_issue(ring_n) reads: the same HBM line, in flight together).
+struct Meta { uint4 v; };
+
+__device__ __forceinline__ void meta_issue(const dmdqn_learn_args &a, int agent, const int *slot,
+                                           Meta &m) {
+    const int tid = threadIdx.x;
+    if (tid < B_)
+        m.v = *reinterpret_cast<const uint4 *>(a.ring_n + ((size_t)agent * a.cap + slot[tid]) *
+                                                                DMDQN_ROW_BYTES + DMDQN_ROW_A);
+}
+
+__device__ __forceinline__ void meta_commit(const Meta &m, const Scratch &S) {
+    static_assert(DMDQN_ROW_D == DMDQN_ROW_A + 1 && DMDQN_ROW_R == DMDQN_ROW_A + 8, "row tail");
+    const int tid = threadIdx.x;
+    if (tid < B_) {
+        S.act[tid] = m.v.x & 0xffu;
+        S.dn[tid] = (m.v.x >> 8) & 0xffu ? 1.0f : 0.0f;
+        S.r64[tid] = __longlong_as_double((long long)(((unsigned long long)m.v.w << 32) | m.v.z));
+    }
+}
+
+// The reward z-score of ReplayBuffer.sample (dqn_agent.py:64-69) over S.r64:
+// f64 mean and population std over the 128 rewards in numpy's pairwise order
+// (8 partial sums of 16), + 1e-8.  Starts with a barrier (S.r64 complete).
+__device__ __forceinline__ void zscore(const Scratch &S) {
+    const int tid = threadIdx.x;
     __syncthreads();
     if (tid < 8) {
         double acc = S.r64[tid];
@@ -629,6 +654,20 @@ __device__ __forceinline__ void batch_meta(const dmdqn_learn_args &a, int agent,
     }
     __syncthreads();
     if (tid < B_) S.rn[tid] = (float)__ddiv_rn(__dsub_rn(S.r64[tid], S.red[8]), S.red[9]);
+}
+
+// Slots, then the s' rows -> X(S') in R2 plus the metadata, then the z-score.
+// X(S') is visible to every thread on return (zscore's barriers).
+__device__ __forceinline__ void batch_head(const dmdqn_learn_args &a, int agent, h16 *R2,
+                                           const Scratch &S) {
+    batch_slots(a, agent, S);
+    Rows gn;
+    Meta mt;
+    gather_issue(a.ring_n, a, agent, S.slot, gn);
+    meta_issue(a, agent, S.slot, mt);
+    gather_commit(R2, gn);
+    meta_commit(mt, S);
+    zscore(S);
 }
 
 // Double-DQN target y = r^ + gamma (1 - d) Q_target(S')[argmax Q_online(S')]
@@ -815,17 +854,11 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
     if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
     else stage_out(Tp, W3L + NACT * H, B3L + NACT);
 
-    batch_meta(a, agent, S);
+    // ---- slots, X(S') + metadata from the s' rows, z-score
+    batch_head(a, agent, R2, S);
     STAMP(1);
-
-    // ---- target(S') -> z3 ; online(S') -> Q ; y
-    {
-        Rows gn;
-        gather_issue(a.ring_n, a, agent, S.slot, gn);
-        gather_commit(R2, gn);
-    }
-    __syncthreads();
     STAMP(2);
+    // ---- target(S') -> z3 ; online(S') -> Q ; y
     // target forward keeps X(S') in R2; the online net's fragments (reused by
     // both online forwards) load layer by layer as the target's die
     const float *Wpc = Wp;

@@ -1,7 +1,10 @@
 // replay.hip -- replay ring store (ReplayBuffer.add, src/agents/dqn_agent.py:31-57).
 //
 // Layout (per agent slot, capacity cap, ring position = total_adds % cap):
-//   ring_s, ring_n : int8  [NA][cap][96]   s and s' rows (89 used, 7 zero pad)
+//   ring_s, ring_n : int8  [NA][cap][128]  s and s' rows: features 0..88, zero
+//                                          to byte 95; the s' row also holds a
+//                                          (byte 96), done (97) and r (f64,
+//                                          104..111) -- the learn kernels' copy
 //   ring_a         : uint8 [NA][cap]
 //   ring_r         : f64   [NA][cap]       Python-float reward, kept in f64 so
 //                                          the batch z-score is numpy-exact
@@ -22,27 +25,34 @@ __device__ __forceinline__ int8_t to_i8(float v, int32_t *err) {
     return (int8_t)(int)r;
 }
 
-// One thread per (agent, 4-byte group): 24 groups of 4 int8 per row.
+// One thread per (agent, 4-byte group): 32 groups of 4 bytes per row.
 __global__ void k_replay_store(int NA, int cap, int slot, const float *obs_s, const float *obs_n,
                                const int32_t *act, const double *rew, const uint8_t *done,
                                int8_t *ring_s, int8_t *ring_n, uint8_t *ring_a, double *ring_r,
                                uint8_t *ring_d, int32_t *err) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int agent = t / 24, grp = t - agent * 24;
+    constexpr int G = DMDQN_ROW_BYTES / 4;
+    const int agent = t / G, grp = t - agent * G;
     if (agent >= NA) return;
     const size_t row = ((size_t)agent * cap + slot);
-    char4 cs, cn;
-    int8_t bs[4], bn[4];
+    uint32_t ws = 0, wn = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        int i = grp * 4 + q;
-        bs[q] = i < DMDQN_OBS_DIM ? to_i8(obs_s[(size_t)agent * DMDQN_OBS_DIM + i], err) : 0;
-        bn[q] = i < DMDQN_OBS_DIM ? to_i8(obs_n[(size_t)agent * DMDQN_OBS_DIM + i], err) : 0;
+        const int i = grp * 4 + q;
+        if (i < DMDQN_OBS_DIM) {
+            ws |= (uint32_t)(uint8_t)to_i8(obs_s[(size_t)agent * DMDQN_OBS_DIM + i], err) << (8 * q);
+            wn |= (uint32_t)(uint8_t)to_i8(obs_n[(size_t)agent * DMDQN_OBS_DIM + i], err) << (8 * q);
+        }
     }
-    cs = make_char4(bs[0], bs[1], bs[2], bs[3]);
-    cn = make_char4(bn[0], bn[1], bn[2], bn[3]);
-    reinterpret_cast<char4 *>(ring_s + row * DMDQN_ROW_BYTES)[grp] = cs;
-    reinterpret_cast<char4 *>(ring_n + row * DMDQN_ROW_BYTES)[grp] = cn;
+    if (4 * grp == DMDQN_ROW_A) {
+        static_assert(DMDQN_ROW_D == DMDQN_ROW_A + 1, "a and done share a word");
+        wn = (uint32_t)(uint8_t)act[agent] | (done[agent] ? 1u : 0u) << 8;
+    } else if (4 * grp == DMDQN_ROW_R || 4 * grp == DMDQN_ROW_R + 4) {
+        const unsigned long long rb = __double_as_longlong(rew[agent]);
+        wn = (uint32_t)(4 * grp == DMDQN_ROW_R ? rb : rb >> 32);
+    }
+    reinterpret_cast<uint32_t *>(ring_s + row * DMDQN_ROW_BYTES)[grp] = ws;
+    reinterpret_cast<uint32_t *>(ring_n + row * DMDQN_ROW_BYTES)[grp] = wn;
     if (grp == 0) {
         ring_a[row] = (uint8_t)act[agent];
         ring_r[row] = rew[agent];
@@ -64,7 +74,7 @@ extern "C" int dmdqn_replay_store(int NA, int cap, int slot, const float *obs_s,
     DMDQN_REQUIRE(obs_s && obs_n && act && rew && done && ring_s && ring_n && ring_a && ring_r &&
                       ring_d && err,
                   "dmdqn_replay_store: null pointer");
-    const int threads = NA * 24;
+    const int threads = NA * (DMDQN_ROW_BYTES / 4);
     hipLaunchKernelGGL(k_replay_store, dim3((threads + 255) / 256), dim3(256), 0,
                        as_stream(stream), NA, cap, slot, obs_s, obs_n, act, rew, done, ring_s,
                        ring_n, ring_a, ring_r, ring_d, err);

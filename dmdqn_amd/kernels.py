@@ -12,7 +12,7 @@ from ._lib import call, ptr, stream_of
 MT_WORDS = 625
 OBS_DIM = 89
 LOCAL_DIM = 17
-ROW_BYTES = 96
+ROW_BYTES = 128  # include/dmdqn.h DMDQN_ROW_BYTES (s' rows carry a, done, r at 96/97/104)
 
 
 def _check(t, dtype, shape=None, name="tensor"):

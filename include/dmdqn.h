@@ -34,8 +34,15 @@ extern "C" {
 /* Observation / local-state sizes (order_lanes.py:497, :554). */
 #define DMDQN_OBS_DIM 89
 #define DMDQN_LOCAL_DIM 17
-/* Replay row stride in bytes for int8 observation storage (89 padded). */
-#define DMDQN_ROW_BYTES 96
+/* Replay rows: one 128-byte line per stored observation (int8 features 0..88,
+ * zero to byte 95).  The s' row of a transition also carries the transition's
+ * action (byte DMDQN_ROW_A), done flag (DMDQN_ROW_D) and f64 reward (bytes
+ * DMDQN_ROW_R..+7), so a sampled transition is one aligned line of s' plus one
+ * of s -- no scattered reads of the per-slot arrays in the learn kernels. */
+#define DMDQN_ROW_BYTES 128
+#define DMDQN_ROW_A 96
+#define DMDQN_ROW_D 97
+#define DMDQN_ROW_R 104
 
 const char *dmdqn_last_error(void);
 int dmdqn_version(void);
@@ -82,8 +89,10 @@ int dmdqn_observe(int R, int C, int E, const int32_t *halt, const int32_t *phase
  * per agent into ring slot `slot` (capacity `cap`).  Observations are stored
  * as int8 rows of DMDQN_ROW_BYTES (exact for this env's integer features; a
  * non-representable value sets *err to DMDQN_ERANGE).  done: uint8 [NA].
- * ring_s / ring_n int8 [NA][cap][96]; ring_a uint8 [NA][cap];
- * ring_r f64 [NA][cap]; ring_d uint8 [NA][cap]; err int32 [1] (device). */
+ * ring_s / ring_n int8 [NA][cap][DMDQN_ROW_BYTES] (ring_n rows also receive
+ * a, done and r at DMDQN_ROW_A / _D / _R); ring_a uint8 [NA][cap];
+ * ring_r f64 [NA][cap]; ring_d uint8 [NA][cap] (the same values, per slot, for
+ * the fp32 learn kernel and the host); err int32 [1] (device). */
 int dmdqn_replay_store(int NA, int cap, int slot, const float *obs_s,
                        const float *obs_n, const int32_t *act, const double *rew,
                        const uint8_t *done, int8_t *ring_s, int8_t *ring_n,

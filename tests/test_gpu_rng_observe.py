@@ -129,6 +129,14 @@ def test_replay_store_roundtrip_and_range_check():
         np.testing.assert_array_equal(ring.a.cpu().numpy()[:, slot], a.numpy())
         np.testing.assert_array_equal(ring.r.cpu().numpy()[:, slot], r.numpy())
         np.testing.assert_array_equal(ring.d.cpu().numpy()[:, slot], d.numpy())
+        # the s' row's tail carries the same a, done, r for the learn kernels
+        # (include/dmdqn.h DMDQN_ROW_A/_D/_R); everything else past 88 is zero
+        N = ring.n.cpu().numpy()[:, slot].view(np.uint8)
+        np.testing.assert_array_equal(N[:, 96], a.numpy())
+        np.testing.assert_array_equal(N[:, 97], d.numpy())
+        np.testing.assert_array_equal(N[:, 104:112].copy().view(np.float64)[:, 0], r.numpy())
+        tail = np.delete(np.arange(89, 128), [96 - 89, 97 - 89] + list(range(104 - 89, 112 - 89)))
+        np.testing.assert_array_equal(N[:, tail], 0)
     bad = torch.zeros((NA, 89), device=DEV)
     bad[3, 5] = 0.5
     ring.store(bad, bad, torch.zeros(NA, dtype=torch.int32, device=DEV),
