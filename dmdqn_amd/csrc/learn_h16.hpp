@@ -553,13 +553,24 @@ __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, si
 
 struct Rows { uint2 v[3]; };
 
+// threadIdx.x behind an empty asm: the per-thread addresses derived from it
+// are recomputed at each use instead of being common-subexpressioned across
+// the whole kernel (the three gathers share their slot-read and LDS-store
+// addresses; kept live from the first to the last they spilled to scratch --
+// 18 KB of scratch writes per workgroup reaching HBM, and vmcnt(0) reloads).
+__device__ __forceinline__ int fresh_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // Replay rows (int8, DMDQN_ROW_BYTES = one 128-B line each) of one agent's
 // batch -> X f16 [128][96] in R2, in two halves so the loads can be in flight
 // across other work: issue (3 x 8 bytes per thread into registers), then
 // commit (convert + LDS store) once R2 is free.
 __device__ __forceinline__ void gather_issue(const int8_t *ring, const dmdqn_learn_args &a,
                                              int agent, const int *slot, Rows &g) {
-    const int tid = threadIdx.x;
+    const int tid = fresh_tid();
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
@@ -569,7 +580,7 @@ __device__ __forceinline__ void gather_issue(const int8_t *ring, const dmdqn_lea
 }
 
 __device__ __forceinline__ void gather_commit(h16 *R2, const Rows &g) {
-    const int tid = threadIdx.x;
+    const int tid = fresh_tid();
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
