@@ -142,6 +142,11 @@ def main():
                     help="stream schedule (dmdqn_amd/trainer.py; all bit-identical): none = one "
                          "stream; sample = replay draws on a side stream beside act/sim/observe/"
                          "store; full = step t+1's act/sim/observe/sample beside learn t")
+    ap.add_argument("--cu-split", type=int, default=0,
+                    help="with --overlap full/sample: run the side stream on this many CUs "
+                         "and the learn stream on the rest (CU-masked HIP streams)")
+    ap.add_argument("--cu-stride", action="store_true",
+                    help="--cu-split picks every k-th CU instead of CUs 0..N-1")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo; only barrier + timing use it")
     args = ap.parse_args()
@@ -163,14 +168,23 @@ def main():
 
     # all work on one dedicated stream: HIP events recorded on the legacy null
     # stream block the host and would inflate the timed region
-    work = torch.cuda.Stream(dev)
+    side = None
+    if args.cu_split:
+        from dmdqn_amd._lib import cu_masked_stream
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        k = args.cu_split
+        side_cus = ([round(i * n_cu / k) for i in range(k)] if args.cu_stride else list(range(k)))
+        work = cu_masked_stream([c for c in range(n_cu) if c not in set(side_cus)], dev)
+        side = cu_masked_stream(side_cus, dev)
+    else:
+        work = torch.cuda.Stream(dev)
     torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
     # independent nets are seeded per rank; the shared net must start identical on every rank
     agent_cfg = AgentConfig(precision=args.precision, seed=1000 if args.shared else 1000 + rank,
                             shared_params=args.shared)
-    tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap)
+    tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side)
     E, A = tr.env.E, tr.env.A
     NA = E * A
     for _ in range(agent_cfg.batch_size - 1):  # replay fill (no learn yet)

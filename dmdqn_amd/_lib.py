@@ -21,6 +21,8 @@ SIGNATURES = {
     "dmdqn_observe": [i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "dmdqn_replay_store": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dmdqn_replay_sample": [vp, i32, i32, i32, i32, vp, vp],
+    "dmdqn_stream_create_cumask": [u32, vp, vp],
+    "dmdqn_stream_destroy": [vp],
 }
 
 
@@ -79,3 +81,19 @@ def ptr(t):
 def stream_of(device=None):
     import torch
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def cu_masked_stream(cus, device=None):
+    """A torch ExternalStream whose kernels run only on the CU indices `cus`
+    (dmdqn_stream_create_cumask).  The stream lives for the process."""
+    import torch
+    cus = sorted(set(int(c) for c in cus))
+    if not cus or cus[0] < 0:
+        raise ValueError("cu_masked_stream: need a non-empty set of CU indices")
+    words = cus[-1] // 32 + 1
+    mask = (C.c_uint32 * words)()
+    for c in cus:
+        mask[c // 32] |= 1 << (c % 32)
+    out = C.c_void_p()
+    call("dmdqn_stream_create_cumask", words, mask, C.byref(out))
+    return torch.cuda.ExternalStream(out.value, device=device)

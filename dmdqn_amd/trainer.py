@@ -52,14 +52,18 @@ class StepStats:
 
 class Trainer:
     def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
-                 overlap="none"):
+                 overlap="none", side_stream=None):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
         if overlap is True or overlap is False:
             overlap = "full" if overlap else "none"
         if overlap not in SCHEDULES:
             raise ValueError(f"overlap must be one of {SCHEDULES}")
         self.overlap = overlap
-        self.side = torch.cuda.Stream(self.env.device) if overlap != "none" else None
+        # side_stream: e.g. a CU-masked stream (_lib.cu_masked_stream), so the
+        # side work and the learn split the chip instead of sharing CU slots
+        self.side = None
+        if overlap != "none":
+            self.side = side_stream if side_stream is not None else torch.cuda.Stream(self.env.device)
         self._ev_store = self._ev_learn = None
         self._join = True  # the side stream's first work waits for everything before it
         self.agent = BatchedDQN(self.env.E, self.env.A, agent_cfg or AgentConfig(), device=device,

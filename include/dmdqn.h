@@ -47,6 +47,14 @@ extern "C" {
 const char *dmdqn_last_error(void);
 int dmdqn_version(void);
 
+/* A HIP stream (returned in *stream as hipStream_t) whose kernels run only on
+ * the CUs set in mask[n_words] (CU i = bit i % 32 of word i / 32).  The
+ * trainer's optional split schedule runs the next step's act / sim / observe /
+ * sample on such a stream beside the learn on the complementary one.  No
+ * reference counterpart (SUMO stepped in its own process). */
+int dmdqn_stream_create_cumask(uint32_t n_words, const uint32_t *mask, void **stream);
+int dmdqn_stream_destroy(void *stream);
+
 /* ------------------------------------------------------------------ streams
  * Seed E MT19937 streams on the device.
  *  _np: numpy legacy RandomState.seed(int) (init_genrand); replaces the global
