@@ -174,15 +174,18 @@ int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *ac
  * per agent): replay gather (ReplayBuffer.sample :64-84, z-scored rewards),
  * Double-DQN target, MSE loss, backward and Keras-3 Adam, fused.
  * Parameters (and target, Adam m, v) use the device layout of qnet_layout.hpp
- * per agent: W1T[H][96] W2T[H][H] W3T[4][H] b1[H] b2[H] b3[4] -- the Keras
- * kernels transposed, fan-in padded to 96 (P floats, row stride P; the host
- * converts to / from the Keras get_weights() order).
+ * per agent: W1T[H][0..87] (tiled) W1T[H][88] W2T[H][H] (tiled) W3T[4][H] b1[H]
+ * b2[H] b3[4] -- the Keras kernels transposed, exactly the Keras parameter count
+ * (P floats, row stride P; the host converts to / from the Keras get_weights()
+ * order).
  * precision: 0 = fp32 MFMA (exact f32 products), 1 = fp16 MFMA with fp32
  * accumulation and fp32 master weights (the reference's mixed_float16),
  * 2 = the same with bf16 MFMA operands (mixed_bfloat16; BASELINE config C2). */
 typedef struct dmdqn_learn_args {
     int32_t NA, cap, start, batch, hidden, precision, sync_target, P;
-    const int8_t *ring_s, *ring_n;   /* [NA][cap][96]                        */
+    const int8_t *ring_s, *ring_n;   /* [NA][cap][DMDQN_ROW_BYTES]; the 16-bit
+                                        kernels read a, done, r from the s'
+                                        row, the fp32 kernel from the arrays */
     const uint8_t *ring_a, *ring_d;  /* [NA][cap]                            */
     const double *ring_r;            /* [NA][cap]                            */
     const int32_t *idx;              /* [NA][batch] deque positions          */
