@@ -93,7 +93,7 @@ def sim_state_fits_lds(rows, cols, cap=24):
     """Mirror of sim.hip's path choice (state image + topology tables <= LDS)."""
     A, X = rows * cols, 2 * rows + 2 * cols
     NL = 3 * (4 * A + X)
-    state = NL * cap * 12 + NL * 24 + A * 24 + 16 + (4 * A + 1) * 4
+    state = NL * cap * 10 + NL * 24 + A * 24 + 16 + (4 * A + 1) * 4
     topo = (A + (4 * A + X) + 4 * A + 2 * X + (4 * A + X)) * 4
     return state + topo <= 160 * 1024 - 64
 
@@ -120,10 +120,23 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
 SIM_PROBE_STEPS = 10  # untimed steps after the timed region that time the sim
 
 
+def _step_roofline(value, K, vbar, A, P, shared, NA):
+    """Whole-step HBM figure of BASELINE.md (roofline accounting): per agent-env
+    step B_sim = 20*K*V-bar/A, B_obs = 424, B_store = 721 and B_learn =
+    128*721 + 28*P (shared: the 28*P of the one net amortised over NA agents)."""
+    b_sim = SIM_BYTES_PER_VEH_SUBSTEP * K * vbar / A
+    b_learn = 128 * REPLAY_ROW_BYTES + (28 * P / NA if shared else 28 * P)
+    b = b_sim + 424 + 721 + b_learn
+    return {"bytes_per_agent_step": round(b, 1), "achieved": round(b * value / 1e9, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(b * value / 1e9 / HBM_PEAK_GBS, 4),
+            "parts": {"sim": round(b_sim, 1), "obs": 424, "store": 721, "learn": round(b_learn, 1)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200,
+                    help="timed RL steps (SURVEY 8d: >= 200 vector steps after warm-up)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--envs", type=int, default=1024, help="env replicas per GPU")
     ap.add_argument("--rows", type=int, default=4)
@@ -308,6 +321,10 @@ def main():
             },
             "cpu_baseline": cpu,
             # secondary figures SURVEY 8d asks for next to the headline roofline
+            # BASELINE.md's whole-step figure: canonical bytes of one agent-env step
+            # (B_sim + B_obs + B_store + B_learn) x steps/s over 8 TB/s
+            "step_roofline": _step_roofline(value, tr.env.cfg.step_duration, vbar, A, P,
+                                            args.shared, NA),
             "sim_roofline": _sim_roofline(E, tr.env.cfg.step_duration, vbar, sim_ms,
                                           read_traffic(f"{wl}_sim"),
                                           sim_state_fits_lds(args.rows, args.cols)),

@@ -197,7 +197,8 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
         // ---- phase 2: pool swaps, lane = agent (groups of 64 agents)
         for (int j0 = 0; j0 < A; j0 += 64) {
             const int G = min(64, A - j0);
-            for (uint32_t t = l; t < (uint32_t)G * n; t += 64) pool[t] = (uint16_t)(t % n);
+            for (uint32_t q = l; q < n; q += 64)  // pool[g][q] = q (no runtime modulo)
+                for (int g = 0; g < G; g++) pool[(size_t)g * n + q] = (uint16_t)q;
             __syncthreads();
             if (l < G) {
                 uint16_t *P = pool + (size_t)l * n;

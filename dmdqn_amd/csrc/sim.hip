@@ -23,6 +23,8 @@
 //         granted fronts leave, arrivals are removed
 //   D     target lanes append the vehicle they granted
 //   E     origin queues insert one departed vehicle per edge if there is room
+#include <type_traits>
+
 #include "common.hpp"
 #include "sim.hpp"
 
@@ -33,17 +35,21 @@ __device__ __forceinline__ int last_slot(int head, int cnt, int cap) {
     return s >= cap ? s - cap : s;
 }
 
-struct EnvView {
+// DT: element type of the destination rings -- int32 in HBM (dmdqn_sim.dst),
+// u16 in the LDS image (edge ids < 440: grids up to 10 x 10).
+template <typename DT>
+struct EnvViewT {
     const dmdqn_sim &S;
     int e, A, X, NL, cap;
     float *x, *v;
-    int32_t *dst, *head, *cnt, *req, *gfrom;
+    DT *dst;
+    int32_t *head, *cnt, *req, *gfrom;
     float *fx, *fv;
     int32_t *phase, *ts, *qptr, *stats;
     const int32_t *q_off;
     const uint16_t *q_ids, *vdst, *q_dst;
 
-    __device__ EnvView(const dmdqn_sim &s, int env) : S(s), e(env) {
+    __device__ EnvViewT(const dmdqn_sim &s, int env) : S(s), e(env) {
         A = s.R * s.C;
         X = 2 * s.R + 2 * s.C;
         NL = 3 * (4 * A + X);
@@ -51,7 +57,8 @@ struct EnvView {
         size_t ls = (size_t)env * NL;
         x = s.x + ls * cap;
         v = s.v + ls * cap;
-        dst = s.dst + ls * cap;
+        if constexpr (std::is_same<DT, int32_t>::value) dst = s.dst + ls * cap;
+        else dst = nullptr;  // the LDS image: set up by k_sim_step
         head = s.head + ls;
         cnt = s.cnt + ls;
         req = s.req + ls;
@@ -68,6 +75,7 @@ struct EnvView {
         stats = s.stats + (size_t)env * 4;
     }
 };
+using EnvView = EnvViewT<int32_t>;
 
 // ---------------------------------------------------------------- substep
 // Next vehicle of an origin queue: queue position p -> (id, destination).
@@ -76,7 +84,8 @@ struct QNext {
 };
 constexpr int QSLOTS = 2;  // queues per thread: 4A <= 2 * blockDim (grids up to 128 junctions)
 
-__device__ __forceinline__ QNext next_vehicle(const EnvView &V, int p) {
+template <typename View>
+__device__ __forceinline__ QNext next_vehicle(const View &V, int p) {
     return QNext{(int)V.q_ids[p], (int)V.q_dst[p]};
 }
 
@@ -93,7 +102,8 @@ __device__ __forceinline__ QNext next_vehicle(const EnvView &V, int p) {
 #define SIM_PROF(i) do { } while (0)
 #endif
 
-__device__ __forceinline__ void substep(EnvView &V, const Topo &T, const IdmK &P, int t,
+template <typename View>
+__device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, int t,
                                         QNext qn[QSLOTS], uint64_t *prof, uint64_t &prof_t) {
     const dmdqn_sim &S = V.S;
     const int A = V.A, NL = V.NL, cap = V.cap;
@@ -329,12 +339,13 @@ __device__ __forceinline__ void substep(EnvView &V, const Topo &T, const IdmK &P
     SIM_PROF(5);
 }
 
-// LDS image of one env's mutable state (kLDS path): x, v, dst rings
-// [NL][cap], then head, cnt, req, gfrom, fx, fv [NL], phase, ts [A], qptr [4A],
-// stats [4].  4x4 grid, cap 24: 75 KB -> two envs per CU.
+// LDS image of one env's mutable state (kLDS path): x, v (f32) and dst (u16)
+// rings [NL][cap], then head, cnt, req, gfrom, fx, fv [NL], phase, ts [A], qptr
+// [4A], stats [4].  4x4 grid, cap 24: 65 KB -> two envs per CU, 30 KB left (a
+// co-resident sampler wave fits, but measured no gain: it stretches the sim).
 __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
     const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
-    return (size_t)NL * cap * 12 + (size_t)NL * 6 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16 +
+    return (size_t)NL * cap * 10 + (size_t)NL * 6 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16 +
            (size_t)(4 * A + 1) * 4;  // q_off
 }
 
@@ -356,15 +367,15 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
     const Topo T = build_topo(reinterpret_cast<int32_t *>(dyn + topo_off), S.R, S.C, S.exit_id,
                               S.exit_ao, P.len_inner, P.len_outer);  // synced below
     EnvView G(S, blockIdx.x);
-    EnvView V(S, blockIdx.x);
+    EnvViewT<typename std::conditional<kLDS, uint16_t, int32_t>::type> V(S, blockIdx.x);
     const int A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
     if constexpr (kLDS) {
         const size_t NS = (size_t)NL * cap;
         V.x = reinterpret_cast<float *>(dyn);
         V.v = V.x + NS;
-        V.dst = reinterpret_cast<int32_t *>(V.v + NS);
-        V.head = V.dst + NS;
+        V.dst = reinterpret_cast<uint16_t *>(V.v + NS);
+        V.head = reinterpret_cast<int32_t *>(V.dst + NS);  // NS = NL * cap is even (NL = 6 * ...)
         V.cnt = V.head + NL;
         V.req = V.cnt + NL;
         V.gfrom = V.req + NL;
@@ -386,7 +397,7 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
             for (int i = 0, s = h; i < n; i++, s = (s + 1 == cap) ? 0 : s + 1) {
                 V.x[base + s] = G.x[base + s];
                 V.v[base + s] = G.v[base + s];
-                V.dst[base + s] = G.dst[base + s];
+                V.dst[base + s] = (uint16_t)G.dst[base + s];
             }
         }
         for (int a = tid; a < A; a += nt) {
