@@ -14,12 +14,12 @@ from dmdqn_amd.env import EnvConfig  # noqa: E402
 from dmdqn_amd.trainer import Trainer  # noqa: E402
 
 
-def _trainer(overlap, precision, shared, greedy):
+def _trainer(overlap, precision, shared, greedy, side_stream=None):
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=8, seed=11, max_sim_time=500),
                  AgentConfig(replay_buffer_size=200, target_update_frequency=9, seed=4,
                              precision=precision, shared_params=shared,
                              count_env_steps=greedy),
-                 overlap=overlap)
+                 overlap=overlap, side_stream=side_stream)
     if greedy:  # past the 8000-step epsilon floor (dqn_agent.py:258-261)
         tr.agent.global_step_count = 12000
     return tr
@@ -37,12 +37,33 @@ def _run(tr, n):
 
 @pytest.mark.parametrize("mode", ["sample", "full"])
 @pytest.mark.parametrize("precision,shared,greedy", [
-    ("fp16", False, False), ("fp32", False, False), ("fp16", True, False), ("fp16", False, True)])
+    ("fp16", False, False), ("fp32", False, False), ("bf16", False, False), ("fp16", True, False),
+    ("fp16", False, True)])
 def test_overlap_matches_sequential(mode, precision, shared, greedy):
     ref = _trainer("none", precision, shared, greedy)
     ovl = _trainer(mode, precision, shared, greedy)
     assert ovl.side is not None and ref.side is None
     a, b = _run(ref, 170), _run(ovl, 170)   # 3 episodes of 50 steps, learn from step 128
+    _compare(ref, ovl, a, b)
+
+
+def test_overlap_on_cu_masked_streams_matches_sequential():
+    """bench --cu-split: the learn on one CU-masked stream, the side work on
+    another (dmdqn_stream_create_cumask) -- still bit-identical."""
+    from dmdqn_amd._lib import cu_masked_stream
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    main = cu_masked_stream(range(32, n_cu))
+    side = cu_masked_stream(range(32))
+    ref = _trainer("none", "fp16", False, False)
+    a = _run(ref, 170)
+    with torch.cuda.stream(main):
+        ovl = _trainer("full", "fp16", False, False, side_stream=side)
+        assert ovl.side is side
+        b = _run(ovl, 170)
+    _compare(ref, ovl, a, b)
+
+
+def _compare(ref, ovl, a, b):
     assert sum(x[4] for x in a) == 3 and ref.episode == ovl.episode == 3
     for t, (x, y) in enumerate(zip(a, b)):
         assert (x[0] is None) == (y[0] is None), t

@@ -20,7 +20,7 @@ for t in range(130):
     r = -torch.rand((E, A), device="cuda", generator=g, dtype=torch.float64) * 100
     ag.remember(s, a, r, s, t % 60 == 59)
 torch.cuda.synchronize()
-names = ["meta+zscore", "gather S'", "fwd target (+online frag loads)",
+names = ["slots + gather S' + metadata + zscore", "-", "fwd target (+online frag loads)",
          "fwd online S' (+S gather)", "-", "argmax+y", "fwd online S", "loss+dW3+Adam W3",
          "dZ2", "dW2+Adam W2+image+dH1+gather S", "dZ1", "dW1+Adam W1"]
 ag.stamps = torch.zeros((NA, 16), dtype=torch.int64, device="cuda")
