@@ -150,7 +150,7 @@ __device__ __forceinline__ uint64_t lanes_below() {
 }
 
 __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32_t n, int k,
-                                               uint32_t setsize, int32_t *idx) {
+                                               uint32_t setsize, int first_table, int32_t *idx) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *mt = smem, *tmp = smem + MT_N, *aux = smem + 2 * MT_N;
     MTWave w{mt, tmp, 0};
@@ -216,7 +216,13 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
     } else {
         uint32_t *bm = aux;  // selected bitmap, n bits
         const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
+        // first[r]: the lowest lane of the current chunk that drew r (all ones
+        // between chunks) -- the in-chunk repeat test in 3 LDS operations
+        // instead of 63 dependent lane shuffles (used when n words fit in LDS)
+        uint32_t *first = bm + words;
         for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
+        if (first_table)
+            for (uint32_t t = l; t < n; t += 64) first[t] = 0xffffffffu;
         __syncthreads();
         int j = 0, i = 0;
         while (j < A) {
@@ -227,11 +233,19 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
             bool cand = live && r < n;
             if (cand) cand = !((bm[r >> 5] >> (r & 31)) & 1u);
             // a repeat of an earlier candidate lane in the same chunk is rejected
-            const uint32_t key = cand ? r : (0x80000000u | (uint32_t)l);
             bool dup = false;
-            for (int d = 1; d < cnt; d++) {
-                const uint32_t o = __shfl(key, (l - d) & 63);
-                dup |= (l >= d) && (o == key);
+            if (first_table) {
+                // one wave: its LDS operations complete in issue order, so the
+                // read sees every lane's min and the reset follows the read
+                if (cand) atomicMin(&first[r], (uint32_t)l);
+                if (cand) dup = first[r] != (uint32_t)l;
+                if (cand) first[r] = 0xffffffffu;
+            } else {
+                const uint32_t key = cand ? r : (0x80000000u | (uint32_t)l);
+                for (int d = 1; d < cnt; d++) {
+                    const uint32_t o = __shfl(key, (l - d) & 63);
+                    dup |= (l >= d) && (o == key);
+                }
             }
             const bool a = cand && !dup;
             const uint64_t acc = __ballot(a);
@@ -312,8 +326,11 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
                             : (size_t)((n + 31) / 32) * 4;
     size_t lds = 2 * MT_N * sizeof(uint32_t) + aux_bytes;
     DMDQN_REQUIRE(lds <= 160 * 1024, "dmdqn_replay_sample: n=%d too large for LDS", n);
+    // set branch: the first-lane table (4n bytes) when it fits in 64 KB of LDS
+    const int first_table = !pool && lds + (size_t)n * 4 <= 64 * 1024;
+    if (first_table) lds += (size_t)n * 4;
     hipLaunchKernelGGL(k_sample, dim3(E), dim3(64), lds, as_stream(stream), py_state, A,
-                       (uint32_t)n, k, setsize, idx);
+                       (uint32_t)n, k, setsize, first_table, idx);
     DMDQN_LAUNCH_CHECK("k_sample");
     return DMDQN_OK;
 }

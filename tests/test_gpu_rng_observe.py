@@ -68,7 +68,8 @@ def test_replay_sample_matches_cpython(n):
 
 
 @pytest.mark.parametrize("A,n,k", [(64, 200, 128), (70, 300, 32), (3, 21, 5), (3, 22, 5),
-                                   (5, 7, 7), (2, 3000, 1000), (64, 10000, 128), (1, 128, 128)])
+                                   (5, 7, 7), (2, 3000, 1000), (64, 10000, 128), (1, 128, 128),
+                                   (4, 20000, 128)])
 def test_replay_sample_shapes(A, n, k):
     """Agent groups beyond one wave (A > 64), small k (setsize 21), k = n and
     large k: every branch and chunk-boundary case of the chunked sampler."""
