@@ -148,6 +148,10 @@ def main():
     ap.add_argument("--shared", action="store_true",
                     help="C5: one shared network (mean per-agent loss, RCCL gradient "
                          "all-reduce across ranks); use with --rows 8 --cols 8")
+    ap.add_argument("--prefill-steps", type=int, default=None,
+                    help="untimed loop steps before warm-up (default batch_size-1: the learn "
+                         "starts at the first warm-up step; >= 1045 puts the replay sampler in "
+                         "its steady-state set branch, as in long training runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=60,
                     help="timed RL steps per replica of the CPU baseline")
@@ -200,7 +204,8 @@ def main():
     tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side)
     E, A = tr.env.E, tr.env.A
     NA = E * A
-    for _ in range(agent_cfg.batch_size - 1):  # replay fill (no learn yet)
+    prefill = agent_cfg.batch_size - 1 if args.prefill_steps is None else args.prefill_steps
+    for _ in range(prefill):  # replay fill (the learn joins once a ring holds batch_size)
         tr.step()
     for _ in range(args.warmup):
         tr.step()
@@ -298,7 +303,10 @@ def main():
                             "envs/GPU, full RL step (act, 10 IDM substeps, observe, remember, "
                             f"sample, {learn_desc}), H=128, batch 128, replay 10000",
                 "envs_per_gpu": args.envs, "agents_per_env": A, "global_envs": args.envs * world,
-                "replay_prefill_steps": agent_cfg.batch_size - 1,
+                "replay_prefill_steps": prefill,
+                "replay_len_timed": [min(prefill + args.warmup + 1, agent_cfg.replay_buffer_size),
+                                     min(prefill + args.warmup + args.steps,
+                                         agent_cfg.replay_buffer_size)],
                 "parallelism": (f"env-shard x{world}" + (" + RCCL all-reduce of the 114 KB "
                                 "gradient" if args.shared and world > 1 else " (no collectives)")),
                 "precision": args.precision,
