@@ -79,6 +79,17 @@ __device__ __forceinline__ f32x4 mfma(half8 a, half8 b, f32x4 c) {
     return H16_MFMA(a, b, c, 0, 0, 0);
 }
 
+// threadIdx.x behind an empty asm: the per-thread addresses derived from it
+// are recomputed at each use instead of being common-subexpressioned across
+// the whole kernel (the three gathers share their slot-read and LDS-store
+// addresses; kept live from the first to the last they spilled to scratch --
+// 18 KB of scratch writes per workgroup reaching HBM, and vmcnt(0) reloads).
+__device__ __forceinline__ int fresh_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // img[r0 + (l&15)][k0 + 8(l>>4) + e], e = 0..7: one 16-byte LDS read.
 __device__ __forceinline__ half8 frag_row(const h16 *img, int ld, int r0, int k0) {
     const int l = threadIdx.x & 63;
@@ -553,16 +564,6 @@ __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, si
 
 struct Rows { uint2 v[3]; };
 
-// threadIdx.x behind an empty asm: the per-thread addresses derived from it
-// are recomputed at each use instead of being common-subexpressioned across
-// the whole kernel (the three gathers share their slot-read and LDS-store
-// addresses; kept live from the first to the last they spilled to scratch --
-// 18 KB of scratch writes per workgroup reaching HBM, and vmcnt(0) reloads).
-__device__ __forceinline__ int fresh_tid() {
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t;
-}
 
 // Replay rows (int8, DMDQN_ROW_BYTES = one 128-B line each) of one agent's
 // batch -> X f16 [128][96] in R2, in two halves so the loads can be in flight
@@ -1010,6 +1011,7 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
     STAMP(11);
     // ---- dW1[i][j] = X^T . dZ1 (wave w: j-tile w, 6 i-tiles) ; db1 (j-tile w)
     {
+        const int tx = fresh_tid(), lr = tx & 15, lg = (tx & 63) >> 4;
         f32x4 g1[6], gb = {0.f, 0.f, 0.f, 0.f};
         // rows i = 16t + 4lg + e, column j = 16w + lr -> W1T[j][i..i+3]; tile 5
         // holds features 80..95: lanes lg < 2 (80..87) update in the pipe, lane
