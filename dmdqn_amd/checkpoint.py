@@ -7,8 +7,8 @@ This module keeps that naming for the exported weights and adds what a resume
 needs, so that load + K steps reproduces an uninterrupted run bit-exactly
 (every kernel on the path is deterministic):
 
-  nets      params / target (+ its f16 shadow) / Adam m, v, learn counters;
-            the online net's f16 copy is rebuilt from params on load
+  nets      params / target (+ its f16 / bf16 shadow) / Adam m, v, learn counters;
+            the shared net's 16-bit online copy is rebuilt from params on load
   replay    the filled part of every ring + the host counter
   streams   both device MT19937 streams per env (numpy act stream, CPython
             sample stream)

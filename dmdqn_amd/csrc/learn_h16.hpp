@@ -820,15 +820,15 @@ __device__ __forceinline__ void bwd_dz1(h16 *R1, const uint32_t *mask, const f32
     }
 }
 
-#define LEARN_SMEM_SETUP                                                                        \
+#define LEARN_SMEM_SETUP                                                                       \
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];                              \
-    h16 *R1 = (h16 *)(smem + R1_OFF), *R2 = (h16 *)(smem + R2_OFF);             \
-    h16 *DQ = (h16 *)(smem + DQ_OFF);                                                \
+    h16 *R1 = (h16 *)(smem + R1_OFF), *R2 = (h16 *)(smem + R2_OFF);                            \
+    h16 *DQ = (h16 *)(smem + DQ_OFF);                                                          \
     char *sc = smem + SC_OFF;                                                                  \
     Scratch S{(float *)sc,          (float *)(sc + 2048), (float *)(sc + 2560),                \
               (float *)(sc + 3072), (float *)(sc + 3584), (int *)(sc + 4096),                  \
               (int *)(sc + 4608),   (double *)(sc + 5120), (double *)(sc + 6144)};             \
-    h16 *W3L = (h16 *)(smem + W3_OFF);                                               \
+    h16 *W3L = (h16 *)(smem + W3_OFF);                                                         \
     float *B3L = (float *)(smem + B3_OFF);                                                     \
     const OutL on{W3L, B3L}, tg{W3L + NACT * H, B3L + NACT};                                   \
     uint32_t *mask = reinterpret_cast<uint32_t *>(DQ)
