@@ -44,12 +44,19 @@ def _headers():
 def _compile(src, force):
     name = os.path.basename(src)
     obj = os.path.join(OBJDIR, name + ".o")
-    if EXTRA:
-        force = True
-    newest = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
-    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest:
-        return obj, False
     flags = COMMON + PER_FILE.get(name, DEFAULT_FP) + EXTRA
+    # the flags an object was built with sit beside it: a changed flag set
+    # (e.g. an experiment's -D switches, then none) forces a rebuild
+    stamp = obj + ".flags"
+    try:
+        with open(stamp) as f:
+            same_flags = f.read() == " ".join(flags)
+    except OSError:
+        same_flags = False
+    newest = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
+    if (not force and same_flags and os.path.exists(obj)
+            and os.path.getmtime(obj) >= newest):
+        return obj, False
     lang = ["-x", "hip"] if name.endswith(".hip") else []
     cmd = [HIPCC] + flags + lang + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -57,6 +64,8 @@ def _compile(src, force):
         raise RuntimeError(f"hipcc failed for {name}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     if r.stderr.strip():
         sys.stderr.write(r.stderr)
+    with open(stamp, "w") as f:
+        f.write(" ".join(flags))
     return obj, True
 
 
