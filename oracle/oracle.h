@@ -61,7 +61,7 @@ void orc_qnet_forward(const float *p, int H1, int H2, int NA, const float *x, in
                       float *z1c, float *z2c);
 float orc_learn(float *p, const float *target, float *m, float *v, int H1, int H2, int NA,
                 int B, const float *S, const int32_t *A, const float *Rn, const float *S2,
-                const float *Dn, const float *hyper, float *grad_out);
+                const float *Dn, const float *hyper, float *grad_out, int loss_kind);
 
 /* ---- the whole training loop, OpenMP over replicas (oracle_loop.c; bench CPU baseline) ---- */
 double orc_train_loop(int R, int C, int E, int fill, int steps, uint64_t seed, int threads,

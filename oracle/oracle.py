@@ -251,7 +251,7 @@ def _declare_learn(L):
                                    C.c_void_p, C.c_void_p]
     L.orc_learn.restype = C.c_float
     L.orc_learn.argtypes = [_f32, _f32, _f32, _f32, C.c_int, C.c_int, C.c_int, C.c_int, _f32, _i32,
-                            _f32, _f32, _f32, _f32, C.c_void_p]
+                            _f32, _f32, _f32, _f32, C.c_void_p, C.c_int]
 
 
 def _L():
@@ -284,8 +284,9 @@ def keras_adam_consts(t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
 
 
 def learn(p, target, m, v, S, A, Rn, S2, Dn, t, gamma=0.99, lr=1e-3, H1=128, H2=128, NA=4,
-          want_grad=False):
-    """In-place Keras-semantics learn step on float32 numpy arrays; returns loss (and grad)."""
+          want_grad=False, loss_kind=0):
+    """In-place Keras-semantics learn step on float32 numpy arrays; returns loss (and grad).
+    loss_kind 0 = MSE (dqn_agent.py:352), 1 = Huber delta 1 (experimental/agent.py:99)."""
     alpha, c1, c2, eps = keras_adam_consts(t, lr)
     hyper = np.array([np.float32(gamma), alpha, c1, c2, eps], np.float32)
     grad = np.zeros(p.size, np.float32) if want_grad else None
@@ -294,7 +295,7 @@ def learn(p, target, m, v, S, A, Rn, S2, Dn, t, gamma=0.99, lr=1e-3, H1=128, H2=
                           np.ascontiguousarray(S, np.float32), np.ascontiguousarray(A, np.int32),
                           np.ascontiguousarray(Rn, np.float32), np.ascontiguousarray(S2, np.float32),
                           np.ascontiguousarray(Dn, np.float32), hyper,
-                          None if grad is None else grad.ctypes.data)
+                          None if grad is None else grad.ctypes.data, int(loss_kind))
     return (loss, grad) if want_grad else loss
 
 

@@ -9,14 +9,20 @@
  *   :343-345   q_t = target(S')[a*]
  *   :347       y = r + gamma * (1 - d) * q_t
  *   :350-352   q = sum(online(S) * one_hot(A)); loss = mean((y - q)^2)
+ *              loss_kind 1: Keras Huber (delta 1; the loss of
+ *              src/experimental/agent.py:99): e = q - y,
+ *              mean(|e| <= 1 ? 0.5 e^2 : |e| - 0.5), dL/dq = clip(e, -1, 1) / B
  *   :356-357   gradients; keras.optimizers.Adam.update_step:
  *              m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);
  *              w -= (m * alpha) / (sqrt(v) + eps),
  *              alpha = lr * sqrt(1 - b2^t) / (1 - b1^t)
  * fp32 throughout (the reference computes under mixed_float16; the fp32
  * restatement is the stricter oracle, tolerances are stated in the tests).
- * Parity vs real TF/Keras is UNPINNED (TF is absent); this restatement is
- * cross-checked against torch autograd in tests/test_learn_oracle_cpu.py.
+ * TF/Keras are absent.  The restatement is pinned by tests/golden/learn.npz:
+ * the reference's own DQNAgent.learn control flow run over a torch-backed TF
+ * shim (tests/golden/make_learn_golden.py, tf_shim.py), 633 MSE and 233 Huber
+ * learns (tests/test_learn_golden_cpu.py); and cross-checked against torch
+ * autograd in tests/test_learn_oracle_cpu.py.
  *
  * Parameter vector (Keras get_weights order): W1[89][H1] b1[H1] W2[H1][H2]
  * b2[H2] W3[H2][NA] b3[NA].
@@ -76,7 +82,7 @@ static int argmax_first(const float *q, int n) {
  * hyper: [gamma, alpha_t, c1=(1-b1), c2=(1-b2), eps]; grad_out (optional) [P] */
 float orc_learn(float *p, const float *target, float *m, float *v, int H1, int H2, int NA,
                 int B, const float *S, const int32_t *A, const float *Rn, const float *S2,
-                const float *Dn, const float *hyper, float *grad_out) {
+                const float *Dn, const float *hyper, float *grad_out, int loss_kind) {
     const float gamma = hyper[0], alpha = hyper[1], c1 = hyper[2], c2 = hyper[3], eps = hyper[4];
     long P = orc_qnet_nparams(H1, H2, NA);
     float *q2 = (float *)malloc(sizeof(float) * B * NA), *qt = (float *)malloc(sizeof(float) * B * NA);
@@ -100,8 +106,15 @@ float orc_learn(float *p, const float *target, float *m, float *v, int H1, int H
     for (int b = 0; b < B; b++) {
         float pred = q[b * NA + A[b]];
         float diff = pred - y[b];
-        loss += diff * diff;
-        float dq = 2.0f * diff / (float)B;
+        float dq;
+        if (loss_kind == 1) {
+            float ae = fabsf(diff);
+            loss += ae <= 1.0f ? 0.5f * diff * diff : ae - 0.5f;
+            dq = (ae <= 1.0f ? diff : (diff > 0.0f ? 1.0f : -1.0f)) / (float)B;
+        } else {
+            loss += diff * diff;
+            dq = 2.0f * diff / (float)B;
+        }
         const float *z1b = z1 + (size_t)b * H1, *z2b = z2 + (size_t)b * H2;
         for (int k = 0; k < H2; k++) {
             float h2 = z2b[k] > 0.0f ? z2b[k] : 0.0f;

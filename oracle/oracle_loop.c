@@ -141,7 +141,7 @@ static void loop_step(loop_env *e, int learn) {
             orc_zscore(e->rb, BATCH, e->Rn);
             size_t o = (size_t)a * e->P;
             orc_learn(e->params + o, e->target + o, e->m + o, e->v + o, 128, 128, 4, BATCH, e->Sb,
-                      e->Ab, e->Rn, e->S2b, e->Db, hyper, NULL);
+                      e->Ab, e->Rn, e->S2b, e->Db, hyper, NULL, 0);
         }
         if (e->learn_steps % 500 == 0)
             memcpy(e->target, e->params, (size_t)A * e->P * sizeof(float));
