@@ -37,7 +37,8 @@ class CLearn(C.Structure):
                                   "params", "adam_m", "adam_v", "target", "target_h",
                                   "loss"]] + [
         (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]] + [
-        ("stamps", C.c_void_p), ("qstats", C.c_void_p), ("params_h", C.c_void_p)]
+        ("stamps", C.c_void_p), ("qstats", C.c_void_p), ("params_h", C.c_void_p),
+        ("loss_kind", C.c_int32), ("rn_out", C.c_void_p)]
 
 
 _lib.register({
@@ -54,6 +55,9 @@ _lib.register({
 })
 
 PRECISIONS = {"fp32": 0, "fp16": 1, "bf16": 2}
+# include/dmdqn.h DMDQN_LOSS_*: the reference's MSE (dqn_agent.py:352) and the
+# Huber loss of src/experimental/agent.py:99 (delta 1)
+LOSSES = {"mse": 0, "huber": 1}
 # dtype of the 16-bit operand copies (target shadow, shared online copy)
 H16_DTYPES = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
@@ -200,6 +204,7 @@ class AgentConfig:
     nn_layers: List[int] = field(default_factory=lambda: [128, 128])
     # build-only knobs (additive)
     precision: str = "fp32"          # "fp32" | "fp16" (mixed, the reference's policy) | "bf16"
+    loss: str = "mse"                # "mse" (dqn_agent.py:352) | "huber" (experimental/agent.py:99)
     count_env_steps: bool = False    # True fixes A-1 (epsilon decays); False = reference
     seed: int = 0
     # C5 (not in the reference): ONE network shared by every agent,
@@ -227,6 +232,8 @@ class BatchedDQN:
             raise ValueError("the fused learn kernel is built for batch_size 128")
         if cfg.precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {list(PRECISIONS)}")
+        if cfg.loss not in LOSSES:
+            raise ValueError(f"loss must be one of {list(LOSSES)}")
         if cfg.shared_params and (cfg.precision != "fp16" or H != 128):
             raise ValueError("shared_params needs precision 'fp16' and nn_layers [128, 128]")
         self.device = dev = torch.device(device)
@@ -297,6 +304,7 @@ class BatchedDQN:
         self.learn_launches = 0
         self.learn_hook = None  # optional callable(before: bool), e.g. HIP event timing
         self.stamps = None      # optional int64 [NA, 16] device tensor: phase timestamps
+        self.rn_out = None      # optional f32 [NA, batch] device tensor: the z-scored rewards
 
     # -------------------------------------------------------------- act
     def current_epsilon(self):
@@ -334,6 +342,7 @@ class BatchedDQN:
             d = done.to(torch.uint8).reshape(self.E, 1).expand(self.E, self.A).reshape(NA).contiguous()
         self.ring.store(obs.reshape(NA, D_IN), next_obs.reshape(NA, D_IN),
                         actions.reshape(NA), rewards.reshape(NA), d)
+        self.ring.poll()  # raises (one store late, no stall) on a non-int8 observation
         if self.cfg.count_env_steps:
             self.global_step_count += 1
 
@@ -370,7 +379,8 @@ class BatchedDQN:
                    np.float32(cfg.gamma), alpha, c1, c2, eps,
                    None if self.stamps is None else self.stamps.data_ptr(),
                    self.qstats.zero_().data_ptr() if collect_stats else None,
-                   None if self.params_h is None else self.params_h.data_ptr())
+                   None if self.params_h is None else self.params_h.data_ptr(),
+                   LOSSES[cfg.loss], None if self.rn_out is None else self.rn_out.data_ptr())
         self._last_args = a  # keeps the struct (and what it points at) inspectable
         if self.learn_hook:
             self.learn_hook(True)

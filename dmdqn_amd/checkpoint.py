@@ -33,6 +33,26 @@ _ENV_TENSORS = ["t_x", "t_v", "t_dst", "t_head", "t_cnt", "t_phase_state", "t_ts
 _AGENT_TENSORS = ["params", "target", "adam_m", "adam_v", "np_state", "py_state"]
 
 
+# Config fields that fix the state layout or its meaning: a resume under a
+# different value would restore tensors that mean something else (or leave
+# derived state stale), so load() refuses it.
+_AGENT_FIXED = ["precision", "shared_params", "nn_layers", "replay_buffer_size", "batch_size",
+                "seed", "loss", "target_update_frequency", "count_env_steps"]
+_ENV_FIXED = ["rows", "cols", "num_envs", "env_offset", "seed", "signal_features", "cap_lane",
+              "end_ms", "period_ms", "step_duration", "max_sim_time", "action_stride", "scenario"]
+_DEFAULTS = {"loss": "mse"}  # fields added after format 4 was introduced
+
+
+def _check_cfg(saved, cur, fields, what):
+    for k in fields:
+        a, b = saved.get(k, _DEFAULTS.get(k)), cur.get(k, _DEFAULTS.get(k))
+        if k == "scenario" and a and b:
+            a, b = os.path.basename(str(a)), os.path.basename(str(b))
+        if a != b:
+            raise ValueError(f"checkpoint {what}.{k} = {a!r} but this Trainer has {b!r}: "
+                             "build the Trainer with the checkpoint's configuration")
+
+
 def _cfg_dict(cfg):
     d = dataclasses.asdict(cfg)
     return {k: (v if isinstance(v, (int, float, str, bool, type(None), list)) else str(v))
@@ -65,6 +85,7 @@ def trainer_state(tr, include_replay=True):
 
 def save(path, tr, include_replay=True):
     torch.cuda.synchronize(tr.env.device)
+    tr.agent.ring.check()  # never persist a replay that holds a refused value
     torch.save(trainer_state(tr, include_replay), path)
 
 
@@ -74,30 +95,42 @@ def load(path, tr):
     if st.get("format") != FORMAT:
         raise ValueError(f"{path}: not a {FORMAT} checkpoint")
     ag, env = tr.agent, tr.env
+    _check_cfg(st["agent_cfg"], _cfg_dict(ag.cfg), _AGENT_FIXED, "agent_cfg")
+    _check_cfg(st["env_cfg"], _cfg_dict(env.cfg), _ENV_FIXED, "env_cfg")
     if int(st["nveh"]) != int(env.nveh):
         raise ValueError("checkpoint demand does not match this env config (nveh differs)")
+    if int(st["counters"]["ring_total"]) > 0 and "replay" not in st:
+        raise ValueError("checkpoint was saved without its replay (include_replay=False) but its "
+                         "rings hold transitions: a resume would train on empty rings")
+
+    def put(group, obj, k, v):
+        dst = getattr(obj, k)
+        if dst is None:
+            raise ValueError(f"checkpoint {group}.{k} has no counterpart in this Trainer")
+        if tuple(dst.shape) != tuple(v.shape) or dst.dtype != v.dtype:
+            raise ValueError(f"checkpoint {group}.{k} {v.dtype}{tuple(v.shape)} != "
+                             f"{dst.dtype}{tuple(dst.shape)}")
+        dst.copy_(v.to(obj.device))
+
     for k, v in st["agent"].items():
-        dst = getattr(ag, k)
-        if tuple(dst.shape) != tuple(v.shape):
-            raise ValueError(f"checkpoint agent.{k} shape {tuple(v.shape)} != {tuple(dst.shape)}")
-        dst.copy_(v.to(ag.device))
+        put("agent", ag, k, v)
     for k, v in st["env"].items():
         if k == "local":
             env.local = v.to(env.device)
             continue
-        dst = getattr(env, k)
-        if tuple(dst.shape) != tuple(v.shape):
-            raise ValueError(f"checkpoint env.{k} shape {tuple(v.shape)} != {tuple(dst.shape)}")
-        dst.copy_(v.to(env.device))
+        put("env", env, k, v)
     c = st["counters"]
     ag.learn_step_counter, ag.global_step_count = c["learn_step_counter"], c["global_step_count"]
     ag.epsilon, ag.learn_launches = c["epsilon"], c["learn_launches"]
     env.t, env.episode = c["env_t"], c["env_episode"]
     tr.episode, tr.step_count, tr.total_steps = c["episode"], c["step_count"], c["total_steps"]
     ag.ring.total = c["ring_total"]
-    ag._refresh_params_h()  # the f16 online copy is derived, not stored
+    ag._refresh_params_h()  # the 16-bit copies are derived from the f32 nets
+    ag._refresh_target_h()
     if "replay" in st:
         n = st["replay"]["s"].shape[1]
+        if n != len(ag.ring):
+            raise ValueError(f"checkpoint replay holds {n} slots, its counter says {len(ag.ring)}")
         for k, v in st["replay"].items():
             getattr(ag.ring, k)[:, :n].copy_(v.to(ag.device))
     tr.obs = st["obs"].to(env.device)

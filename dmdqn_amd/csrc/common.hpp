@@ -163,4 +163,22 @@ __device__ inline void learn_qstats(float *qstats, int agent, const float *z3, c
     }
 }
 
+// Per-row loss term and dL/dq for a batch of B rows, diff = q - y:
+//   DMDQN_LOSS_MSE    (dqn_agent.py:352, MeanSquaredError): diff^2, 2 diff / B
+//   DMDQN_LOSS_HUBER  (src/experimental/agent.py:99, keras Huber, delta 1):
+//                     |d| <= 1 ? d^2 / 2 : |d| - 1/2,  clip(d, -1, 1) / B
+// The loss is the mean of the terms.  kind is uniform over the block, so the
+// select costs two VALU ops per row.
+__device__ __forceinline__ void loss_term(int kind, float diff, float inv_b, float &term,
+                                          float &dq) {
+    if (kind == DMDQN_LOSS_HUBER) {
+        const float ae = fabsf(diff);
+        term = ae <= 1.0f ? 0.5f * diff * diff : ae - 0.5f;
+        dq = (ae <= 1.0f ? diff : copysignf(1.0f, diff)) * inv_b;
+    } else {
+        term = diff * diff;
+        dq = 2.0f * diff * inv_b;
+    }
+}
+
 }  // namespace dmdqn

@@ -208,6 +208,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     if (tid < B_) {
         double z = __ddiv_rn(__dsub_rn(S.r64[tid], S.red[8]), S.red[9]);
         S.rn[tid] = (float)z;
+        if (a.rn_out) a.rn_out[(size_t)agent * B_ + tid] = (float)z;
     }
 
     // ---- P1: gather S' rows
@@ -246,9 +247,9 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];
-        float diff = q - S.y[tid];
-        S.dq[tid] = 2.0f * diff / (float)B_;
-        lsum = diff * diff;
+        float dq;
+        loss_term(a.loss_kind, q - S.y[tid], 1.0f / (float)B_, lsum, dq);
+        S.dq[tid] = dq;
     }
     // loss: wave reductions then one lane
     if (w < 2) {
@@ -447,6 +448,8 @@ extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
                   "dmdqn_learn: null pointer");
     DMDQN_REQUIRE(a->precision >= 0 && a->precision <= 2, "dmdqn_learn: precision %d",
                   a->precision);
+    DMDQN_REQUIRE(a->loss_kind == DMDQN_LOSS_MSE || a->loss_kind == DMDQN_LOSS_HUBER,
+                  "dmdqn_learn: loss_kind %d", a->loss_kind);
     if (a->precision == 1) return launch_learn_f16(a, as_stream(stream));
     if (a->precision == 2) return launch_learn_bf16(a, as_stream(stream));
     if (a->hidden == 128) {

@@ -183,6 +183,8 @@ extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, i
                       a->params && a->target && a->params_h,
                   "dmdqn_learn_shared_grad: null array");
     DMDQN_REQUIRE(n_slabs >= 1, "dmdqn_learn_shared_grad: n_slabs must be >= 1");
+    DMDQN_REQUIRE(a->loss_kind == DMDQN_LOSS_MSE || a->loss_kind == DMDQN_LOSS_HUBER,
+                  "dmdqn_learn_shared_grad: loss_kind %d", a->loss_kind);
     hipStream_t s = as_stream(stream);
     if (a->qstats)
         hipLaunchKernelGGL(f16k::k_learn_shared_f16<true>, dim3(n_slabs), dim3(512), 0, s, *a, slab);

@@ -680,6 +680,7 @@ __device__ __forceinline__ void batch_head(const dmdqn_learn_args &a, int agent,
     gather_commit(R2, gn);
     meta_commit(mt, S);
     zscore(S);
+    if (a.rn_out && threadIdx.x < B_) a.rn_out[(size_t)agent * B_ + threadIdx.x] = S.rn[threadIdx.x];
 }
 
 // Double-DQN target y = r^ + gamma (1 - d) Q_target(S')[argmax Q_online(S')]
@@ -702,8 +703,8 @@ __device__ __forceinline__ void ddqn_target(const dmdqn_learn_args &a, const flo
     __syncthreads();
 }
 
-// MSE loss (dqn_agent.py:350-352) of Q_online(S) in S.z3 at the taken actions,
-// written to a.loss[agent]; dL/dQ (2 (q - y) / B, f16) into DQ [128][16] and
+// MSE (dqn_agent.py:350-352) or Huber loss (loss_term) of Q_online(S) in S.z3 at
+// the taken actions, written to a.loss[agent]; dL/dQ (f16) into DQ [128][16] and
 // S.dq.  Ends with a barrier.
 template <bool QSTATS>
 __device__ __forceinline__ void loss_dq(const dmdqn_learn_args &a, int agent, h16 *DQ,
@@ -713,9 +714,8 @@ __device__ __forceinline__ void loss_dq(const dmdqn_learn_args &a, int agent, h1
     float lsum = 0.0f;
     if (tid < B_) {
         float q = S.z3[tid * NACT + S.act[tid]];
-        float diff = q - S.y[tid];
-        float dq = 2.0f * diff / (float)B_;
-        lsum = diff * diff;
+        float dq;
+        loss_term(a.loss_kind, q - S.y[tid], 1.0f / (float)B_, lsum, dq);
         half8 z;
 #pragma unroll
         for (int e = 0; e < 8; e++) z[e] = (h16)0.0f;

@@ -123,6 +123,13 @@ class TrafficEnv:
             q_ids, q_off, vdst, nveh, period = demand_tables(g, self.seeds, cfg.end_ms,
                                                              cfg.period_ms)
         self.nveh, self.period_ms = nveh, period
+        # train.py:233-236 ends an episode when t >= MAX_SIM_TIME or no vehicle is
+        # running or pending (getMinExpectedNumber() == 0).  While departures are
+        # still scheduled at or after max_sim_time (the shipped demand: 2499.6 s
+        # > 2400 s) the second condition cannot fire, and the host clock decides
+        # without a device read; otherwise step() reads the kernel's per-replica
+        # flags (one sync per step).
+        self.drains_early = (nveh - 1) * period < cfg.max_sim_time * 1000
         dev = self.device
         z32 = lambda *s: torch.zeros(s, dtype=torch.int32, device=dev)  # noqa: E731
         self.t_x = torch.zeros((E, NL, cap), dtype=torch.float32, device=dev)
@@ -192,10 +199,19 @@ class TrafficEnv:
         prev = self.local
         self.local, self.obs, reward = K.observe(self.R, self.C, self.halt, self.phase,
                                                  self.tspent, self.mode, prev_local=prev)
-        # every replica shares the clock and the demand horizon, so `done` is
-        # uniform across replicas; the host knows it without a device sync
-        done = self.t >= cfg.max_sim_time
-        info = {"simulation_time": float(self.t), "done_flags": self.done_u8}
+        if self.drains_early:
+            # the reference rule per replica (done_u8, from the last substep);
+            # the transition of replica e carries its own flag, and the episode
+            # (one shared clock) ends once every replica is done -- for E = 1,
+            # train.py's `while not done` exactly
+            flags = self.done_u8.cpu()
+            done_out = self.done_u8.clone()
+            done = bool(flags.all())
+        else:
+            # shared clock and demand horizon: `done` is uniform and known on
+            # the host without a device sync
+            done = done_out = self.t >= cfg.max_sim_time
+        info = {"simulation_time": float(self.t), "done_flags": self.done_u8, "done": done_out}
         return self.obs, reward, done, info
 
     def stats(self):

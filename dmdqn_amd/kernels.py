@@ -95,6 +95,8 @@ class ReplayRing:
         self.d = torch.zeros((NA, cap), dtype=torch.uint8, **z)
         self.err = torch.zeros(1, dtype=torch.int32, **z)
         self.total = 0
+        self._err_host = None  # pinned copy of err in flight (poll)
+        self._err_event = None
 
     def __len__(self):
         return min(self.total, self.cap)
@@ -119,7 +121,28 @@ class ReplayRing:
     def check(self):
         """Raise if a stored value was not exactly representable (syncs)."""
         if int(self.err.item()) != 0:
-            raise _lib.DmdqnError("replay_store: observation value not representable in int8")
+            raise _lib.DmdqnError(_RANGE_MSG)
+
+    def poll(self):
+        """Deferred check without stalling the stream: raise if the flag copied
+        at the previous poll was set, then start an asynchronous copy of the
+        current flag into pinned host memory.  A bad store therefore raises at
+        the next poll (the product path polls after every store, so one step
+        later) -- the reference stores float32 rows (dqn_agent.py:39-56), and
+        this build's int8 rows must never silently hold a rounded value."""
+        if self._err_event is not None:
+            self._err_event.synchronize()  # recorded a step ago: long complete
+            if int(self._err_host[0]) != 0:
+                raise _lib.DmdqnError(_RANGE_MSG)
+        else:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_event = torch.cuda.Event()
+        self._err_host.copy_(self.err, non_blocking=True)
+        self._err_event.record()
+
+
+_RANGE_MSG = ("replay_store: an observation value is not an integer in [-128, 127]; the int8 "
+              "replay rows store this env's features exactly and refuse anything else")
 
 
 def replay_sample(py_state, A, n, k=128, out=None):

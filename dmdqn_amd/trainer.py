@@ -85,12 +85,13 @@ class Trainer:
         env, agent = self.env, self.agent
         actions = agent.act(self.obs)                          # train.py:211-222
         next_obs, reward, done, info = env.step(actions)       # train.py:225-270
-        agent.remember(self.obs, actions, reward, next_obs, done)  # train.py:274-282
+        agent.remember(self.obs, actions, reward, next_obs, info["done"])  # train.py:274-282
         loss = agent.learn(collect_stats=collect_stats)
         self.last_loss, self.last_reward = loss, reward
         self.step_count += 1
         self.total_steps += 1
         if done:                                               # train.py:188-190
+            agent.ring.check()  # episode boundary: every store so far was exact
             self.episode += 1
             self.step_count = 0
             self.obs = env.reset()
@@ -113,7 +114,7 @@ class Trainer:
                 ev_s.record(side)
         actions = agent.act(self.obs)                          # train.py:211-222
         next_obs, reward, done, info = env.step(actions)       # train.py:225-270
-        agent.remember(self.obs, actions, reward, next_obs, done)  # train.py:274-282
+        agent.remember(self.obs, actions, reward, next_obs, info["done"])  # train.py:274-282
         if ev_s is not None:
             main.wait_event(ev_s)
         loss = agent.learn(collect_stats=collect_stats)
@@ -123,6 +124,7 @@ class Trainer:
         self.step_count += 1
         self.total_steps += 1
         if done:                                               # train.py:188-190
+            agent.ring.check()  # episode boundary: every store so far was exact
             self.episode += 1
             self.step_count = 0
             self.obs = env.reset()
@@ -149,7 +151,7 @@ class Trainer:
         main.wait_event(ev_obs)
         for t in (self.obs, next_obs, reward, env.local):
             t.record_stream(main)  # side-allocated, read on main
-        agent.remember(self.obs, actions, reward, next_obs, done)  # train.py:274-282
+        agent.remember(self.obs, actions, reward, next_obs, info["done"])  # train.py:274-282
         self._ev_store = torch.cuda.Event()
         self._ev_store.record(main)
         loss = agent.learn(collect_stats=collect_stats)
@@ -159,6 +161,7 @@ class Trainer:
         self.step_count += 1
         self.total_steps += 1
         if done:                                               # train.py:188-190
+            agent.ring.check()  # episode boundary: every store so far was exact
             self.episode += 1
             self.step_count = 0
             with torch.cuda.stream(side):

@@ -181,6 +181,12 @@ int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *ac
  * precision: 0 = fp32 MFMA (exact f32 products), 1 = fp16 MFMA with fp32
  * accumulation and fp32 master weights (the reference's mixed_float16),
  * 2 = the same with bf16 MFMA operands (mixed_bfloat16; BASELINE config C2). */
+/* Loss of the learn step: MSE is the reference's (dqn_agent.py:141, :352);
+ * Huber (delta 1, Keras mean reduction) is the loss of
+ * src/experimental/agent.py:99 that BASELINE.json's north_star names. */
+#define DMDQN_LOSS_MSE 0
+#define DMDQN_LOSS_HUBER 1
+
 typedef struct dmdqn_learn_args {
     int32_t NA, cap, start, batch, hidden, precision, sync_target, P;
     const int8_t *ring_s, *ring_n;   /* [NA][cap][DMDQN_ROW_BYTES]; the 16-bit
@@ -197,7 +203,7 @@ typedef struct dmdqn_learn_args {
                                         f32 target to f16 for its matmuls, so
                                         this is the exact operand; written on
                                         target syncs.  NULL: use `target`.     */
-    float *loss;                     /* [NA] MSE loss of this learn (or NULL) */
+    float *loss;                     /* [NA] loss of this learn (or NULL)     */
     float gamma, alpha, c1, c2, eps; /* alpha = lr*sqrt(1-b2^t)/(1-b1^t),
                                         c1 = 1-b1, c2 = 1-b2 (float32)       */
     uint64_t *stamps;                /* diagnostics: NULL, or [NA][16] phase
@@ -211,6 +217,10 @@ typedef struct dmdqn_learn_args {
                                         online net (Keras' f16 cast of the f32
                                         variables) the forwards read; dmdqn_adam
                                         rewrites it.  Ignored by dmdqn_learn. */
+    int32_t loss_kind;               /* DMDQN_LOSS_MSE (default) | DMDQN_LOSS_HUBER */
+    float *rn_out;                   /* diagnostics: NULL, or [NA][batch] the
+                                        z-scored rewards the learn used
+                                        (ReplayBuffer.sample :66-69, f32)     */
 } dmdqn_learn_args;
 
 int dmdqn_learn(const dmdqn_learn_args *args, void *stream);

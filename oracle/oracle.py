@@ -329,3 +329,81 @@ def train_loop(R, Cc, E, fill, steps, seed=0, threads=1):
     n = C.c_long(0)
     el = L.orc_train_loop(R, Cc, E, fill, steps, seed, threads, C.byref(n))
     return el, n.value
+
+
+# ---------------------------------------------------------------- the loop body, one replica
+class OracleLoop:
+    """src/scripts/train.py:188-310 for ONE env replica on the CPU oracle (TEST
+    INFRASTRUCTURE): env step (oracle_sim.c), observe / reward from the pre-step
+    local state, act on the replica's numpy stream (epsilon 1, A-1), remember
+    into a per-agent deque of maxlen `cap`, then per agent in junction order
+    random.sample on the replica's CPython stream, z-score and (learn=True) the
+    fp32 learn of oracle_learn.c, with the hard target sync every `tuf` learns.
+    Episode end (done: t >= max_time or no vehicle left, train.py:233-236)
+    reloads the replica (train.py:190).  With learn=False the replay draws
+    still run (they advance the stream exactly as the training loop does)."""
+
+    def __init__(self, R, Cc, seed, cap=10000, tuf=500, weights=None, mode=0, max_time=2400,
+                 learn=True, loss_kind=0, H=128, gamma=0.99, lr=1e-3, env=None):
+        self.R, self.C, self.A = R, Cc, R * Cc
+        self.env = env or OracleEnv(R, Cc, seed)
+        self.nps, self.pys = np_stream(seed), py_stream(seed)
+        self.cap, self.tuf, self.mode, self.max_time = cap, tuf, mode, max_time
+        self.learn, self.loss_kind, self.H, self.gamma, self.lr = learn, loss_kind, H, gamma, lr
+        self.dq = [[] for _ in range(self.A)]
+        if learn:
+            self.params = np.array(weights, np.float32).reshape(self.A, -1).copy()
+            self.target = self.params.copy()
+            self.m = np.zeros_like(self.params)
+            self.v = np.zeros_like(self.params)
+        self.learn_steps = 0
+        self._reset()
+
+    def _reset(self):
+        A = self.A
+        self.t = 0
+        self.L = local_state(np.zeros((A, 12)), np.zeros(A), np.zeros(A), self.mode)
+        self.obs = build_obs(self.R, self.C, self.L)
+
+    def step(self):
+        A = self.A
+        acts = act(self.nps, A, 1.0)
+        halt, ph, ts, done = self.env.step(acts, 3, self.t, 10, self.max_time)
+        self.t += 10
+        rew = reward(self.L)
+        L2 = local_state(halt, ph, ts, self.mode)
+        obs2 = build_obs(self.R, self.C, L2)
+        for j in range(A):
+            self.dq[j].append((self.obs[j].astype(np.int8), int(acts[j]), float(rew[j]),
+                               obs2[j].astype(np.int8), float(done)))
+            if len(self.dq[j]) > self.cap:
+                self.dq[j].pop(0)
+        out = {"actions": acts, "halt": halt, "phase": ph, "tspent": ts, "reward": rew,
+               "obs": obs2, "done": done, "idx": None, "loss": None}
+        n = len(self.dq[0])
+        if n >= 128:
+            idx = np.zeros((A, 128), np.int32)
+            loss = np.zeros(A, np.float32)
+            if self.learn:
+                self.learn_steps += 1
+            for j in range(A):
+                idx[j] = py_sample(self.pys, n, 128)
+                if self.learn:
+                    d = self.dq[j]
+                    S = np.stack([d[i][0] for i in idx[j]]).astype(np.float32)
+                    Aa = np.array([d[i][1] for i in idx[j]], np.int32)
+                    Rn = zscore(np.array([d[i][2] for i in idx[j]]))
+                    S2 = np.stack([d[i][3] for i in idx[j]]).astype(np.float32)
+                    Dn = np.array([d[i][4] for i in idx[j]], np.float32)
+                    loss[j] = learn(self.params[j], self.target[j], self.m[j], self.v[j], S, Aa, Rn,
+                                    S2, Dn, self.learn_steps, gamma=self.gamma, lr=self.lr,
+                                    H1=self.H, H2=self.H, loss_kind=self.loss_kind)
+            if self.learn and self.learn_steps % self.tuf == 0:
+                self.target = self.params.copy()
+            out["idx"], out["loss"] = idx, (loss if self.learn else None)
+        if done:
+            self.env.reset()
+            self._reset()
+        else:
+            self.L, self.obs = L2, obs2
+        return out

@@ -65,11 +65,14 @@ class ReplayBuffer:
         _, py = _streams(self.device)
         idx = K.replay_sample(py, 1, n, batch_size)[0].long()
         slots = (self.ring.start + idx) % self.ring.cap
-        r = self.ring.r[0, slots]
-        mean = r.mean()
-        std = ((r - mean) ** 2).mean().sqrt()
+        # the z-score in float64 numpy on the host, exactly the reference's
+        # expression (:66-69: np.mean / np.std use numpy's pairwise summation),
+        # so the rewards are bit-identical; the fused learn kernel restates the
+        # same order on the device
+        r = self.ring.r[0, slots].cpu().numpy()
+        rn = ((r - np.mean(r)) / (np.std(r) + 1e-8)).astype(np.float32)
         return (self.ring.s[0, slots, :89].float(), self.ring.a[0, slots].int(),
-                ((r - mean) / (std + 1e-8)).float(), self.ring.n[0, slots, :89].float(),
+                torch.from_numpy(rn).to(self.device), self.ring.n[0, slots, :89].float(),
                 self.ring.d[0, slots].float())
 
     def __len__(self):
@@ -113,6 +116,7 @@ class DQNAgent:
 
     def remember(self, state, action, reward, next_state, done):
         self.replay_buffer.add((state, action, reward, next_state, done))  # :312-326
+        self.replay_buffer.ring.check()  # per-call host path: a non-int8 value raises now
 
     def learn(self):
         """One fused learn step; None while the buffer is underfilled (:333-335)."""
