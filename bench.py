@@ -12,9 +12,10 @@ Keras-style weights) and resident in HBM before the timed region.
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run, one rank per GPU, each with its own env shard
 (env ids offset by rank), no data-path collectives ("weak" scaling).
-The replay rings are first filled for batch_size-1 untimed steps so that the
-learn step is active in every warm-up and timed step (train.py learns only
-once a buffer holds batch_size transitions, dqn_agent.py:333).
+The replay rings are first filled for replay_buffer_size (10000) untimed
+steps, so the timed steps run the steady state a training run spends almost
+all of its steps in: every ring full and wrapped, the learn active
+(dqn_agent.py:333) and the sampler in CPython's set branch at n = 10000.
 """
 import argparse
 import json
@@ -56,24 +57,52 @@ MFMA_OPS = {"fp32": "v_mfma_f32_16x16x4_f32", "fp16": "v_mfma_f32_16x16x32_f16",
 SIM_BYTES_PER_VEH_SUBSTEP = 20  # read x, v, lane cursor (12 B) + write x, v (8 B)
 
 
+def cpu_model():
+    """The host CPU's model string (/proc/cpuinfo), or the platform's name."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def cpu_threads():
+    """Threads for the multi-threaded CPU baseline: the CPUs this process may
+    run on (affinity), capped by OMP_NUM_THREADS when the launcher sets it --
+    on the GPU pool the box's CPU share for one GPU is 16 and OMP_NUM_THREADS
+    says so, while nproc / os.cpu_count() report the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp else max(1, n)
+
+
 def cpu_baseline(rows, cols, steps=60, seed=0):
     """The reference loop body on the GPU box's host cores: oracle/oracle_loop.c
     (the C restatement the parity tests pin -- act, sim, observe, reward,
     remember, CPython sample, z-score, Double-DQN learn with Keras Adam) for env
     replicas of the same grid, learn active after a 127-step untimed fill.
     Runs 1 thread x 1 replica and T threads x T replicas (OpenMP over replicas,
-    T = OMP_NUM_THREADS capped by the CPU count).  Returns the cpu_baseline dict
-    (value = the T-thread throughput)."""
+    T = cpu_threads()), plus BASELINE config C1 (1x1 grid, 1 agent, 1 thread).
+    Returns the cpu_baseline dict (value = the T-thread throughput)."""
     import oracle as O
     A = rows * cols
     el1, n1 = O.train_loop(rows, cols, 1, 127, steps, seed, 1)
-    T = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    T = cpu_threads()
     elT, nT = O.train_loop(rows, cols, T, 127, steps, seed, T)
+    c1s = 240  # one full episode of the 1x1 grid after the fill
+    elc, nc = O.train_loop(1, 1, 1, 127, c1s, seed, 1)
     return {"value": round(nT / elT, 2), "unit": "agent-env steps/s", "cores": T, "kind": "port",
             "single_thread_value": round(n1 / el1, 2),
+            "c1_1x1_single_thread_value": round(nc / elc, 2),
+            "cpu_model": cpu_model(), "machine_logical_cpus": os.cpu_count(),
             "sample": (f"{rows}x{cols} grid ({A} agents): {T} replicas x {steps} RL steps on "
                        f"{T} threads ({elT:.1f} s) and 1 replica x {steps} steps on 1 thread "
-                       f"({el1:.1f} s), learn active after a 127-step untimed fill; "
+                       f"({el1:.1f} s); C1 1x1 grid, 1 agent, {c1s} steps on 1 thread "
+                       f"({elc:.1f} s); learn active after a 127-step untimed fill; "
                        "oracle/oracle_loop.c (C restatement, OpenMP over replicas)")}
 
 
@@ -149,9 +178,10 @@ def main():
                     help="C5: one shared network (mean per-agent loss, RCCL gradient "
                          "all-reduce across ranks); use with --rows 8 --cols 8")
     ap.add_argument("--prefill-steps", type=int, default=None,
-                    help="untimed loop steps before warm-up (default batch_size-1: the learn "
-                         "starts at the first warm-up step; >= 1045 puts the replay sampler in "
-                         "its steady-state set branch, as in long training runs)")
+                    help="untimed loop steps before warm-up (default replay_buffer_size = "
+                         "10000: the timed steps run at the steady state of a training run -- "
+                         "full, wrapped rings, sampler in CPython's set branch at n = 10000; "
+                         "batch_size-1 = 127 times the first learns instead)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=60,
                     help="timed RL steps per replica of the CPU baseline")
@@ -204,7 +234,7 @@ def main():
     tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side)
     E, A = tr.env.E, tr.env.A
     NA = E * A
-    prefill = agent_cfg.batch_size - 1 if args.prefill_steps is None else args.prefill_steps
+    prefill = agent_cfg.replay_buffer_size if args.prefill_steps is None else args.prefill_steps
     for _ in range(prefill):  # replay fill (the learn joins once a ring holds batch_size)
         tr.step()
     for _ in range(args.warmup):
@@ -301,7 +331,9 @@ def main():
             "config": {
                 "workload": f"{cname}: {args.rows}x{args.cols} grid ({A} agents) x {args.envs} "
                             "envs/GPU, full RL step (act, 10 IDM substeps, observe, remember, "
-                            f"sample, {learn_desc}), H=128, batch 128, replay 10000",
+                            f"sample, {learn_desc}), H=128, batch 128, replay 10000 "
+                            f"(timed at n = {min(prefill + args.warmup + 1, agent_cfg.replay_buffer_size)}"
+                            f"..{min(prefill + args.warmup + args.steps, agent_cfg.replay_buffer_size)})",
                 "envs_per_gpu": args.envs, "agents_per_env": A, "global_envs": args.envs * world,
                 "replay_prefill_steps": prefill,
                 "replay_len_timed": [min(prefill + args.warmup + 1, agent_cfg.replay_buffer_size),

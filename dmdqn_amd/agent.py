@@ -23,8 +23,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import call, ptr, stream_of
 from . import kernels as K
+from .ops import load as _ops
 
 D_IN = 89
 N_ACTIONS = 4
@@ -41,6 +41,8 @@ class CLearn(C.Structure):
         ("loss_kind", C.c_int32), ("rn_out", C.c_void_p)]
 
 
+# ctypes signatures of the learn entry points: the C-ABI tests call them
+# directly (c_learn_args); the product path goes through torch.ops.dmdqn
 _lib.register({
     "dmdqn_learn": [C.POINTER(CLearn), C.c_void_p],
     "dmdqn_q_argmax": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -52,6 +54,8 @@ _lib.register({
     "dmdqn_adam": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                    C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
                    C.c_int, C.c_void_p],
+    "dmdqn_target_sync": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                          C.c_void_p],
 })
 
 PRECISIONS = {"fp32": 0, "fp16": 1, "bf16": 2}
@@ -189,6 +193,21 @@ def keras_initial_weights(rng, hidden, n_agents):
     return np.concatenate(parts, axis=1).astype(np.float32)
 
 
+def initial_weights(seed, env_seeds, n_agents, hidden, shared=False):
+    """Initial weights [NW, P_keras] for the agents of the replicas whose env
+    seeds are `env_seeds` (n_agents per replica).  Each replica's agents draw
+    from their own generator, keyed on (seed, env seed), so a rank that owns
+    replicas [r*E, (r+1)*E) builds exactly the weights those replicas get in a
+    single-process run (shards are independent).  The shared net
+    (C5) draws from `seed` alone, identical on every rank."""
+    if shared:
+        return keras_initial_weights(np.random.RandomState(seed & 0xFFFFFFFF), hidden, 1)
+    return np.concatenate([
+        keras_initial_weights(np.random.RandomState([seed & 0xFFFFFFFF, int(s) & 0xFFFFFFFF,
+                                                     0x5EED]), hidden, n_agents)
+        for s in env_seeds])
+
+
 @dataclass
 class AgentConfig:
     """Keys of config/agent_config.yaml; defaults are the values train.py uses
@@ -224,7 +243,7 @@ class BatchedDQN:
     def __init__(self, num_envs, n_agents, cfg: AgentConfig = None, device="cuda",
                  env_seeds=None, init_weights=None, streams=None):
         self.cfg = cfg = cfg or AgentConfig()
-        _lib.load()
+        self._ops = _ops()
         H = cfg.nn_layers[0]
         if len(cfg.nn_layers) != 2 or cfg.nn_layers[1] != H or H not in (64, 128):
             raise ValueError("the fused learn kernel supports nn_layers [64,64] or [128,128]")
@@ -242,8 +261,10 @@ class BatchedDQN:
         self.shared = cfg.shared_params
         self.NW = NW = 1 if self.shared else NA   # parameter sets
         self.H, self.P = H, n_params(H)
+        seeds = (np.arange(num_envs, dtype=np.int64) + cfg.seed if env_seeds is None
+                 else np.asarray(env_seeds))
         if init_weights is None:
-            init_weights = keras_initial_weights(np.random.RandomState(cfg.seed), H, NW)
+            init_weights = initial_weights(cfg.seed, seeds, n_agents, H, self.shared)
         init = np.asarray(init_weights, dtype=np.float32).reshape(NW, -1)
         if init.shape[1] == n_params_keras(H):
             init = keras_to_kernel(init, H)
@@ -279,8 +300,6 @@ class BatchedDQN:
             # ones behind the per-agent DQNAgent surface
             self.np_state, self.py_state = streams
         else:
-            seeds = (np.arange(num_envs, dtype=np.int64) + cfg.seed if env_seeds is None
-                     else np.asarray(env_seeds))
             self.np_state = K.seed_streams(seeds, "np", dev)
             self.py_state = K.seed_streams(seeds, "py", dev)
         # two index buffers: presample() may draw the next learn's batch (on
@@ -323,9 +342,8 @@ class BatchedDQN:
         eps = self.current_epsilon() if eps is None else float(eps)
         greedy = None
         if eps < 1.0:
-            call("dmdqn_q_argmax_shared" if self.shared else "dmdqn_q_argmax", ptr(self.params),
-                 self.NA, self.P, self.H, ptr(obs.reshape(self.NA, D_IN)), ptr(self.greedy), None,
-                 stream_of(self.device))
+            self._ops.q_argmax(self.params, self.H, obs.reshape(self.NA, D_IN).contiguous(),
+                               self.greedy, None, self.shared)
             greedy = self.greedy
         self.actions = self._act_bufs[1] if self.actions is self._act_bufs[0] else self._act_bufs[0]
         return K.act(self.np_state, self.A, eps=eps, n_actions=N_ACTIONS, greedy=greedy,
@@ -370,28 +388,40 @@ class BatchedDQN:
         self.learn_step_counter += 1
         alpha, c1, c2, eps = keras_adam_consts(self.learn_step_counter, cfg.learning_rate)
         sync = self.learn_step_counter % cfg.target_update_frequency == 0
-        a = CLearn(self.NA, self.ring.cap, self.ring.start, cfg.batch_size, self.H,
-                   PRECISIONS[cfg.precision], int(sync), self.P,
-                   *[None if t is None else t.data_ptr()
-                     for t in [self.ring.s, self.ring.n, self.ring.a, self.ring.d, self.ring.r,
-                               self.idx, self.params, self.adam_m, self.adam_v, self.target,
-                               self.target_h, self.loss]],
-                   np.float32(cfg.gamma), alpha, c1, c2, eps,
-                   None if self.stamps is None else self.stamps.data_ptr(),
-                   self.qstats.zero_().data_ptr() if collect_stats else None,
-                   None if self.params_h is None else self.params_h.data_ptr(),
-                   LOSSES[cfg.loss], None if self.rn_out is None else self.rn_out.data_ptr())
-        self._last_args = a  # keeps the struct (and what it points at) inspectable
+        qstats = self.qstats.zero_() if collect_stats else None
+        self._last_learn = (alpha, c1, c2, eps, sync, qstats)
         if self.learn_hook:
             self.learn_hook(True)
+        ring = self.ring
         if self.shared:
-            self._learn_shared(a, alpha, c1, c2, eps, sync)
+            self._learn_shared(alpha, c1, c2, eps, sync, qstats)
         else:
-            call("dmdqn_learn", C.byref(a), stream_of(self.device))
+            self._ops.learn_step(ring.s, ring.n, ring.a, ring.d, ring.r, self.idx, self.params,
+                                 self.adam_m, self.adam_v, self.target, self.target_h, self.loss,
+                                 ring.start, self.H, PRECISIONS[cfg.precision], sync, cfg.gamma,
+                                 alpha, c1, c2, eps, LOSSES[cfg.loss], qstats, self.rn_out,
+                                 self.stamps)
         if self.learn_hook:
             self.learn_hook(False)
         self.learn_launches += 1
         return self.loss
+
+    def c_learn_args(self):
+        """The dmdqn_learn_args struct of the last learn (ctypes), for tests that
+        call the C ABI directly; the tensors it points at belong to self."""
+        alpha, c1, c2, eps, sync, qstats = self._last_learn
+        cfg = self.cfg
+        return CLearn(self.NA, self.ring.cap, self.ring.start, cfg.batch_size, self.H,
+                      PRECISIONS[cfg.precision], int(sync), self.P,
+                      *[None if t is None else t.data_ptr()
+                        for t in [self.ring.s, self.ring.n, self.ring.a, self.ring.d, self.ring.r,
+                                  self.idx, self.params, self.adam_m, self.adam_v, self.target,
+                                  self.target_h, self.loss]],
+                      np.float32(cfg.gamma), alpha, c1, c2, eps,
+                      None if self.stamps is None else self.stamps.data_ptr(),
+                      None if qstats is None else qstats.data_ptr(),
+                      None if self.params_h is None else self.params_h.data_ptr(),
+                      LOSSES[cfg.loss], None if self.rn_out is None else self.rn_out.data_ptr())
 
     def presample(self, n):
         """Draw the next learn's replay indices now (ReplayBuffer.sample,
@@ -422,22 +452,27 @@ class BatchedDQN:
                 "q_values_mean": float(mean.mean()), "q_values_std": float(std.mean()),
                 "action_distribution": qs[:, 2:6].sum(0).round().long().tolist()}
 
-    def _learn_shared(self, a, alpha, c1, c2, eps, sync):
+    def _learn_shared(self, alpha, c1, c2, eps, sync, qstats):
         """C5: grad = mean over this rank's agents of the per-agent gradients,
         all-reduced (sum, RCCL) across ranks, then one Adam step with 1/world."""
         import torch.distributed as dist
-        st = stream_of(self.device)
-        call("dmdqn_learn_shared_grad", C.byref(a), ptr(self.slab), self.n_slabs, ptr(self.grad),
-             C.c_float(1.0 / self.NA), st)
+        ring, cfg = self.ring, self.cfg
+        self._ops.learn_shared_grad(ring.s, ring.n, ring.a, ring.d, ring.r, self.idx, self.params,
+                                    self.target, self.target_h, self.params_h, self.loss,
+                                    ring.start, cfg.gamma, LOSSES[cfg.loss], qstats, self.rn_out,
+                                    self.slab, self.grad, 1.0 / self.NA)
         world = 1
         if dist.is_available() and dist.is_initialized():
             world = dist.get_world_size()
-            if world > 1:
+            if world > 1 and dist.get_backend() == "gloo" and self.grad.is_cuda:
+                # gloo (several ranks on one device: the multi-process tests) reduces host memory
+                g = self.grad.cpu()
+                dist.all_reduce(g, op=dist.ReduceOp.SUM)
+                self.grad.copy_(g)
+            elif world > 1:
                 dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)  # one flat 114 KB buffer
-        call("dmdqn_adam", ptr(self.params), ptr(self.adam_m), ptr(self.adam_v), ptr(self.target),
-             ptr(self.target_h), ptr(self.params_h), ptr(self.grad), self.P, C.c_float(1.0 / world),
-             C.c_float(alpha),
-             C.c_float(c1), C.c_float(c2), C.c_float(eps), int(sync), st)
+        self._ops.adam(self.params, self.adam_m, self.adam_v, self.target, self.target_h,
+                       self.params_h, self.grad, 1.0 / world, alpha, c1, c2, eps, sync)
 
     def _refresh_params_h(self):
         if self.params_h is not None:
@@ -448,8 +483,9 @@ class BatchedDQN:
             self.target_h[:, :self.P].copy_(self.target.to(self.target_h.dtype))
 
     def update_target_network(self):
-        self.target.copy_(self.params)
-        self._refresh_target_h()
+        """dqn_agent.py:382-387: target <- online, and the 16-bit shadow."""
+        self._ops.target_sync(self.params, self.target, self.target_h,
+                              PRECISIONS[self.cfg.precision])
 
     # -------------------------------------------------------------- weights
     def keras_params(self, which="params"):

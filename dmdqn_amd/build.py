@@ -69,6 +69,43 @@ def _compile(src, force):
     return obj, True
 
 
+TORCH_EXT = os.path.join(HERE, "torch_ext", "dmdqn_torch.cpp")
+TORCH_LIBNAME = "libdmdqn_torch.so"
+
+
+def build_torch_ext(force=False, verbose=True):
+    """libdmdqn_torch.so: the C ABI registered as torch.ops.dmdqn.* (TORCH_LIBRARY),
+    linked against libdmdqn_hip.so (same directory) and the installed PyTorch."""
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    so = os.path.join(LIBDIR, TORCH_LIBNAME)
+    deps = [TORCH_EXT, os.path.join(LIBDIR, LIBNAME)] + _headers()
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags = ["-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+             f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{tdir}/include",
+             f"-I{tdir}/include/torch/csrc/api/include", "-I/opt/rocm/include"]
+    stamp = so + ".flags"
+    try:
+        with open(stamp) as f:
+            same = f.read() == " ".join(flags)
+    except OSError:
+        same = False
+    if (not force and same and os.path.exists(so)
+            and os.path.getmtime(so) >= max(os.path.getmtime(d) for d in deps)):
+        return so
+    cmd = (["g++"] + flags + ["-shared", TORCH_EXT, "-o", so, f"-L{tdir}/lib", "-lc10", "-lc10_hip",
+                              "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-L{LIBDIR}", "-ldmdqn_hip",
+                              "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{tdir}/lib"])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch extension build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(" ".join(flags))
+    if verbose:
+        print(f"built {so}")
+    return so
+
+
 def build(force=False, verbose=True):
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = _sources()
@@ -83,6 +120,7 @@ def build(force=False, verbose=True):
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"built {so}")
+    build_torch_ext(force, verbose)
     return so
 
 

@@ -492,3 +492,35 @@ extern "C" int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hid
                                      const float *obs, int32_t *out, float *q_out, void *stream) {
     return q_argmax(params, 0, NA, P, hidden, obs, out, q_out, stream);
 }
+
+// Hard target sync outside a learn (dqn_agent.py:382-387, update_target_network):
+// target <- params for NW nets, and the 16-bit shadow the target forward reads
+// (RNE; f16 or bf16) when target_h is given.
+template <typename T16>
+__global__ void __launch_bounds__(256) k_target_sync(const float *params, float *target,
+                                                     T16 *target_h, int P, int Ph, long n) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const long w = i / P, k = i - w * P;
+    const float x = params[i];
+    target[i] = x;
+    if (target_h) target_h[w * Ph + k] = (T16)x;
+}
+
+extern "C" int dmdqn_target_sync(const float *params, float *target, uint16_t *target_h, int NW,
+                                 int P, int Ph, int precision, void *stream) {
+    DMDQN_REQUIRE(params && target && NW > 0 && P > 0 && Ph >= P,
+                  "dmdqn_target_sync: NW=%d P=%d Ph=%d", NW, P, Ph);
+    DMDQN_REQUIRE(precision >= 0 && precision <= 2, "dmdqn_target_sync: precision %d", precision);
+    DMDQN_REQUIRE(!target_h || precision != 0, "dmdqn_target_sync: fp32 has no 16-bit shadow");
+    const long n = (long)NW * P;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (precision == 2)
+        hipLaunchKernelGGL(k_target_sync<__bf16>, grid, dim3(256), 0, as_stream(stream), params,
+                           target, reinterpret_cast<__bf16 *>(target_h), P, Ph, n);
+    else
+        hipLaunchKernelGGL(k_target_sync<_Float16>, grid, dim3(256), 0, as_stream(stream), params,
+                           target, reinterpret_cast<_Float16 *>(target_h), P, Ph, n);
+    DMDQN_LAUNCH_CHECK("k_target_sync");
+    return DMDQN_OK;
+}

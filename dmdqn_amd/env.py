@@ -16,16 +16,14 @@ Semantics follow train.py (89-dim N,S,E,W observation, reward on the PRE-step
 state, setPhase every RL step with ACTION_MAP {0:0,1:3,2:6,3:9}, K = 10
 one-second substeps, done at t >= 2400), not sumo_env.py's 74-dim variant.
 """
-import ctypes as C
 from dataclasses import dataclass, field
 from typing import Optional
 
 import numpy as np
 import torch
 
-from . import _lib
-from ._lib import call, ptr, stream_of
 from . import kernels as K
+from .ops import load as load_ops
 from .scenario import Grid, demand_tables
 
 SIGNAL_MODES = {"reference": 0, "intended": 1}
@@ -44,12 +42,14 @@ class IDMParams:
     len_inner: float = 172.8
     len_outer: float = 86.4
 
-    def c_struct(self):
+    def values(self):
+        """The dmdqn_idm constants in struct order (include/dmdqn.h), as float32
+        values (two_sqrt_ab = 2 sqrt(a b) computed in float32, as the oracle)."""
         f = np.float32
         two_sqrt_ab = f(2.0) * np.sqrt(f(self.accel) * f(self.decel), dtype=np.float32)
-        return CIdm(f(self.length), f(self.min_gap), f(self.accel), f(self.decel), f(self.tau),
-                    f(self.vmax), f(two_sqrt_ab), f(self.halt_speed), f(self.len_inner),
-                    f(self.len_outer))
+        return [float(f(x)) for x in (self.length, self.min_gap, self.accel, self.decel, self.tau,
+                                      self.vmax, two_sqrt_ab, self.halt_speed, self.len_inner,
+                                      self.len_outer)]
 
 
 @dataclass
@@ -78,26 +78,6 @@ class EnvConfig:
         return self.rows * self.cols
 
 
-class CSim(C.Structure):
-    _fields_ = [("R", C.c_int32), ("C", C.c_int32), ("E", C.c_int32), ("cap_lane", C.c_int32),
-                ("period_ms", C.c_int32), ("nveh", C.c_int32)] + [
-        (n, C.c_void_p) for n in ["x", "v", "dst", "head", "cnt", "req", "gfrom", "fx", "fv",
-                                  "tl_phase", "tl_ts", "qptr", "q_off", "q_ids", "vdst",
-                                  "exit_id", "exit_ao", "stats", "q_dst"]]
-
-
-class CIdm(C.Structure):
-    _fields_ = [(n, C.c_float) for n in ["length", "min_gap", "accel", "decel", "tau", "vmax",
-                                         "two_sqrt_ab", "halt_speed", "len_inner", "len_outer"]]
-
-
-_lib.register({
-    "dmdqn_sim_reset": [C.POINTER(CSim), C.c_void_p],
-    "dmdqn_sim_step": [C.POINTER(CSim), C.POINTER(CIdm), C.c_void_p, C.c_int, C.c_int, C.c_int,
-                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
-})
-
-
 class TrafficEnv:
     """E replicas of the grid on one device.  All state lives in device memory."""
 
@@ -105,7 +85,7 @@ class TrafficEnv:
         self.cfg = cfg = cfg or EnvConfig()
         if cfg.signal_features not in SIGNAL_MODES:
             raise ValueError(f"signal_features must be one of {list(SIGNAL_MODES)}")
-        _lib.load()
+        self._ops = load_ops()
         self.device = torch.device(device)
         self.scenario = None
         if cfg.scenario:
@@ -148,13 +128,14 @@ class TrafficEnv:
         self.t_exit_id = torch.from_numpy(g.exit_id.reshape(-1).copy()).to(dev)
         self.t_exit_ao = torch.from_numpy(g.exit_ao.reshape(-1).copy()).to(dev)
         self.t_stats = z32(E, 4)
-        self.csim = CSim(cfg.rows, cfg.cols, E, cap, period, nveh, *[
-            t.data_ptr() for t in [self.t_x, self.t_v, self.t_dst, self.t_head, self.t_cnt,
-                                   self.t_req, self.t_gfrom, self.t_fx, self.t_fv,
-                                   self.t_phase_state, self.t_ts, self.t_qptr, self.t_q_off,
-                                   self.t_q_ids, self.t_vdst, self.t_exit_id, self.t_exit_ao,
-                                   self.t_stats, self.t_q_dst]])
-        self.cidm = cfg.idm.c_struct()
+        # the dmdqn_sim arrays in the order of the sim ops (dmdqn_torch.cpp make_sim)
+        self._sim_state = [self.t_x, self.t_v, self.t_dst, self.t_head, self.t_cnt, self.t_req,
+                           self.t_gfrom, self.t_fx, self.t_fv, self.t_phase_state, self.t_ts,
+                           self.t_qptr, self.t_stats]
+        self._sim_tables = [self.t_q_off, self.t_q_ids, self.t_vdst, self.t_exit_id,
+                            self.t_exit_ao, self.t_q_dst]
+        self._sim_dims = [cfg.rows, cfg.cols, E, cap, period, nveh]
+        self._idm = cfg.idm.values()
         # observation buffers
         self.halt = z32(E, A, 12)
         self.phase = z32(E, A)
@@ -170,7 +151,7 @@ class TrafficEnv:
     # ------------------------------------------------------------ batched API
     def reset(self):
         """traci.load (train.py:190) for every replica; returns obs [E,A,89]."""
-        call("dmdqn_sim_reset", C.byref(self.csim), stream_of(self.device))
+        self._ops.sim_reset(self._sim_state, self._sim_tables, self._sim_dims)
         self.t = 0
         self.halt.zero_()
         self.phase.zero_()
@@ -190,9 +171,9 @@ class TrafficEnv:
         cfg = self.cfg
         if self.sim_hook:
             self.sim_hook(True)
-        call("dmdqn_sim_step", C.byref(self.csim), C.byref(self.cidm), ptr(actions),
-             cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time, ptr(self.halt),
-             ptr(self.phase), ptr(self.tspent), ptr(self.done_u8), stream_of(self.device))
+        self._ops.sim_step(self._sim_state, self._sim_tables, self._sim_dims, self._idm, actions,
+                           cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time,
+                           self.halt, self.phase, self.tspent, self.done_u8)
         if self.sim_hook:
             self.sim_hook(False)
         self.t += cfg.step_duration

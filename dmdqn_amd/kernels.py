@@ -1,13 +1,15 @@
-"""Thin torch-facing wrappers over the C ABI (device tensors in, device tensors out).
+"""Thin torch-facing wrappers over the custom operators torch.ops.dmdqn.*
+(device tensors in, device tensors out).
 
 PyTorch is used only for device memory and the current HIP stream; every op
 below is one (or a few) launches of a hand-written gfx950 kernel in
-libdmdqn_hip.so, on torch's current stream.
+libdmdqn_hip.so, through the TORCH_LIBRARY(dmdqn) registration (ops.py), on
+torch's current stream.
 """
 import torch
 
 from . import _lib
-from ._lib import call, ptr, stream_of
+from .ops import load as _ops
 
 MT_WORDS = 625
 OBS_DIM = 89
@@ -33,15 +35,14 @@ def seed_streams(seeds, kind, device="cuda"):
     seeds = torch.as_tensor(seeds, dtype=torch.int64).to(device).contiguous()
     E = seeds.numel()
     st = torch.empty((E, MT_WORDS), dtype=torch.int32, device=device)
-    fn = "dmdqn_mt_seed_np" if kind == "np" else "dmdqn_mt_seed_py"
-    call(fn, ptr(st), ptr(seeds), E, stream_of(device))
+    _ops().mt_seed(st, seeds, "np" if kind == "np" else "py")
     return st
 
 
 def draw_u32(state, count):
     E = state.shape[0]
     out = torch.empty((E, count), dtype=torch.int32, device=state.device)
-    call("dmdqn_mt_draw_u32", ptr(state), E, count, ptr(out), stream_of(state.device))
+    _ops().mt_draw_u32(state, count, out)
     return out
 
 
@@ -53,8 +54,7 @@ def act(np_state, A, eps=1.0, n_actions=4, greedy=None, out=None):
         out = torch.empty((E, A), dtype=torch.int32, device=np_state.device)
     if greedy is not None:
         _check(greedy, torch.int32, (E, A), "greedy")
-    call("dmdqn_act", ptr(np_state), E, A, float(eps), n_actions, ptr(greedy), ptr(out),
-         stream_of(np_state.device))
+    _ops().act(np_state, A, float(eps), n_actions, greedy, out)
     return out
 
 
@@ -72,8 +72,7 @@ def observe(R, C, halt, phase, tspent, mode, prev_local=None, want_obs=True):
     if prev_local is not None:
         _check(prev_local, torch.float32, (E, A, LOCAL_DIM), "prev_local")
         reward = torch.empty((E, A), dtype=torch.float64, device=dev)
-    call("dmdqn_observe", R, C, E, ptr(halt), ptr(phase), ptr(tspent), int(mode), ptr(local),
-         ptr(obs), ptr(prev_local), ptr(reward), stream_of(dev))
+    _ops().observe(R, C, halt, phase, tspent, int(mode), local, obs, prev_local, reward)
     return local, obs, reward
 
 
@@ -113,9 +112,8 @@ class ReplayRing:
         _check(rew, torch.float64, (NA,), "rew")
         _check(done, torch.uint8, (NA,), "done")
         slot = self.total % self.cap
-        call("dmdqn_replay_store", NA, self.cap, slot, ptr(obs_s), ptr(obs_n), ptr(act), ptr(rew),
-             ptr(done), ptr(self.s), ptr(self.n), ptr(self.a), ptr(self.r), ptr(self.d),
-             ptr(self.err), stream_of(obs_s.device))
+        _ops().replay_store(slot, obs_s, obs_n, act, rew, done, self.s, self.n, self.a, self.r,
+                            self.d, self.err)
         self.total += 1
 
     def check(self):
@@ -150,6 +148,5 @@ def replay_sample(py_state, A, n, k=128, out=None):
     _check(py_state, torch.int32, (E, MT_WORDS), "py_state")
     if out is None:
         out = torch.empty((E * A, k), dtype=torch.int32, device=py_state.device)
-    call("dmdqn_replay_sample", ptr(py_state), E, A, int(n), int(k), ptr(out),
-         stream_of(py_state.device))
+    _ops().replay_sample(py_state, A, int(n), int(k), out)
     return out

@@ -225,6 +225,12 @@ typedef struct dmdqn_learn_args {
 
 int dmdqn_learn(const dmdqn_learn_args *args, void *stream);
 
+/* Hard target sync outside a learn (DQNAgent.update_target_network,
+ * dqn_agent.py:382-387): target[NW][P] <- params[NW][P]; when target_h is not
+ * NULL (precision 1 = f16, 2 = bf16) also its 16-bit shadow [NW][Ph], RNE. */
+int dmdqn_target_sync(const float *params, float *target, uint16_t *target_h, int NW, int P,
+                      int Ph, int precision, void *stream);
+
 /* Greedy actions argmax_a Q_online(obs) for NA agents (dqn_agent.py:268-273);
  * obs f32 [NA][89]; out int32 [NA].  Used by dmdqn_act when eps < 1. */
 int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, const float *obs,

@@ -344,7 +344,7 @@ class OracleLoop:
     still run (they advance the stream exactly as the training loop does)."""
 
     def __init__(self, R, Cc, seed, cap=10000, tuf=500, weights=None, mode=0, max_time=2400,
-                 learn=True, loss_kind=0, H=128, gamma=0.99, lr=1e-3, env=None):
+                 learn=True, loss_kind=0, H=128, gamma=0.99, lr=1e-3, env=None, track_ties=False):
         self.R, self.C, self.A = R, Cc, R * Cc
         self.env = env or OracleEnv(R, Cc, seed)
         self.nps, self.pys = np_stream(seed), py_stream(seed)
@@ -357,6 +357,11 @@ class OracleLoop:
             self.m = np.zeros_like(self.params)
             self.v = np.zeros_like(self.params)
         self.learn_steps = 0
+        # track_ties: per learn and agent, the smallest relative gap between the
+        # two largest online Q(S') of the batch -- below ~1e-6 the Double-DQN
+        # argmax (dqn_agent.py:342) can go either way under another fp32
+        # summation order, and two correct implementations part ways there
+        self.track_ties, self.tie_gaps = track_ties, []
         self._reset()
 
     def _reset(self):
@@ -386,6 +391,7 @@ class OracleLoop:
             loss = np.zeros(A, np.float32)
             if self.learn:
                 self.learn_steps += 1
+            gaps = np.full(A, np.inf)
             for j in range(A):
                 idx[j] = py_sample(self.pys, n, 128)
                 if self.learn:
@@ -395,9 +401,14 @@ class OracleLoop:
                     Rn = zscore(np.array([d[i][2] for i in idx[j]]))
                     S2 = np.stack([d[i][3] for i in idx[j]]).astype(np.float32)
                     Dn = np.array([d[i][4] for i in idx[j]], np.float32)
+                    if self.track_ties:
+                        q = np.sort(qnet_forward(self.params[j], S2, self.H, self.H), axis=1)
+                        gaps[j] = float(((q[:, -1] - q[:, -2]) / (np.abs(q[:, -1]) + 1e-30)).min())
                     loss[j] = learn(self.params[j], self.target[j], self.m[j], self.v[j], S, Aa, Rn,
                                     S2, Dn, self.learn_steps, gamma=self.gamma, lr=self.lr,
                                     H1=self.H, H2=self.H, loss_kind=self.loss_kind)
+            if self.learn and self.track_ties:
+                self.tie_gaps.append(gaps)
             if self.learn and self.learn_steps % self.tuf == 0:
                 self.target = self.params.copy()
             out["idx"], out["loss"] = idx, (loss if self.learn else None)

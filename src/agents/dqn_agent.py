@@ -15,6 +15,8 @@ Each DQNAgent is one agent slot run by the fused kernels (act, replay store,
 replay sample, learn).  For many agents / many env replicas use
 dmdqn_amd.agent.BatchedDQN, which runs all of them in one launch per stage.
 """
+import zlib
+
 import numpy as np
 import torch
 
@@ -33,6 +35,11 @@ def _streams(device):
     if str(device) not in _STREAMS:
         seed(0, device)
     return _STREAMS[str(device)]
+
+
+def init_seed(seed, agent_id):
+    """Initial-weight seed of agent `agent_id` (see DQNAgent.__init__)."""
+    return (int(seed) ^ zlib.crc32(str(agent_id).encode())) & 0x7FFFFFFF
 
 
 def _as_obs(x, device):
@@ -96,6 +103,11 @@ class DQNAgent:
         self.batch_size = cfg.batch_size
         self.target_update_frequency = cfg.target_update_frequency
         self.device = torch.device(device)
+        # Keras draws every model's initial weights from TF's global generator, so
+        # agents start from different weights; here each agent's initial-weight
+        # seed is cfg.seed mixed with a hash of its id (TF's stream itself cannot
+        # be reproduced)
+        cfg.seed = init_seed(cfg.seed, agent_id)
         self._core = BatchedDQN(1, 1, cfg, device=self.device, streams=_streams(self.device))
         self.replay_buffer = ReplayBuffer.__new__(ReplayBuffer)
         self.replay_buffer.device, self.replay_buffer.ring = self.device, self._core.ring

@@ -36,10 +36,29 @@ def test_all_declared_symbols_exported(lib):
     assert not missing, f"symbols declared in include/*.h but not exported: {missing}"
 
 
-def test_python_signatures_cover_header(lib):
-    from dmdqn_amd import _lib, agent, env  # noqa: F401  (agent / env register theirs)
+def test_python_bindings_cover_header(lib):
+    """Every compute entry point is wrapped by a torch.ops.dmdqn operator (the
+    product path) and every entry point but the sim's struct calls has a
+    ctypes signature (the C-ABI tests' path)."""
+    from dmdqn_amd import _lib, agent, env, ops  # noqa: F401  (agent registers its signatures)
     declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version"}
-    assert declared <= set(_lib.SIGNATURES), sorted(declared - set(_lib.SIGNATURES))
+    host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy"}
+    assert declared - host_only <= set(ops.ENTRY_POINTS), sorted(declared - host_only -
+                                                                 set(ops.ENTRY_POINTS))
+    ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_step"}
+    assert ctypes_only <= set(_lib.SIGNATURES), sorted(ctypes_only - set(_lib.SIGNATURES))
+
+
+def test_torch_ops_registered_without_gpu(lib):
+    """libdmdqn_torch.so loads on a CPU-only host and registers every op with
+    a schema; a CPU tensor is refused (no CPU kernel, no fallback)."""
+    import torch
+    from dmdqn_amd import ops
+    D = ops.load()
+    for name in set(ops.ENTRY_POINTS.values()):
+        assert getattr(D, name).default._schema.name == f"dmdqn::{name}"
+    with pytest.raises(NotImplementedError):
+        D.mt_seed(torch.zeros((1, 625), dtype=torch.int32), torch.zeros(1, dtype=torch.int64), "np")
 
 
 def test_version_and_error_string(lib):

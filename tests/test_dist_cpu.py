@@ -70,24 +70,25 @@ def _shared_worker(rank, ws, port, q):
     from dmdqn_amd import dist as D
     D.init(backend="gloo")
     P = 8
-    fake = SimpleNamespace(NA=4, n_slabs=2, P=P, device="cpu",
-                           slab=torch.zeros((2, P)), grad=torch.zeros(P),
-                           params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
-                           target=torch.zeros(P), target_h=None, params_h=None)
     seen = {}
 
-    def fake_call(name, *args):
-        if name == "dmdqn_learn_shared_grad":
-            fake.grad.copy_(torch.arange(P, dtype=torch.float32) * (rank + 1))
-            seen["scale"] = args[4].value
-        elif name == "dmdqn_adam":
-            seen["grad"] = fake.grad.tolist()
-            seen["gscale"] = args[8].value
-            seen["sync"] = args[13]
-        return 0
+    def learn_shared_grad(*args):
+        fake.grad.copy_(torch.arange(P, dtype=torch.float32) * (rank + 1))
+        seen["scale"] = args[-1]
 
-    AG.call, AG.stream_of = fake_call, (lambda *a: None)
-    AG.BatchedDQN._learn_shared(fake, AG.CLearn(), 1e-3, 0.1, 1e-3, 1e-7, True)
+    def adam(params, m, v, target, target_h, params_h, grad, gscale, alpha, c1, c2, eps, sync):
+        seen["grad"] = grad.tolist()
+        seen["gscale"] = gscale
+        seen["sync"] = sync
+
+    ring = SimpleNamespace(s=None, n=None, a=None, d=None, r=None, start=0)
+    fake = SimpleNamespace(NA=4, n_slabs=2, P=P, device="cpu", ring=ring, idx=None,
+                           cfg=AG.AgentConfig(), loss=None, rn_out=None,
+                           slab=torch.zeros((2, P)), grad=torch.zeros(P),
+                           params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
+                           target=torch.zeros(P), target_h=None, params_h=None,
+                           _ops=SimpleNamespace(learn_shared_grad=learn_shared_grad, adam=adam))
+    AG.BatchedDQN._learn_shared(fake, 1e-3, 0.1, 1e-3, 1e-7, True, None)
     q.put((rank, seen))
     dist.destroy_process_group()
 

@@ -1,0 +1,153 @@
+"""BASELINE configurations at their real size on one GPU, checked against the
+oracle on sampled replicas and agents (BASELINE.json configs).
+
+  C1  1x1 grid, 1 agent, the drop-in src/scripts/train.py loop (one episode)
+  C2  2x2 grid x 256 replicas, bf16, replay 10000
+  C3  4x4 grid x 1024 replicas, fp16 (mixed_float16), replay 10000: 16,384
+      learn workgroups, 21 GB per ring array (byte offsets past 2^31), 1100
+      steps so the sampler runs CPython's set branch (n > 1045)
+  C5  8x8 grid x 256 replicas, one shared network (the 8x8 sim runs from
+      global memory), replay 10000
+
+Per step, for sampled replicas (first, middle, last): actions, rewards and
+observations bit-exact vs oracle.OracleLoop (same seeds); once the replay is
+active, every sampled agent's 128 replay indices bit-exact vs CPython's
+random.sample.  At the checked learns, for 8 agents across those replicas: the
+device z-scored rewards bit-exact, the loss vs the 16-bit rounding emulation
+(test_gpu_learn TOL16) and vs the fp32 oracle (rtol 2e-2), and the
+gradient >= 99 % within the emulation's tolerance; every agent's loss finite.
+C4 (8 GPUs, env-sharded) is the C3 shard per GPU (tests/test_gpu_multiproc.py
+covers the sharding with real kernels)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import oracle as O  # noqa: E402
+from dmdqn_amd.agent import AgentConfig, initial_weights, kernel_to_keras  # noqa: E402
+from dmdqn_amd.env import EnvConfig  # noqa: E402
+from dmdqn_amd.trainer import Trainer  # noqa: E402
+
+from test_gpu_learn import ROUND, TOL16, _host_batch, _mixed_emulation  # noqa: E402
+
+DEV = "cuda"
+
+
+def _rows(t, idx):
+    return t[torch.as_tensor(idx, device=t.device)].cpu().numpy()
+
+
+def _check_learn(tr, agents, pre, precision, shared):
+    """One learn of tr's last step for `agents`, from the pre-step state `pre`."""
+    ag = tr.agent
+    rnd = ROUND[precision]
+    tl, ta, tr_, _, t32 = TOL16[precision]
+    loss = ag.loss.cpu().numpy()
+    assert np.isfinite(loss).all(), "every agent's loss is finite"
+    idx = ag.idx.cpu().numpy()
+    rn = ag.rn_out.cpu().numpy()
+    t = ag.learn_step_counter
+    p_now = kernel_to_keras(ag.params[0:1].cpu().numpy(), 128)[0] if shared else None
+    for k, j in enumerate(agents):
+        S, Aa, Rn, S2, D = _host_batch(ag, j, idx[j])
+        np.testing.assert_array_equal(rn[j], Rn)  # device z-score == numpy's
+        p0, t0, m0, v0 = (x[0 if shared else k] for x in pre)
+        l_e, g_e, _, _, _ = _mixed_emulation(p0, t0, m0, v0, S, Aa, Rn, S2, D, t, rnd=rnd)
+        np.testing.assert_allclose(loss[j], l_e, rtol=tl, err_msg=f"agent {j} vs emulation")
+        p1, m1, v1 = p0.copy(), m0.copy(), v0.copy()
+        l32 = O.learn(p1, t0, m1, v1, S, Aa, Rn, S2, D, t)
+        np.testing.assert_allclose(loss[j], l32, rtol=t32, err_msg=f"agent {j} vs fp32 oracle")
+        if not shared:
+            m_g = kernel_to_keras(ag.adam_m[j:j + 1].cpu().numpy(), 128)[0]
+            g_g = m0 + (m_g - m0) / np.float32(0.1)  # m1 = m0 + (g - m0) c1
+            gs = np.abs(g_e).max()
+            close = np.abs(g_g - g_e) <= 2 * ta * gs + tr_ * np.abs(g_e)
+            assert close.mean() > 0.99, f"agent {j}: {np.sum(~close)} gradient entries off"
+    if shared:
+        assert np.isfinite(p_now).all() and not np.array_equal(p_now, pre[0][0])
+
+
+def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False):
+    cfg = AgentConfig(precision=precision, seed=0, shared_params=shared)
+    tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=0), cfg)
+    A, ag = tr.env.A, tr.agent
+    sampled = [0, envs // 2, envs - 1]
+    loops = [O.OracleLoop(rows, cols, int(tr.env.seeds[e]), learn=False) for e in sampled]
+    arows = [e * A + j for e in sampled for j in range(A)]
+    pick = [sampled[0] * A, sampled[0] * A + A - 1, sampled[1] * A + A // 3,
+            sampled[1] * A + A - 1, sampled[2] * A, sampled[2] * A + A // 2,
+            sampled[2] * A + A - 2, sampled[2] * A + A - 1]
+    ag.rn_out = torch.zeros((ag.NA, 128), dtype=torch.float32, device=DEV)
+    checked = 0
+    for step in range(steps):
+        pre = None
+        if step + 1 in learn_checks:
+            src = [0] if shared else pick
+            pre = [kernel_to_keras(_rows(getattr(ag, k), src), 128)
+                   for k in ["params", "target", "adam_m", "adam_v"]]
+        tr.step()
+        outs = [lp.step() for lp in loops]
+        acts, obs, rew = (_rows(x, sampled) for x in (ag.actions, tr.obs, tr.last_reward))
+        for i, out in enumerate(outs):
+            np.testing.assert_array_equal(acts[i], out["actions"], err_msg=f"step {step} env {i}")
+            np.testing.assert_array_equal(rew[i], out["reward"], err_msg=f"step {step} env {i}")
+            np.testing.assert_array_equal(obs[i], loops[i].obs, err_msg=f"step {step} env {i}")
+        if outs[0]["idx"] is not None:
+            idx = _rows(ag.idx, arows).reshape(len(sampled), A, 128)
+            for i, out in enumerate(outs):
+                np.testing.assert_array_equal(idx[i], out["idx"], err_msg=f"step {step} env {i}")
+        if pre is not None:
+            _check_learn(tr, pick, pre, precision, shared)
+            checked += 1
+    assert checked == len(learn_checks)
+    return tr
+
+
+def test_c3_4x4x1024_fp16_full_size():
+    tr = _run_config(4, 4, 1024, "fp16", 1100, {128, 1100})
+    assert len(tr.agent.ring) == 1100 and tr.agent.ring.s.numel() > 2 ** 31
+    assert tr.episode == 4  # episode boundaries at 240, 480, 720, 960
+    del tr
+    torch.cuda.empty_cache()
+
+
+def test_c2_2x2x256_bf16_full_size():
+    tr = _run_config(2, 2, 256, "bf16", 140, {128, 140})
+    del tr
+    torch.cuda.empty_cache()
+
+
+def test_c5_8x8x256_shared_full_size():
+    tr = _run_config(8, 8, 256, "fp16", 130, {128, 130}, shared=True)
+    del tr
+    torch.cuda.empty_cache()
+
+
+def test_c1_train_py_1x1_episode(tmp_path):
+    """The drop-in src/scripts/train.py loop (DQNAgent per junction, process-
+    global streams) for one 240-step episode on a 1x1 grid vs OracleLoop with
+    learning on: per-step rewards exact, per-step loss rtol 1e-4 (fp32)."""
+    from src.agents import dqn_agent as DA
+    from src.scripts import train as T
+    seed = 3
+    mpath = os.path.join(str(tmp_path), "m.jsonl")
+    agents = T.train_agents(episodes=1, rows=1, cols=1, seed=seed, metrics=mpath)
+    recs = [json.loads(x) for x in open(mpath)]
+    assert len(recs) == 240
+    s0 = DA.init_seed(0, "J_0_0")
+    w0 = initial_weights(s0, [s0], 1, 128)  # BatchedDQN(1, 1) inside DQNAgent: env seed = seed
+    ol = O.OracleLoop(1, 1, seed, cap=10000, tuf=500, weights=w0)
+    for rec in recs:
+        out = ol.step()
+        assert rec["total_reward"] == float(out["reward"].sum())
+        if out["loss"] is None:
+            assert rec["total_loss"] == 0
+        else:
+            np.testing.assert_allclose(rec["total_loss"], float(out["loss"].sum()), rtol=1e-4)
+    assert ol.learn_steps == 240 - 127
+    got = np.concatenate([w.reshape(-1) for w in agents["J_0_0"]._core.get_weights(0)])
+    np.testing.assert_allclose(got, ol.params[0], atol=5e-5)

@@ -16,9 +16,9 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run \
     -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline "$@" > $O/keep_$TAG/bench_prof.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcF_$TAG -o run \
-    -- python3 $R/bench.py --steps 4 --warmup 1 --no-cpu-baseline "$@" > $O/pmcF_$TAG.log 2>&1
+    -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline "$@" > $O/pmcF_$TAG.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcW_$TAG -o run \
-    -- python3 $R/bench.py --steps 4 --warmup 1 --no-cpu-baseline "$@" > $O/pmcW_$TAG.log 2>&1
+    -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline "$@" > $O/pmcW_$TAG.log 2>&1
 F=$(find $O/pmcF_$TAG -name '*counter_collection.csv' | head -n 1)
 W=$(find $O/pmcW_$TAG -name '*counter_collection.csv' | head -n 1)
 cd $R
