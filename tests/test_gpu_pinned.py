@@ -123,48 +123,61 @@ def test_dropin_h16_tracks_reference(precision):
 def test_trainer_many_learns_match_oracle_loop():
     """Trainer (2x2 grid x 2 replicas, fp32) vs oracle.OracleLoop for replica 1
     over 330 steps: the ring wraps (cap 250), 203 learns per agent, 4 target
-    syncs, an episode boundary at step 240 -- never re-synced.
+    syncs, an episode boundary at step 240.  Actions, observations and replay
+    indices are bit-exact at every step.  Two oracle loops run beside it:
 
-    Each agent is compared up to its first Double-DQN near-tie: a learn whose
-    batch has two online Q(S') within 1e-5 (relative) of each other, where
-    the argmax (dqn_agent.py:342) may legitimately differ between two fp32
-    summation orders and the trajectories part (this seed: one agent at learn
-    40, relative gap 2e-7).  Before it: loss rtol 1e-4; agents that never meet
-    one: all 203 losses and the final weights (5e-5).  At least 600 of the
-    812 agent-learns must be in the compared horizon."""
+    * free (never re-synced): each agent's loss rtol 1e-4 until its first
+      Double-DQN near-tie -- a batch with two online Q(S') within 1e-5
+      (relative), where the argmax (dqn_agent.py:342) may go either way under
+      another fp32 summation order -- or learn 100, whichever comes first;
+      >= 200 agent-learns in total.  In this env the two fp32 trajectories part
+      after ~100-150 learns even without a tie (measured on the CPU between the
+      C oracle and a torch restatement: first 1e-5 difference at learns 53 / 136
+      / 151 / never), as the reference fixture's do after ~420
+      (test_learn_golden_cpu.py); the drop-in test above covers 393 un-synced
+      learns against the reference itself.
+    * forced (its weights, target and Adam slots copied from the GPU before
+      every step): every one of the 812 agent-learns rtol 1e-4 and the Adam
+      update 1e-5 -- each learn of the long run, syncs, wrap and episode
+      boundary included, is checked from the state the GPU actually had."""
     E, steps = 2, 330
     cfg = AgentConfig(precision="fp32", replay_buffer_size=250, target_update_frequency=50,
                       seed=21)
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=E, seed=40), cfg)
-    A = tr.env.A
-    w0 = tr.agent.keras_params("params")
-    ol = O.OracleLoop(2, 2, int(tr.env.seeds[1]), cap=250, tuf=50, weights=w0[A:2 * A],
-                      track_ties=True)
-    lg, lo = [], []
+    A, ag = tr.env.A, tr.agent
+    rows = slice(A, 2 * A)
+    w0 = ag.keras_params("params")[rows]
+    free = O.OracleLoop(2, 2, int(tr.env.seeds[1]), cap=250, tuf=50, weights=w0, track_ties=True)
+    forced = O.OracleLoop(2, 2, int(tr.env.seeds[1]), cap=250, tuf=50, weights=w0)
+    lg, lf, lo = [], [], []
     for t in range(steps):
+        for k in ["params", "target", "adam_m", "adam_v"]:
+            setattr(forced, k, kernel_to_keras(getattr(ag, k)[rows].cpu().numpy(), 128))
+        forced.learn_steps = ag.learn_step_counter
         tr.step()
-        out = ol.step()
-        np.testing.assert_array_equal(tr.agent.actions[1].cpu().numpy(), out["actions"])
-        np.testing.assert_array_equal(tr.obs[1].cpu().numpy(), ol.obs)
+        out, outf = free.step(), forced.step()
+        np.testing.assert_array_equal(ag.actions[1].cpu().numpy(), out["actions"])
+        np.testing.assert_array_equal(tr.obs[1].cpu().numpy(), free.obs)
         if out["idx"] is not None:
-            np.testing.assert_array_equal(tr.agent.idx[A:2 * A].cpu().numpy(), out["idx"])
-            lg.append(tr.last_loss[A:2 * A].cpu().numpy())
+            np.testing.assert_array_equal(ag.idx[rows].cpu().numpy(), out["idx"])
+            lg.append(tr.last_loss[rows].cpu().numpy())
             lo.append(out["loss"])
-    lg, lo = np.array(lg), np.array(lo)
+            lf.append(outf["loss"])
+            np.testing.assert_allclose(ag.keras_params("params")[rows], forced.params, atol=1e-5,
+                                       err_msg=f"forced step {t}")
+    lg, lo, lf = np.array(lg), np.array(lo), np.array(lf)
     assert lg.shape == (203, A)
-    gaps = np.array(ol.tie_gaps)
-    tied = gaps < 1e-5
-    horizon = [int(np.argmax(tied[:, j])) if tied[:, j].any() else len(lg) for j in range(A)]
+    np.testing.assert_allclose(lg, lf, rtol=1e-4)
+    tied = np.array(free.tie_gaps) < 1e-5
+    horizon = [min(100, int(np.argmax(tied[:, j])) if tied[:, j].any() else len(lg))
+               for j in range(A)]
     rel = np.abs(lg - lo) / np.abs(lo)
-    print(f"trainer vs oracle loop: near-tie horizons {horizon}; loss rel err inside them "
-          f"max {max(rel[:h, j].max() for j, h in enumerate(horizon) if h):.3g}")
-    assert sum(horizon) >= 600
-    p_g, t_g = tr.agent.keras_params("params")[A:2 * A], tr.agent.keras_params("target")[A:2 * A]
+    print(f"trainer vs oracle loop: un-synced horizons {horizon}, loss rel err inside max "
+          f"{max(rel[:h, j].max() for j, h in enumerate(horizon) if h):.3g}; forced max "
+          f"{(np.abs(lg - lf) / np.abs(lf)).max():.3g}")
+    assert sum(horizon) >= 200
     for j, h in enumerate(horizon):
         np.testing.assert_allclose(lg[:h, j], lo[:h, j], rtol=1e-4, err_msg=f"agent {j}")
-        if h == len(lg):
-            np.testing.assert_allclose(p_g[j], ol.params[j], atol=5e-5)
-            np.testing.assert_allclose(t_g[j], ol.target[j], atol=5e-5)
 
 
 # ---------------------------------------------------------------------------
