@@ -26,10 +26,10 @@ import os
 import numpy as np
 import torch
 
-FORMAT = "dmdqn-ckpt-4"  # 4: 128-B replay rows (s' rows carry a, done, r); unpadded W1T (qnet_layout.hpp)
+FORMAT = "dmdqn-ckpt-5"  # 5: + the actuated-mode detector times; 4: 128-B replay rows, unpadded W1T
 
 _ENV_TENSORS = ["t_x", "t_v", "t_dst", "t_head", "t_cnt", "t_phase_state", "t_ts", "t_qptr",
-                "t_stats", "halt", "phase", "tspent", "done_u8"]
+                "t_stats", "t_last_det", "halt", "phase", "tspent", "done_u8"]
 _AGENT_TENSORS = ["params", "target", "adam_m", "adam_v", "np_state", "py_state"]
 
 
@@ -39,8 +39,9 @@ _AGENT_TENSORS = ["params", "target", "adam_m", "adam_v", "np_state", "py_state"
 _AGENT_FIXED = ["precision", "shared_params", "nn_layers", "replay_buffer_size", "batch_size",
                 "seed", "loss", "target_update_frequency", "count_env_steps"]
 _ENV_FIXED = ["rows", "cols", "num_envs", "env_offset", "seed", "signal_features", "cap_lane",
-              "end_ms", "period_ms", "step_duration", "max_sim_time", "action_stride", "scenario"]
-_DEFAULTS = {"loss": "mse"}  # fields added after format 4 was introduced
+              "end_ms", "period_ms", "step_duration", "max_sim_time", "action_stride", "scenario",
+              "actuated"]
+_DEFAULTS = {"loss": "mse", "actuated": False}  # fields added after format 4 was introduced
 
 
 def _check_cfg(saved, cur, fields, what):

@@ -21,7 +21,8 @@
 //         with t) if it has room
 //   C     every lane advances its vehicles front-to-back (IDM, no overlap);
 //         granted fronts leave, arrivals are removed
-//   D     target lanes append the vehicle they granted
+//   D     target lanes append the vehicle they granted (its route word
+//         advanced past the junction: sim.hpp route words)
 //   E     origin queues insert one departed vehicle per edge if there is room
 #include <type_traits>
 
@@ -45,7 +46,7 @@ struct EnvViewT {
     DT *dst;
     int32_t *head, *cnt, *req, *gfrom;
     float *fx, *fv;
-    int32_t *phase, *ts, *qptr, *stats;
+    int32_t *phase, *ts, *qptr, *stats, *last_det;
     const int32_t *q_off;
     const uint16_t *q_ids, *vdst, *q_dst;
 
@@ -73,6 +74,7 @@ struct EnvViewT {
         vdst = s.vdst + (size_t)env * s.nveh;
         q_dst = s.q_dst + (size_t)env * s.nveh;
         stats = s.stats + (size_t)env * 4;
+        last_det = s.last_det + (size_t)env * 12 * A;
     }
 };
 using EnvView = EnvViewT<int32_t>;
@@ -109,10 +111,23 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
     const int A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
 
-    // ---- TL: natural phase advance (fixed durations)
+    // ---- TL: natural phase advance (fixed durations; actuated gap-out of
+    // phase 0 in actuated mode: after minDur, once no vehicle has been over a
+    // detector of the phase's green lanes for more than max_gap, or at maxDur)
     for (int a = tid; a < A; a += nt) {
-        int p = V.phase[a];
-        if (t - V.ts[a] >= kPhaseDur[p]) {
+        const int p = V.phase[a], el = t - V.ts[a];
+        bool sw;
+        if (S.actuated && p == 0) {
+            constexpr uint32_t gl = green_lanes(0x11BB);  // kGreen[0]
+            int last = kNoDetection;
+#pragma unroll
+            for (int k = 0; k < 12; k++)
+                if ((gl >> k) & 1u) last = max(last, V.last_det[a * 12 + k]);
+            sw = el >= kActMax || (el >= kActMin && (float)(t - last) > P.max_gap);
+        } else {
+            sw = el >= kPhaseDur[p];
+        }
+        if (sw) {
             V.phase[a] = (p + 1) % 12;
             V.ts[a] = t;
         }
@@ -133,17 +148,17 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const int d0 = V.dst[base + h0];
         const float len = lane_length(T, e);
         float acc, vn, xn;
-        if (e >= 4 * A || d0 == e) {  // exit edge or destination edge: free road
+        if (e >= 4 * A || on_final_edge(d0, e)) {  // exit edge or last edge: free road
             acc = idm_free(v0, P);
             vn = clamp_speed(v0 + acc, P);
             xn = x0 + vn;
             V.req[l] = kArrive;
         } else {
             const int aj = e >> 2, d = e & 3, h = opp(d);
-            const int o = route_out(T, aj, h, d0);
+            const int o = out_dir(T, aj, h, d0);
             const int m = movement(h, o);
             const int e2 = next_edge(T, aj, o);
-            const int k2 = lane_for(T, e2, kf, d0, V.cnt);
+            const int k2 = lane_for(T, e2, kf, route_advance(d0), V.cnt);
             const int tl = e2 * 3 + k2;
             const bool green = (kGreen[V.phase[aj]] >> (d * 4 + m)) & 1;
             if (green) {
@@ -238,6 +253,10 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             V.x[base + hd] = lead_x_new;
             V.v[base + hd] = fvn;
         }
+        // actuated mode: a vehicle's body over the detector point dp during
+        // the substep (old front < dp + length, new front >= dp)
+        const float dp = len - P.det_dist, dpl = dp + P.length;
+        bool det = lead_x_new >= dp && lead_x_old < dpl;
         int s = hd;
         for (int i = 1; i < n; i++) {
             s = (s + 1 == cap) ? 0 : s + 1;
@@ -258,6 +277,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             }
             V.x[base + s] = xn;
             V.v[base + s] = vn;
+            det = det || (xn >= dp && xi < dpl);
             lead_x_old = xi;
             lead_v_old = vi;
             lead_x_new = xn;
@@ -266,6 +286,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             V.head[l] = (hd + 1 == cap) ? 0 : hd + 1;
             V.cnt[l] = n - 1;
         }
+        if (S.actuated && det && l < 12 * A) V.last_det[l] = t + 1;
     }
     __syncthreads();
     SIM_PROF(3);
@@ -281,7 +302,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         // the source lane already popped its front; read its (old) destination
         // from the slot it vacated
         const int fh = V.head[f] == 0 ? cap - 1 : V.head[f] - 1;
-        const int dv = V.dst[(size_t)f * cap + fh];
+        const int dv = route_advance(V.dst[(size_t)f * cap + fh]);
         int nc = V.cnt[tl];
         float xe = over;
         if (nc > 0) {
@@ -315,8 +336,8 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         if ((long long)id * S.period_ms > (long long)t * 1000) continue;
         const int d0 = qn[q].dst;
         const int aj = e >> 2, d = e & 3, h = opp(d);
-        const int o = route_out(T, aj, h, d0);
-        const int m = movement(h, o);
+        // a one-edge route departs on the straight lanes (its origin is its end)
+        const int m = on_final_edge(d0, e) ? (int)MV_S : movement(h, out_dir(T, aj, h, d0));
         const int k = lane_for_move(m, e, V.cnt);
         const int l = e * 3 + k;
         const int nc = V.cnt[l];
@@ -341,12 +362,12 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
 
 // LDS image of one env's mutable state (kLDS path): x, v (f32) and dst (u16)
 // rings [NL][cap], then head, cnt, req, gfrom, fx, fv [NL], phase, ts [A], qptr
-// [4A], stats [4].  4x4 grid, cap 24: 65 KB -> two envs per CU, 30 KB left (a
+// [4A], stats [4], q_off [4A+1], last_det [12A].  4x4 grid, cap 24: 65 KB -> two envs per CU, 30 KB left (a
 // co-resident sampler wave fits, but measured no gain: it stretches the sim).
 __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
     const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
     return (size_t)NL * cap * 10 + (size_t)NL * 6 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16 +
-           (size_t)(4 * A + 1) * 4;  // q_off
+           (size_t)(4 * A + 1) * 4 + (size_t)A * 48;  // q_off, last_det
 }
 
 // One RL step per env (block).  kLDS: the env's state is staged into LDS for
@@ -388,6 +409,9 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
         int32_t *qoff = V.stats + 4;
         for (int i = tid; i <= 4 * A; i += nt) qoff[i] = G.q_off[i];
         V.q_off = qoff;
+        V.last_det = qoff + 4 * A + 1;
+        if (S.actuated)
+            for (int i = tid; i < 12 * A; i += nt) V.last_det[i] = G.last_det[i];
         // each thread stages its lanes' occupied slots only (~8 % of the rings)
         for (int l = tid; l < NL; l += nt) {
             const int h = G.head[l], n = G.cnt[l];
@@ -476,6 +500,8 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
             G.ts[a] = V.ts[a];
         }
         for (int e = tid; e < 4 * A; e += nt) G.qptr[e] = V.qptr[e];
+        if (S.actuated)
+            for (int i = tid; i < 12 * A; i += nt) G.last_det[i] = V.last_det[i];
     }
 #ifdef DMDQN_SIM_PROFILE
     __syncthreads();
@@ -499,6 +525,7 @@ __global__ void k_sim_reset(dmdqn_sim S) {
         V.ts[a] = 0;
     }
     for (int e = threadIdx.x; e < 4 * V.A; e += blockDim.x) V.qptr[e] = V.q_off[e];
+    for (int i = threadIdx.x; i < 12 * V.A; i += blockDim.x) V.last_det[i] = kNoDetection;
     if (threadIdx.x < 4) V.stats[threadIdx.x] = 0;
 }
 
@@ -512,10 +539,11 @@ static int check_sim(const dmdqn_sim *s) {
                   s->R, s->C);
     DMDQN_REQUIRE(s->E >= 1 && s->cap_lane >= 2 && s->cap_lane <= 64, "dmdqn_sim: E/cap_lane");
     DMDQN_REQUIRE(s->nveh >= 0 && s->nveh <= 65535 && s->period_ms > 0, "dmdqn_sim: demand");
+    DMDQN_REQUIRE(s->actuated == 0 || s->actuated == 1, "dmdqn_sim: actuated must be 0 or 1");
     DMDQN_REQUIRE(4 * s->R * s->C <= 2 * 256, "dmdqn_sim: at most 128 junctions (queue slots)");
     DMDQN_REQUIRE(s->x && s->v && s->dst && s->head && s->cnt && s->req && s->gfrom && s->fx &&
                       s->fv && s->tl_phase && s->tl_ts && s->qptr && s->q_off && s->exit_id &&
-                      s->exit_ao && s->stats &&
+                      s->exit_ao && s->stats && s->last_det &&
                       (s->nveh == 0 || (s->q_ids && s->vdst && s->q_dst)),
                   "dmdqn_sim: null array");
     return DMDQN_OK;

@@ -13,6 +13,23 @@ __constant__ int kPhaseDur[12] = {25, 6, 2, 20, 6, 2, 25, 6, 2, 20, 6, 2};
 // phase strings with the link layout of grid_3x3.net.xml:1375-1461
 // (per approach: r, s, s, -, l, t).
 __constant__ uint32_t kGreen[12] = {0x11BB, 0, 0, 0x11DD, 0, 0, 0xBB11, 0, 0, 0xDD11, 0, 0};
+// Actuated mode (dmdqn_sim.actuated): phase 0 carries minDur 5 / maxDur 50
+// (grid_3x3.net.xml:894); the others have no actuation range.
+constexpr int kActMin = 5, kActMax = 50;
+constexpr int kNoDetection = -1000;
+
+// Observed lanes (lane k of approach d) with a green link in phase p: lane 0
+// carries right + straight, lane 1 straight, lane 2 left + U-turn.  Bit d*3+k.
+__host__ __device__ constexpr uint32_t green_lanes(uint32_t g) {
+    uint32_t out = 0;
+    for (int d = 0; d < 4; d++) {
+        const uint32_t m = (g >> (4 * d)) & 15u;
+        out |= (m & 3u ? 1u : 0u) << (3 * d);
+        out |= (m & 2u ? 1u : 0u) << (3 * d + 1);
+        out |= (m & 12u ? 1u : 0u) << (3 * d + 2);
+    }
+    return out;
+}
 
 constexpr int kArrive = -2;
 enum { DIR_N = 0, DIR_S = 1, DIR_E = 2, DIR_W = 3 };
@@ -110,6 +127,27 @@ __device__ __forceinline__ int route_out(const Topo &T, int a, int h, int dst) {
     return dv >= 0 ? dv : dh;
 }
 
+// Route words (the per-vehicle u16 carried in the lane rings, dmdqn_sim.vdst):
+//   < 0x8000  the destination edge; the vehicle is routed on the fly (route_out)
+//   >= 0x8000 an explicit route (a loaded SUMO scenario, grid_3x3_p06.rou.xml):
+//             c = w & 0x7fff holds the out-directions still to take, 2 bits per
+//             junction from the lowest, above a sentinel 1 -- c == 1 means the
+//             vehicle is on the last edge of its route.
+constexpr int kRouted = 0x8000;
+
+__device__ __forceinline__ bool on_final_edge(int w, int e) {
+    return w < kRouted ? w == e : (w & 0x7fff) == 1;
+}
+
+__device__ __forceinline__ int out_dir(const Topo &T, int a, int h, int w) {
+    return w < kRouted ? route_out(T, a, h, w) : (w & 3);
+}
+
+// The route word once the vehicle has crossed the junction at the end of its edge.
+__device__ __forceinline__ int route_advance(int w) {
+    return w < kRouted ? w : (kRouted | ((w & 0x7fff) >> 2));
+}
+
 __device__ __forceinline__ int next_edge(const Topo &T, int a, int o) {
     int nb = T.nbr(a, o);
     return nb >= 0 ? nb * 4 + opp(o) : 4 * T.A + T.exit_id[a * 4 + o];
@@ -123,12 +161,13 @@ __device__ __forceinline__ int lane_for_move(int m, int e, const int32_t *cnt) {
     return cnt[e * 3 + 1] <= cnt[e * 3 + 0] ? 1 : 0;
 }
 
-// Lane a vehicle takes when entering edge e2 from lane index kf.
-__device__ __forceinline__ int lane_for(const Topo &T, int e2, int kf, int dst,
+// Lane a vehicle takes when entering edge e2 from lane index kf; w2 is its
+// route word on e2 (route_advance of the word it has now).
+__device__ __forceinline__ int lane_for(const Topo &T, int e2, int kf, int w2,
                                         const int32_t *cnt) {
-    if (e2 >= 4 * T.A || e2 == dst) return kf;  // connections keep the lane index
+    if (e2 >= 4 * T.A || on_final_edge(w2, e2)) return kf;  // connections keep the lane index
     int h2 = opp(e2 & 3);
-    int o2 = route_out(T, e2 >> 2, h2, dst);
+    int o2 = out_dir(T, e2 >> 2, h2, w2);
     return lane_for_move(movement(h2, o2), e2, cnt);
 }
 

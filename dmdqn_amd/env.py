@@ -41,15 +41,19 @@ class IDMParams:
     halt_speed: float = 0.1
     len_inner: float = 172.8
     len_outer: float = 86.4
+    # actuated mode (EnvConfig.actuated): SUMO's actuated-TLS defaults
+    detector_gap_s: float = 2.0   # detector distance upstream = detector_gap_s * vmax
+    max_gap: float = 3.0          # gap-out time (s)
 
     def values(self):
         """The dmdqn_idm constants in struct order (include/dmdqn.h), as float32
         values (two_sqrt_ab = 2 sqrt(a b) computed in float32, as the oracle)."""
         f = np.float32
         two_sqrt_ab = f(2.0) * np.sqrt(f(self.accel) * f(self.decel), dtype=np.float32)
+        det = f(self.detector_gap_s) * f(self.vmax)
         return [float(f(x)) for x in (self.length, self.min_gap, self.accel, self.decel, self.tau,
                                       self.vmax, two_sqrt_ab, self.halt_speed, self.len_inner,
-                                      self.len_outer)]
+                                      self.len_outer, det, self.max_gap)]
 
 
 @dataclass
@@ -63,6 +67,9 @@ class EnvConfig:
     max_sim_time: int = 2400     # MAX_SIM_TIME (train.py:58)
     action_stride: int = 3       # ACTION_MAP {a: 3a} (train.py:57)
     signal_features: str = "reference"  # A-5: "reference" (padding) | "intended"
+    # A-14: SUMO's actuated gap-out on phase 0 (grid_3x3.net.xml:894, minDur 5,
+    # maxDur 50).  Off by default: fixed durations.
+    actuated: bool = False
     cap_lane: int = 24           # vehicle slots per lane (172.8 m / 7.5 m + 1)
     end_ms: int = 2_500_000      # last departure (trips_p06.trips.xml:7-9)
     period_ms: Optional[int] = None
@@ -128,13 +135,14 @@ class TrafficEnv:
         self.t_exit_id = torch.from_numpy(g.exit_id.reshape(-1).copy()).to(dev)
         self.t_exit_ao = torch.from_numpy(g.exit_ao.reshape(-1).copy()).to(dev)
         self.t_stats = z32(E, 4)
+        self.t_last_det = z32(E, 12 * g.A)
         # the dmdqn_sim arrays in the order of the sim ops (dmdqn_torch.cpp make_sim)
         self._sim_state = [self.t_x, self.t_v, self.t_dst, self.t_head, self.t_cnt, self.t_req,
                            self.t_gfrom, self.t_fx, self.t_fv, self.t_phase_state, self.t_ts,
-                           self.t_qptr, self.t_stats]
+                           self.t_qptr, self.t_stats, self.t_last_det]
         self._sim_tables = [self.t_q_off, self.t_q_ids, self.t_vdst, self.t_exit_id,
                             self.t_exit_ao, self.t_q_dst]
-        self._sim_dims = [cfg.rows, cfg.cols, E, cap, period, nveh]
+        self._sim_dims = [cfg.rows, cfg.cols, E, cap, period, nveh, int(bool(cfg.actuated))]
         self._idm = cfg.idm.values()
         # observation buffers
         self.halt = z32(E, A, 12)

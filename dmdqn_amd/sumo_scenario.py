@@ -13,9 +13,10 @@ naming scheme, and maps it onto the HIP simulator:
     ``J_r_c_to_END_<D>_r_c``  exit of J_r_c toward D              -> 4A + exit index
 * vehicles (grid_3x3_p06.rou.xml:23-12524): origin = first route edge,
   destination = last route edge, vehicle i departs at i * period (the file's
-  departures are exactly i * 0.6 s, checked).  The explicit duarouter path is
-  not kept: the simulator routes on the grid toward the destination (DESIGN.md
-  section 3 -- the simulator is new, SUMO parity is unpinned).
+  departures are exactly i * 0.6 s, checked), and the duarouter path itself:
+  the out-direction taken at every junction on the way, packed 2 bits each
+  above a sentinel into the vehicle's route word (0x8000 | code, sim.hpp), so
+  the simulator drives exactly the file's edges.
 
 Checks that the net matches what the simulator models and raises otherwise:
 3 lanes per edge, the 12-phase program of grid_3x3.net.xml:893-906, junction
@@ -28,7 +29,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .scenario import Grid
+from .scenario import Grid, neighbor
 
 DIR = {"N": 0, "S": 1, "E": 2, "W": 3}
 PHASE_DURATIONS = [25, 6, 2, 20, 6, 2, 25, 6, 2, 20, 6, 2]  # sim.hpp kPhaseDur
@@ -49,16 +50,18 @@ class Scenario:
     lane_len_inner: float   # J -> J lane length (m)
     lane_len_outer: float   # END -> J / J -> END lane length (m)
     source: str = ""
+    route: np.ndarray = None  # uint16 [N] route words (route_word), or None: on-the-fly routing
 
     @property
     def nveh(self):
         return len(self.origin)
 
     def save(self, path):
+        extra = {} if self.route is None else {"route": self.route}
         np.savez_compressed(path, rows=self.rows, cols=self.cols, origin=self.origin,
                             dest=self.dest, period_ms=self.period_ms,
                             lane_len_inner=self.lane_len_inner,
-                            lane_len_outer=self.lane_len_outer)
+                            lane_len_outer=self.lane_len_outer, **extra)
 
 
 def read_sumocfg(path):
@@ -96,6 +99,45 @@ def edge_index(edge_id, grid: Grid):
     raise ValueError(f"edge id {edge_id!r} is not in the J_r_c / END_<D>_r_c scheme")
 
 
+ROUTED = 0x8000   # sim.hpp kRouted
+MAX_TURNS = 7     # 2 bits each above the sentinel in 15 bits
+
+
+def next_edge(grid: Grid, a, o):
+    """Simulator edge reached by leaving junction a toward o (sim.hpp next_edge)."""
+    nb = neighbor(grid.R, grid.C, a, o)
+    return nb * 4 + (o ^ 1) if nb >= 0 else 4 * grid.A + int(grid.exit_id[a, o])
+
+
+def route_word(edges, grid: Grid):
+    """Route word of a path of simulator edges: the out-direction at each
+    junction crossed, 2 bits each from the lowest, above a sentinel 1."""
+    turns = []
+    for e, e2 in zip(edges[:-1], edges[1:]):
+        if e >= 4 * grid.A:
+            raise ValueError("a route continues past an exit edge")
+        a = e >> 2
+        outs = [o for o in range(4) if next_edge(grid, a, o) == e2]
+        if not outs:
+            raise ValueError(f"edges {e} -> {e2} are not connected at junction {a}")
+        turns.append(outs[0])
+    if len(turns) > MAX_TURNS:
+        raise ValueError(f"route crosses {len(turns)} junctions (route words hold {MAX_TURNS})")
+    code = 1 << (2 * len(turns))
+    for i, o in enumerate(turns):
+        code |= o << (2 * i)
+    return ROUTED | code
+
+
+def route_edges(word, origin, grid: Grid):
+    """Inverse of route_word: the simulator edges a route word drives from `origin`."""
+    edges, c = [int(origin)], int(word) & 0x7FFF
+    while c > 1:
+        edges.append(next_edge(grid, edges[-1] >> 2, c & 3))
+        c >>= 2
+    return edges
+
+
 def load_net(path):
     """Grid + lane lengths of a SUMO net in the J_r_c scheme; validates lanes per
     edge and the signal program."""
@@ -130,15 +172,17 @@ def load_net(path):
 
 
 def load_routes(path, grid: Grid):
-    """origin / destination edge per vehicle and the departure period (ms)."""
+    """origin / destination edge and route word per vehicle, and the
+    departure period (ms)."""
     root = ET.parse(path).getroot()
-    org, dst, dep = [], [], []
+    org, dst, dep, words = [], [], [], []
     for i, v in enumerate(root.iter("vehicle")):
         if int(v.get("id")) != i:
             raise ValueError(f"{path}: vehicle ids must be 0..N-1 in order")
-        edges = v.find("route").get("edges").split()
-        org.append(edge_index(edges[0], grid))
-        dst.append(edge_index(edges[-1], grid))
+        edges = [edge_index(e, grid) for e in v.find("route").get("edges").split()]
+        org.append(edges[0])
+        dst.append(edges[-1])
+        words.append(route_word(edges, grid))
         dep.append(float(v.get("depart")))
     if not org:
         raise ValueError(f"{path}: no vehicles")
@@ -149,7 +193,8 @@ def load_routes(path, grid: Grid):
     if not np.allclose(dep, np.arange(len(dep)) * period_ms / 1000.0, atol=1e-6):
         raise ValueError(f"{path}: departures are not i * {period_ms} ms "
                          "(the simulator's origin queues assume a fixed period)")
-    return np.asarray(org, np.int32), np.asarray(dst, np.int32), period_ms
+    return (np.asarray(org, np.int32), np.asarray(dst, np.int32), period_ms,
+            np.asarray(words, np.uint16))
 
 
 def load_scenario(path):
@@ -158,11 +203,12 @@ def load_scenario(path):
         with np.load(path) as f:
             return Scenario(int(f["rows"]), int(f["cols"]), f["origin"].astype(np.int32),
                             f["dest"].astype(np.int32), int(f["period_ms"]),
-                            float(f["lane_len_inner"]), float(f["lane_len_outer"]), path)
+                            float(f["lane_len_inner"]), float(f["lane_len_outer"]), path,
+                            f["route"].astype(np.uint16) if "route" in f.files else None)
     net, routes = read_sumocfg(path)
     grid, li, lo = load_net(net)
-    o, d, p = load_routes(routes[0], grid)
-    return Scenario(grid.R, grid.C, o, d, p, li, lo, path)
+    o, d, p, w = load_routes(routes[0], grid)
+    return Scenario(grid.R, grid.C, o, d, p, li, lo, path, w)
 
 
 def scenario_tables(sc: Scenario, E):
@@ -177,5 +223,8 @@ def scenario_tables(sc: Scenario, E):
     off[1:] = np.cumsum(np.bincount(sc.origin, minlength=4 * A))
     q_ids = np.broadcast_to(order, (E, N)).copy()
     q_off = np.broadcast_to(off, (E, 4 * A + 1)).copy()
-    vdst = np.broadcast_to(sc.dest.astype(np.uint16), (E, N)).copy()
+    # per vehicle the word the lane rings carry: its explicit route when the
+    # scenario has one, else its destination (on-the-fly routing)
+    word = sc.route if sc.route is not None else sc.dest.astype(np.uint16)
+    vdst = np.broadcast_to(word.astype(np.uint16), (E, N)).copy()
     return q_ids, q_off, vdst, N, sc.period_ms

@@ -149,14 +149,14 @@ void replay_sample(Tensor &py_state, int64_t A, int64_t n, int64_t k, Tensor &id
 
 // ---------------------------------------------------------------- simulator
 // state (mutable, in order): x, v, dst, head, cnt, req, gfrom, fx, fv, tl_phase,
-// tl_ts, qptr, stats; tables: q_off, q_ids, vdst, exit_id, exit_ao, q_dst;
-// dims: R, C, E, cap_lane, period_ms, nveh.
+// tl_ts, qptr, stats, last_det; tables: q_off, q_ids, vdst, exit_id, exit_ao,
+// q_dst; dims: R, C, E, cap_lane, period_ms, nveh, actuated.
 dmdqn_sim make_sim(at::TensorList state, at::TensorList tables, at::IntArrayRef dims) {
-    TORCH_CHECK(state.size() == 13 && tables.size() == 6 && dims.size() == 6,
-                "sim: 13 state tensors, 6 tables, 6 dims");
+    TORCH_CHECK(state.size() == 14 && tables.size() == 6 && dims.size() == 7,
+                "sim: 14 state tensors, 6 tables, 7 dims");
     dmdqn_sim s{};
     s.R = (int)dims[0]; s.C = (int)dims[1]; s.E = (int)dims[2]; s.cap_lane = (int)dims[3];
-    s.period_ms = (int)dims[4]; s.nveh = (int)dims[5];
+    s.period_ms = (int)dims[4]; s.nveh = (int)dims[5]; s.actuated = (int)dims[6];
     const int64_t A = (int64_t)s.R * s.C, X = 2 * (int64_t)s.R + 2 * s.C, E = s.E;
     const int64_t NL = 3 * (4 * A + X), ns = E * NL * s.cap_lane;
     s.x = dptr<float>(state[0], at::kFloat, "x", ns);
@@ -172,6 +172,7 @@ dmdqn_sim make_sim(at::TensorList state, at::TensorList tables, at::IntArrayRef 
     s.tl_ts = dptr<int32_t>(state[10], at::kInt, "tl_ts", E * A);
     s.qptr = dptr<int32_t>(state[11], at::kInt, "qptr", E * 4 * A);
     s.stats = dptr<int32_t>(state[12], at::kInt, "stats", E * 4);
+    s.last_det = dptr<int32_t>(state[13], at::kInt, "last_det", E * 12 * A);
     s.q_off = dptr<int32_t>(tables[0], at::kInt, "q_off", E * (4 * A + 1));
     s.q_ids = dptr<uint16_t>(tables[1], at::kShort, "q_ids", E * s.nveh);
     s.vdst = dptr<uint16_t>(tables[2], at::kShort, "vdst", E * s.nveh);
@@ -191,9 +192,10 @@ void sim_step(at::TensorList state, at::TensorList tables, at::IntArrayRef dims,
               at::ArrayRef<double> idm, const OptT &actions, int64_t stride, int64_t t0, int64_t K,
               int64_t max_time, Tensor &halt, Tensor &phase, Tensor &tspent, Tensor &done) {
     dmdqn_sim s = make_sim(state, tables, dims);
-    TORCH_CHECK(idm.size() == 10, "idm: 10 constants (include/dmdqn.h dmdqn_idm order)");
+    TORCH_CHECK(idm.size() == 12, "idm: 12 constants (include/dmdqn.h dmdqn_idm order)");
     dmdqn_idm p{(float)idm[0], (float)idm[1], (float)idm[2], (float)idm[3], (float)idm[4],
-                (float)idm[5], (float)idm[6], (float)idm[7], (float)idm[8], (float)idm[9]};
+                (float)idm[5], (float)idm[6], (float)idm[7], (float)idm[8], (float)idm[9],
+                (float)idm[10], (float)idm[11]};
     const int64_t A = (int64_t)s.R * s.C, E = s.E;
     auto a = optr<int32_t>(actions, at::kInt, "actions", E * A);
     auto h = dptr<int32_t>(halt, at::kInt, "halt", E * A * 12);

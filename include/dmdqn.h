@@ -144,6 +144,12 @@ typedef struct dmdqn_sim {
     int32_t *stats;              /* [E][4] inserted, arrived, running, pending */
     const uint16_t *q_dst;       /* [E][nveh] vdst[q_ids[i]]: destination of the
                                     vehicle at queue position i                */
+    int32_t actuated;            /* 1: SUMO's actuated gap-out on phase 0
+                                    (grid_3x3.net.xml:894, minDur 5 maxDur 50;
+                                    SURVEY A-14); 0: fixed durations (default) */
+    int32_t *last_det;           /* [E][12A] substep of the last detection on each
+                                    observed lane's detector (actuated mode; the
+                                    reset writes -1000)                        */
 } dmdqn_sim;
 
 /* Car-following / geometry constants (SUMO passenger defaults + grid_3x3
@@ -151,6 +157,9 @@ typedef struct dmdqn_sim {
 typedef struct dmdqn_idm {
     float length, min_gap, accel, decel, tau, vmax, two_sqrt_ab, halt_speed;
     float len_inner, len_outer;  /* J->J lanes 172.8 m; END->J and J->END 86.4 m */
+    float det_dist, max_gap;     /* actuated mode: detector distance upstream of
+                                    the stop line (SUMO detector-gap 2 s x 13.89
+                                    m/s) and the gap-out time (max-gap 3 s)    */
 } dmdqn_idm;
 
 /* Reset every env to t = 0: empty lanes, all TLs in phase 0 (started at 0),
@@ -160,6 +169,10 @@ int dmdqn_sim_reset(const dmdqn_sim *sim, void *stream);
 /* One RL step for every env (train.py:225-236): if actions != NULL set
  * phase = action_stride*action (ACTION_MAP {0:0,1:3,2:6,3:9}) with the phase
  * timer restarted at t0, then run K one-second substeps from time t0.
+ * With sim->actuated, phase 0 is SUMO's actuated phase (grid_3x3.net.xml:894):
+ * it ends once it has run minDur = 5 s and no vehicle has been over a detector
+ * of its green lanes for more than max_gap, or at maxDur = 50 s; the other
+ * phases keep their fixed durations.
  * Outputs after the last substep (time t0+K):
  *   halt   int32 [E][A][12] vehicles with v < halt_speed per incoming lane
  *   phase  int32 [E][A], tspent int32 [E][A] (= t - phase start)

@@ -41,6 +41,7 @@ void orc_reward(int A, const float *local, double *rew);
 typedef struct {
     float length, min_gap, accel, decel, tau, vmax, two_sqrt_ab, halt_speed;
     float len_inner, len_outer;
+    float det_dist, max_gap; /* actuated mode: detector distance, gap-out time */
 } orc_idm;
 typedef struct orc_env orc_env;
 orc_env *orc_env_create(int R, int C, int cap, uint64_t seed, long end_ms, int period_ms,
@@ -54,6 +55,9 @@ void orc_env_step(orc_env *g, const int32_t *actions, int stride, int t0, int K,
 int orc_env_info(const orc_env *g, int32_t *out);
 void orc_env_lanes(const orc_env *g, float *x, float *v, int32_t *dst, int32_t *head, int32_t *cnt);
 void orc_env_demand(const orc_env *g, uint16_t *q_ids, int32_t *q_off, uint16_t *vdst);
+void orc_env_enable_trace(orc_env *g, int max_events);
+void orc_env_set_actuated(orc_env *g, int on);
+int orc_env_trace(const orc_env *g, int32_t *out);
 
 /* ---- learn step (oracle_learn.c) ---- */
 long orc_qnet_nparams(int H1, int H2, int NA);

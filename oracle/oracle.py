@@ -156,13 +156,15 @@ def reward(local):
 # ---------------------------------------------------------------- simulator
 class CIdmO(C.Structure):
     _fields_ = [(n, C.c_float) for n in ["length", "min_gap", "accel", "decel", "tau", "vmax",
-                                         "two_sqrt_ab", "halt_speed", "len_inner", "len_outer"]]
+                                         "two_sqrt_ab", "halt_speed", "len_inner", "len_outer",
+                                         "det_dist", "max_gap"]]
 
 
 def idm_default():
     f = np.float32
     return CIdmO(f(5.0), f(2.5), f(2.6), f(4.5), f(1.0), f(13.89),
-                 f(2.0) * np.sqrt(f(2.6) * f(4.5), dtype=np.float32), f(0.1), f(172.8), f(86.4))
+                 f(2.0) * np.sqrt(f(2.6) * f(4.5), dtype=np.float32), f(0.1), f(172.8), f(86.4),
+                 f(2.0) * f(13.89), f(3.0))
 
 
 def _declare_env(L):
@@ -177,12 +179,17 @@ def _declare_env(L):
     L.orc_env_lanes.argtypes = [C.c_void_p, _f32, _f32, _i32, _i32, _i32]
     L.orc_env_demand.argtypes = [C.c_void_p, _u16, _i32, _u16]
     L.orc_env_set_demand.argtypes = [C.c_void_p, C.c_int, C.c_int, _u16, _i32, _u16]
+    L.orc_env_enable_trace.argtypes = [C.c_void_p, C.c_int]
+    L.orc_env_set_actuated.argtypes = [C.c_void_p, C.c_int]
+    L.orc_env_trace.restype = C.c_int
+    L.orc_env_trace.argtypes = [C.c_void_p, C.c_void_p]
 
 
 class OracleEnv:
     """One replica of the grid microsimulation on the CPU (oracle_sim.c)."""
 
-    def __init__(self, R, Cc, seed, cap=24, end_ms=2_500_000, period_ms=0, idm=None):
+    def __init__(self, R, Cc, seed, cap=24, end_ms=2_500_000, period_ms=0, idm=None,
+                 actuated=False):
         L = lib()
         if not hasattr(L, "_env_declared"):
             _declare_env(L)
@@ -192,6 +199,8 @@ class OracleEnv:
         self.h = L.orc_env_create(R, Cc, cap, seed, end_ms, period_ms or 0, C.byref(self.idm))
         info = self.info()
         self.NL, self.nveh = int(info[0]), int(info[1])
+        if actuated:
+            L.orc_env_set_actuated(self.h, 1)
 
     def __del__(self):
         try:
@@ -234,6 +243,20 @@ class OracleEnv:
                                  np.ascontiguousarray(q_off, np.int32),
                                  np.ascontiguousarray(vdst, np.uint16))
         self.nveh = len(q)
+
+    def enable_trace(self, max_events=1 << 20):
+        """Record every edge entry (insertion or junction crossing) from now on."""
+        lib().orc_env_enable_trace(self.h, int(max_events))
+        self._max_trace = int(max_events)
+
+    def trace(self):
+        """[n, 2] int32 (vehicle id, simulator edge) in the order they happened."""
+        n = lib().orc_env_trace(self.h, None)
+        if n > self._max_trace:
+            raise RuntimeError(f"trace overflow: {n} events > {self._max_trace}")
+        out = np.zeros((n, 2), np.int32)
+        lib().orc_env_trace(self.h, out.ctypes.data)
+        return out
 
     def demand(self):
         q = np.zeros(self.nveh, np.uint16)

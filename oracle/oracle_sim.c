@@ -22,6 +22,10 @@
 
 static const int PDUR[12] = {25, 6, 2, 20, 6, 2, 25, 6, 2, 20, 6, 2};
 static const unsigned GREEN[12] = {0x11BB, 0, 0, 0x11DD, 0, 0, 0xBB11, 0, 0, 0xDD11, 0, 0};
+/* actuated mode (SURVEY A-14): phase 0 minDur 5 / maxDur 50, grid_3x3.net.xml:894 */
+#define ACT_MIN 5
+#define ACT_MAX 50
+#define NO_DET (-1000)
 enum { N_ = 0, S_ = 1, E_ = 2, W_ = 3 };
 enum { MR = 0, MS = 1, ML = 2, MU = 3 };
 #define ARRIVE (-2)
@@ -36,6 +40,10 @@ struct orc_env {
     int *exit_id, *exit_ao;
     int stats[4];
     orc_idm P;
+    /* optional trace (tests): vehicle id per ring slot and the (vehicle, edge)
+     * of every edge entry (insertion or junction crossing) */
+    int *vid, *trace, ntrace, max_trace;
+    int actuated, *last_det; /* [12A] */
 };
 
 static int opp(int d) { return d ^ 1; }
@@ -76,6 +84,15 @@ static int route_out(const orc_env *g, int a, int h, int dst) {
     if (dh >= 0 && dh != opp(h)) return dh;
     return dv >= 0 ? dv : dh;
 }
+/* route words (sim.hpp): < 0x8000 destination edge (routed on the fly);
+ * >= 0x8000 explicit route, 2-bit out-directions above a sentinel 1 */
+#define ROUTED 0x8000
+static int on_final(int w, int e) { return w < ROUTED ? w == e : (w & 0x7fff) == 1; }
+static int out_dir(const orc_env *g, int a, int h, int w) {
+    return w < ROUTED ? route_out(g, a, h, w) : (w & 3);
+}
+static int advance(int w) { return w < ROUTED ? w : (ROUTED | ((w & 0x7fff) >> 2)); }
+
 static int next_edge(const orc_env *g, int a, int o) {
     int nb = nbr(g, a, o);
     return nb >= 0 ? nb * 4 + opp(o) : 4 * g->A + g->exit_id[a * 4 + o];
@@ -86,10 +103,10 @@ static int lane_for_move(const orc_env *g, const int *cnt, int m, int e) {
     if (m != MS) return 2;
     return cnt[e * 3 + 1] <= cnt[e * 3 + 0] ? 1 : 0;
 }
-static int lane_for(const orc_env *g, const int *cnt, int e2, int kf, int dst) {
-    if (e2 >= 4 * g->A || e2 == dst) return kf;
+static int lane_for(const orc_env *g, const int *cnt, int e2, int kf, int w2) {
+    if (e2 >= 4 * g->A || on_final(w2, e2)) return kf;
     int h2 = opp(e2 & 3);
-    int o2 = route_out(g, e2 >> 2, h2, dst);
+    int o2 = out_dir(g, e2 >> 2, h2, w2);
     return lane_for_move(g, cnt, movement(h2, o2), e2);
 }
 static int feeders(const orc_env *g, int e2, int fl[5]) {
@@ -235,6 +252,7 @@ orc_env *orc_env_create(int R, int C, int cap, uint64_t seed, long end_ms, int p
     g->phase = (int *)calloc(g->A, sizeof(int));
     g->ts = (int *)calloc(g->A, sizeof(int));
     g->qptr = (int *)calloc(4 * g->A, sizeof(int));
+    g->last_det = (int *)calloc(12 * g->A, sizeof(int));
     make_demand(g, seed, end_ms);
     orc_env_reset(g);
     return g;
@@ -257,11 +275,33 @@ void orc_env_set_demand(orc_env *g, int nveh, int period_ms, const uint16_t *q_i
     orc_env_reset(g);
 }
 
+/* Trace every edge entry (vehicle id, simulator edge) into trace[2 * max_events]
+ * from now on; orc_env_trace_count returns the number of entries (may exceed
+ * max_events: the excess is dropped). */
+void orc_env_enable_trace(orc_env *g, int max_events) {
+    free(g->vid); free(g->trace);
+    g->vid = (int *)calloc((size_t)g->NL * g->cap, sizeof(int));
+    g->trace = (int *)malloc(sizeof(int) * 2 * (size_t)(max_events > 0 ? max_events : 1));
+    g->ntrace = 0;
+    g->max_trace = max_events;
+}
+
+int orc_env_trace(const orc_env *g, int32_t *out) {
+    int n = g->ntrace < g->max_trace ? g->ntrace : g->max_trace;
+    if (out) memcpy(out, g->trace, sizeof(int) * 2 * (size_t)n);
+    return g->ntrace;
+}
+
+/* SUMO's actuated gap-out on phase 0 (0 = fixed durations, the default). */
+void orc_env_set_actuated(orc_env *g, int on) { g->actuated = on ? 1 : 0; }
+
 void orc_env_free(orc_env *g) {
     if (!g) return;
+    free(g->vid); free(g->trace);
     free(g->x); free(g->v); free(g->dst); free(g->head); free(g->cnt); free(g->req);
     free(g->gfrom); free(g->fx); free(g->fv); free(g->phase); free(g->ts); free(g->qptr);
     free(g->q_off); free(g->q_ids); free(g->vdst); free(g->exit_id); free(g->exit_ao);
+    free(g->last_det);
     free(g);
 }
 
@@ -272,6 +312,7 @@ void orc_env_reset(orc_env *g) {
     memset(g->phase, 0, sizeof(int) * g->A);
     memset(g->ts, 0, sizeof(int) * g->A);
     for (int e = 0; e < 4 * g->A; e++) g->qptr[e] = g->q_off[e];
+    for (int i = 0; i < 12 * g->A; i++) g->last_det[i] = NO_DET;
     memset(g->stats, 0, sizeof(g->stats));
 }
 
@@ -283,8 +324,25 @@ static int last_slot(int head, int cnt, int cap) {
 static void substep(orc_env *g, int t) {
     const orc_idm *P = &g->P;
     const int A = g->A, cap = g->cap;
-    for (int a = 0; a < A; a++)
-        if (t - g->ts[a] >= PDUR[g->phase[a]]) { g->phase[a] = (g->phase[a] + 1) % 12; g->ts[a] = t; }
+    for (int a = 0; a < A; a++) {
+        int p = g->phase[a], el = t - g->ts[a], sw;
+        if (g->actuated && p == 0) {
+            /* lanes with a green link in phase 0: lane 0 right+straight, 1
+             * straight, 2 left+U; the last detection over them */
+            int last = NO_DET;
+            for (int d = 0; d < 4; d++)
+                for (int k = 0; k < 3; k++) {
+                    unsigned m = (GREEN[0] >> (4 * d)) & 15u;
+                    int green = k == 0 ? (m & 3u) != 0 : k == 1 ? (m & 2u) != 0 : (m & 12u) != 0;
+                    if (green && g->last_det[a * 12 + d * 3 + k] > last)
+                        last = g->last_det[a * 12 + d * 3 + k];
+                }
+            sw = el >= ACT_MAX || (el >= ACT_MIN && (float)(t - last) > P->max_gap);
+        } else {
+            sw = el >= PDUR[p];
+        }
+        if (sw) { g->phase[a] = (p + 1) % 12; g->ts[a] = t; }
+    }
     /* A */
     for (int l = 0; l < g->NL; l++) {
         g->req[l] = -1;
@@ -295,17 +353,17 @@ static void substep(orc_env *g, int t) {
         float x0 = g->x[base + h0], v0 = g->v[base + h0];
         int d0 = g->dst[base + h0];
         float len = lane_len(g, e), acc, vn, xn;
-        if (e >= 4 * A || d0 == e) {
+        if (e >= 4 * A || on_final(d0, e)) {
             acc = idm_free(P, v0);
             vn = clampv(P, v0 + acc);
             xn = x0 + vn;
             g->req[l] = ARRIVE;
         } else {
             int aj = e >> 2, d = e & 3, h = opp(d);
-            int o = route_out(g, aj, h, d0);
+            int o = out_dir(g, aj, h, d0);
             int m = movement(h, o);
             int e2 = next_edge(g, aj, o);
-            int tl = e2 * 3 + lane_for(g, g->cnt, e2, kf, d0);
+            int tl = e2 * 3 + lane_for(g, g->cnt, e2, kf, advance(d0));
             int green = (GREEN[g->phase[aj]] >> (d * 4 + m)) & 1;
             if (green) {
                 int nc = g->cnt[tl];
@@ -365,6 +423,8 @@ static void substep(orc_env *g, int t) {
             if (!pop) { lxn = len; fvn = 0.0f; }
         }
         if (!pop) { g->x[base + hd] = lxn; g->v[base + hd] = fvn; }
+        float dp = len - P->det_dist, dpl = dp + P->length;
+        int det = lxn >= dp && lxo < dpl;
         int s = hd;
         for (int i = 1; i < n; i++) {
             s = (s + 1 == cap) ? 0 : s + 1;
@@ -379,9 +439,11 @@ static void substep(orc_env *g, int t) {
             }
             g->x[base + s] = xn;
             g->v[base + s] = vn;
+            det = det || (xn >= dp && xi < dpl);
             lxo = xi; lvo = vi; lxn = xn;
         }
         if (pop) { g->head[l] = (hd + 1 == cap) ? 0 : hd + 1; g->cnt[l] = n - 1; }
+        if (g->actuated && det && l < 12 * A) g->last_det[l] = t + 1;
     }
     /* D */
     for (int tl = 0; tl < g->NL; tl++) {
@@ -389,7 +451,7 @@ static void substep(orc_env *g, int t) {
         if (f < 0) continue;
         float over = g->fx[f] - lane_len(g, f / 3), vin = g->fv[f];
         int fh = g->head[f] == 0 ? cap - 1 : g->head[f] - 1;
-        int dv = g->dst[(size_t)f * cap + fh];
+        int dv = advance(g->dst[(size_t)f * cap + fh]);
         int nc = g->cnt[tl];
         float xe = over;
         if (nc > 0) {
@@ -404,6 +466,15 @@ static void substep(orc_env *g, int t) {
         g->v[(size_t)tl * cap + slot] = vin;
         g->dst[(size_t)tl * cap + slot] = dv;
         g->cnt[tl] = nc + 1;
+        if (g->vid) {
+            int id = g->vid[(size_t)f * cap + fh];
+            g->vid[(size_t)tl * cap + slot] = id;
+            if (g->ntrace < g->max_trace) {
+                g->trace[2 * g->ntrace] = id;
+                g->trace[2 * g->ntrace + 1] = tl / 3;
+            }
+            g->ntrace++;
+        }
     }
     /* E */
     for (int e = 0; e < 4 * A; e++) {
@@ -412,8 +483,8 @@ static void substep(orc_env *g, int t) {
         int id = g->q_ids[p];
         if ((long long)id * g->period_ms > (long long)t * 1000) continue;
         int d0 = g->vdst[id], h = opp(e & 3);
-        int o = route_out(g, e >> 2, h, d0);
-        int l = e * 3 + lane_for_move(g, g->cnt, movement(h, o), e);
+        int m = on_final(d0, e) ? MS : movement(h, out_dir(g, e >> 2, h, d0));
+        int l = e * 3 + lane_for_move(g, g->cnt, m, e);
         int nc = g->cnt[l];
         if (nc >= cap) continue;
         if (nc > 0) {
@@ -427,6 +498,14 @@ static void substep(orc_env *g, int t) {
         g->dst[(size_t)l * cap + slot] = d0;
         g->cnt[l] = nc + 1;
         g->qptr[e] = p + 1;
+        if (g->vid) {
+            g->vid[(size_t)l * cap + slot] = id;
+            if (g->ntrace < g->max_trace) {
+                g->trace[2 * g->ntrace] = id;
+                g->trace[2 * g->ntrace + 1] = e;
+            }
+            g->ntrace++;
+        }
         g->stats[0]++;
     }
 }

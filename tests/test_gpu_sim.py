@@ -11,13 +11,13 @@ from dmdqn_amd.env import EnvConfig, TrafficEnv  # noqa: E402
 
 
 def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_at=(),
-         scenario=None):
+         scenario=None, actuated=False):
     cfg = EnvConfig(rows=R, cols=C, num_envs=E, seed=seed, signal_features=mode,
-                    scenario=scenario)
+                    scenario=scenario, actuated=actuated)
     env = TrafficEnv(cfg)
     R, C = env.R, env.C
     obs = env.reset()
-    refs = [O.OracleEnv(R, C, seed + e) for e in range(E)]
+    refs = [O.OracleEnv(R, C, seed + e, actuated=actuated) for e in range(E)]
     if scenario is not None:
         from dmdqn_amd.sumo_scenario import scenario_tables
         q, off, vd, _, period = scenario_tables(env.scenario, 1)
@@ -113,3 +113,19 @@ def test_sim_shipped_3x3_scenario_matches_oracle():
     st = env.stats()  # inserted, arrived, running, pending
     assert (st[:, 0] > 3900).all() and (st[:, 1] > 3500).all()
     assert (st[:, 0] + st[:, 3] == 4167).all()
+
+
+@pytest.mark.parametrize("grid", [(2, 2), (4, 4)])
+def test_sim_actuated_gap_out_matches_oracle(grid):
+    """SUMO's actuated phase 0 (A-14, EnvConfig.actuated): bit-exact vs the
+    oracle over 120 steps, detector times included; gap-outs do happen."""
+    env = _run(*grid, E=4, steps=120, actuated=True, check_every=7, full_state_at=(60,))
+    ld = env.t_last_det.cpu().numpy()
+    assert (ld > 0).any()
+
+
+def test_sim_actuated_shipped_scenario():
+    from conftest import GOLDEN
+    import os
+    _run(0, 0, E=2, steps=240, check_every=20, actuated=True,
+         scenario=os.path.join(GOLDEN, "grid_3x3_p06_scenario.npz"))

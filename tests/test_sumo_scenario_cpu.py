@@ -29,6 +29,7 @@ def test_loader_on_reference_files_matches_fixture():
     a, b = load_scenario(REF_CFG), load_scenario(FIXTURE)
     np.testing.assert_array_equal(a.origin, b.origin)
     np.testing.assert_array_equal(a.dest, b.dest)
+    np.testing.assert_array_equal(a.route, b.route)
     assert (a.rows, a.cols, a.period_ms) == (b.rows, b.cols, b.period_ms)
 
 
@@ -121,3 +122,70 @@ def test_oracle_runs_the_shipped_scenario():
         t += 10
     ins, arr, run, pend = env.info()[4:8]
     assert ins + pend == 4167 and ins > 900 and arr > 0
+
+
+def _traversed(env):
+    """vehicle id -> list of simulator edges it entered, in order."""
+    seq = {}
+    for vid, e in env.trace():
+        seq.setdefault(int(vid), []).append(int(e))
+    return seq
+
+
+def test_vehicles_follow_their_scenario_routes():
+    """Every vehicle of the shipped scenario drives exactly its duarouter path
+    (grid_3x3_p06.rou.xml:23-12524): over a full 240-step episode of the
+    oracle simulator (which the HIP sim matches bit for bit, test_gpu_sim), each
+    vehicle's entered edges are its route's edges -- all of them for the
+    vehicles that arrived, a prefix for those still driving."""
+    from dmdqn_amd.sumo_scenario import route_edges
+    sc = load_scenario(FIXTURE)
+    grid = Grid(3, 3)
+    q, off, vd, N, period = scenario_tables(sc, 1)
+    env = O.OracleEnv(3, 3, 100)
+    env.set_demand(q[0], off[0], vd[0], period)
+    env.enable_trace(1 << 16)
+    rng = np.random.RandomState(1)
+    t = 0
+    for _ in range(240):
+        env.step(rng.randint(0, 4, 9).astype(np.int32), 3, t, 10, 2400)
+        t += 10
+    seq = _traversed(env)
+    ins, arr, run, pend = env.info()[4:8]
+    assert len(seq) == ins > 3900 and arr > 3500
+    full = 0
+    for vid, got in seq.items():
+        want = route_edges(sc.route[vid], sc.origin[vid], grid)
+        assert got == want[:len(got)], (vid, got, want)
+        full += got == want
+    assert full >= arr  # every arrived vehicle drove its whole route
+    if os.path.exists(REF_CFG):  # and the words decode to the file's own edge lists
+        import xml.etree.ElementTree as ET
+        rou = os.path.join(os.path.dirname(REF_CFG), "grid_3x3_p06.rou.xml")
+        for i, v in enumerate(ET.parse(rou).getroot().iter("vehicle")):
+            edges = [edge_index(e, grid) for e in v.find("route").get("edges").split()]
+            assert route_edges(sc.route[i], sc.origin[i], grid) == edges
+
+
+def test_route_words_roundtrip_and_limits():
+    from dmdqn_amd.sumo_scenario import ROUTED, route_edges, route_word
+    g = Grid(3, 3)
+    path = [edge_index("END_W_1_0_to_J_1_0", g), edge_index("J_1_0_to_J_0_0", g),
+            edge_index("J_0_0_to_END_N_0_0", g)]
+    w = route_word(path, g)
+    assert w & ROUTED and route_edges(w, path[0], g) == path
+    assert route_word(path[:1], g) == ROUTED | 1          # one-edge route: sentinel only
+    with pytest.raises(ValueError, match="not connected"):
+        route_word([path[0], path[2]], g)
+    g4 = Grid(1, 9)
+    long_path = [edge_index("END_W_0_0_to_J_0_0", g4)] + [
+        edge_index(f"J_0_{c}_to_J_0_{c + 1}", g4) for c in range(8)]
+    with pytest.raises(ValueError, match="route words hold"):
+        route_word(long_path, g4)
+
+
+def test_synthetic_demand_keeps_on_the_fly_routing():
+    """Generated demand carries destinations (< 0x8000), not route words."""
+    q, off, vd, N, period = __import__("dmdqn_amd.scenario", fromlist=["x"]).demand_tables(
+        Grid(4, 4), [0, 1])
+    assert vd.max() < 0x8000
