@@ -45,6 +45,8 @@ def parse_eval_args(argv=None):
                    help="SUMO scenario (.sumocfg or .npz) or 'synthetic' with --grid")
     p.add_argument("--grid", default="3x3")
     p.add_argument("--max_steps_per_episode", type=int, default=1000)
+    p.add_argument("--actuated", action="store_true",
+                   help="SUMO's actuated gap-out on phase 0 (grid_3x3.net.xml:894; default fixed)")
     return p.parse_args(argv)
 
 
@@ -69,7 +71,7 @@ def main_eval(argv=None):
     modes = list(args.modes)
     scenario = None if args.scenario == "synthetic" else args.scenario
     rows, cols = (int(x) for x in args.grid.split("x"))
-    env_cfg = EnvConfig(rows=rows, cols=cols, scenario=scenario)
+    env_cfg = EnvConfig(rows=rows, cols=cols, scenario=scenario, actuated=args.actuated)
     if scenario:
         from dmdqn_amd.sumo_scenario import load_scenario
         sc = load_scenario(scenario)

@@ -131,7 +131,8 @@ def train_agents(episodes=EPISODES, rows=3, cols=3, seed=0, metrics=None, scenar
 
 
 def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None, scenario=None,
-                  shared=False, save_dir=None, resume=None, log_every=20):
+                  shared=False, save_dir=None, resume=None, log_every=20, loss="mse",
+                  actuated=False):
     """E env replicas of the loop on the GPU.  The optional JSONL carries the
     reference's learn scalars (dqn_agent.py:361-370: loss, epsilon,
     q_values_mean / _std, action_distribution) and its per-step rewards with
@@ -140,8 +141,9 @@ def train_batched(episodes, rows, cols, envs, precision, seed, metrics=None, sce
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.trainer import Trainer
     cfg = AgentConfig.from_dict(AGENT_CONFIG)
-    cfg.precision, cfg.seed, cfg.shared_params = precision, seed, shared
-    tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=seed, scenario=scenario), cfg)
+    cfg.precision, cfg.seed, cfg.shared_params, cfg.loss = precision, seed, shared, loss
+    tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=seed, scenario=scenario,
+                           actuated=actuated), cfg)
     from dmdqn_amd import checkpoint as CK
     if resume:
         CK.load(resume, tr)
@@ -198,6 +200,10 @@ def main():
                     help="write agent_<id>.weights.npz (and, batched, checkpoint.pt) at the end")
     ap.add_argument("--resume", default=None, help="batched only: a checkpoint.pt to resume from")
     ap.add_argument("--log_every", type=int, default=20, help="batched metrics interval (steps)")
+    ap.add_argument("--loss", default="mse", choices=["mse", "huber"],
+                    help="batched only: mse (dqn_agent.py:352) or huber (experimental/agent.py:99)")
+    ap.add_argument("--actuated", action="store_true",
+                    help="batched only: SUMO's actuated gap-out on phase 0 (default fixed durations)")
     args = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
     rows, cols = (int(x) for x in args.grid.split("x"))
@@ -208,7 +214,8 @@ def main():
         scenario = None
     if args.batched:
         train_batched(args.episodes, rows, cols, args.envs, args.precision, args.seed, args.metrics,
-                      scenario, args.shared, args.save_dir, args.resume, args.log_every)
+                      scenario, args.shared, args.save_dir, args.resume, args.log_every, args.loss,
+                      args.actuated)
     else:
         train_agents(args.episodes, rows, cols, args.seed, args.metrics, scenario, args.save_dir)
 
