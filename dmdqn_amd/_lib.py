@@ -7,7 +7,13 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdmdqn_hip.so")
+# DMDQN_VARIANT=debug loads the debug-bounds build (libdmdqn_hip_debug.so and
+# its operator library): kernels check the indices they derive (common.hpp)
+VARIANT = os.environ.get("DMDQN_VARIANT", "")
+if VARIANT not in ("", "debug"):
+    raise ValueError(f"DMDQN_VARIANT must be '' or 'debug', got {VARIANT!r}")
+_SUFFIX = f"_{VARIANT}" if VARIANT else ""
+LIB_PATH = os.path.join(_HERE, "lib", f"libdmdqn_hip{_SUFFIX}.so")
 _LIB = None
 
 vp, i32, u32, u64, f64 = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64, C.c_double
@@ -58,6 +64,10 @@ def load(path=None):
     lib.dmdqn_last_error.restype = C.c_char_p
     lib.dmdqn_last_error.argtypes = []
     lib.dmdqn_version.restype = C.c_int
+    lib.dmdqn_debug_status.restype = C.c_int
+    lib.dmdqn_debug_status.argtypes = []
+    lib.dmdqn_debug_build.restype = C.c_int
+    lib.dmdqn_debug_build.argtypes = []
     _apply(lib, SIGNATURES)
     _LIB = lib
     return lib
@@ -69,6 +79,26 @@ def call(name, *args):
     if rc != 0:
         raise DmdqnError(f"{name} failed (rc={rc}): {lib.dmdqn_last_error().decode()}")
     return rc
+
+
+DEBUG_BITS = {1: "sim ring slot", 2: "sim route leaves the grid", 4: "replay index >= n",
+              8: "learn deque position >= cap", 16: "stored action >= 4"}
+
+
+def debug_check():
+    """Debug-bounds build: wait for the device, raise if a kernel recorded an
+    out-of-range index since the last check (the flags are cleared).  A no-op
+    in the product build."""
+    lib = load()
+    if not lib.dmdqn_debug_build():
+        return
+    import torch
+    torch.cuda.synchronize()
+    v = lib.dmdqn_debug_status()
+    if v != 0:
+        what = "HIP error reading the flags" if v < 0 else ", ".join(
+            n for b, n in DEBUG_BITS.items() if v & b)
+        raise DmdqnError(f"debug-bounds check failed ({v}): {what}")
 
 
 def ptr(t):

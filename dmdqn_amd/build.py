@@ -12,8 +12,24 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
-OBJDIR = os.path.join(LIBDIR, "obj")
-LIBNAME = "libdmdqn_hip.so"
+# variants: "" (the product build) and "debug" (-DDMDQN_DEBUG_BOUNDS: kernels
+# check and clamp the indices they derive, dmdqn_debug_status reports them)
+VARIANT_FLAGS = {"": [], "debug": ["-DDMDQN_DEBUG_BOUNDS"]}
+
+
+def _suffix(variant):
+    return f"_{variant}" if variant else ""
+
+
+def objdir(variant=""):
+    return os.path.join(LIBDIR, "obj" + _suffix(variant))
+
+
+def libname(variant=""):
+    return f"libdmdqn_hip{_suffix(variant)}.so"
+
+
+LIBNAME = libname()
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DMDQN_ARCH", "gfx950")
 
@@ -41,10 +57,10 @@ def _headers():
         os.path.join(HERE, "..", "include", "*.h"))
 
 
-def _compile(src, force):
+def _compile(src, force, variant=""):
     name = os.path.basename(src)
-    obj = os.path.join(OBJDIR, name + ".o")
-    flags = COMMON + PER_FILE.get(name, DEFAULT_FP) + EXTRA
+    obj = os.path.join(objdir(variant), name + ".o")
+    flags = COMMON + PER_FILE.get(name, DEFAULT_FP) + VARIANT_FLAGS[variant] + EXTRA
     # the flags an object was built with sit beside it: a changed flag set
     # (e.g. an experiment's -D switches, then none) forces a rebuild
     stamp = obj + ".flags"
@@ -73,13 +89,17 @@ TORCH_EXT = os.path.join(HERE, "torch_ext", "dmdqn_torch.cpp")
 TORCH_LIBNAME = "libdmdqn_torch.so"
 
 
-def build_torch_ext(force=False, verbose=True):
+def torch_libname(variant=""):
+    return f"libdmdqn_torch{_suffix(variant)}.so"
+
+
+def build_torch_ext(force=False, verbose=True, variant=""):
     """libdmdqn_torch.so: the C ABI registered as torch.ops.dmdqn.* (TORCH_LIBRARY),
     linked against libdmdqn_hip.so (same directory) and the installed PyTorch."""
     import torch
     tdir = os.path.dirname(torch.__file__)
-    so = os.path.join(LIBDIR, TORCH_LIBNAME)
-    deps = [TORCH_EXT, os.path.join(LIBDIR, LIBNAME)] + _headers()
+    so = os.path.join(LIBDIR, torch_libname(variant))
+    deps = [TORCH_EXT, os.path.join(LIBDIR, libname(variant))] + _headers()
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     flags = ["-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{tdir}/include",
@@ -94,7 +114,8 @@ def build_torch_ext(force=False, verbose=True):
             and os.path.getmtime(so) >= max(os.path.getmtime(d) for d in deps)):
         return so
     cmd = (["g++"] + flags + ["-shared", TORCH_EXT, "-o", so, f"-L{tdir}/lib", "-lc10", "-lc10_hip",
-                              "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-L{LIBDIR}", "-ldmdqn_hip",
+                              "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-L{LIBDIR}",
+                              f"-ldmdqn_hip{_suffix(variant)}",
                               "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{tdir}/lib"])
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -106,12 +127,12 @@ def build_torch_ext(force=False, verbose=True):
     return so
 
 
-def build(force=False, verbose=True):
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force=False, verbose=True, variant=""):
+    os.makedirs(objdir(variant), exist_ok=True)
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        results = list(ex.map(lambda s: _compile(s, force), srcs))
-    so = os.path.join(LIBDIR, LIBNAME)
+        results = list(ex.map(lambda s: _compile(s, force, variant), srcs))
+    so = os.path.join(LIBDIR, libname(variant))
     objs = [o for o, _ in results]
     if force or any(ch for _, ch in results) or not os.path.exists(so):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", so] + objs
@@ -120,9 +141,19 @@ def build(force=False, verbose=True):
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"built {so}")
-    build_torch_ext(force, verbose)
+    build_torch_ext(force, verbose, variant)
+    return so
+
+
+def build_all(force=False, verbose=True):
+    """The product build and the debug-bounds build (both travel to the GPU box)."""
+    so = build(force, verbose)
+    build(force, verbose, "debug")
     return so
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--debug" in sys.argv:
+        build(force="--force" in sys.argv, variant="debug")
+    else:
+        build_all(force="--force" in sys.argv)

@@ -13,7 +13,34 @@ void set_error(const char *fmt, ...) {
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
 }
+
+// per-source-file debug flags (common.hpp DMDQN_DBG_READER)
+int dbg_flags_sim();
+int dbg_flags_rng();
+int dbg_flags_learn();
+namespace f16k { int dbg_flags(); }
+namespace bf16k { int dbg_flags(); }
 }  // namespace dmdqn
+
+extern "C" int dmdqn_debug_status(void) {
+    using namespace dmdqn;
+    const int f[5] = {dbg_flags_sim(), dbg_flags_rng(), dbg_flags_learn(), f16k::dbg_flags(),
+                      bf16k::dbg_flags()};
+    int v = 0;
+    for (int x : f) {
+        if (x < 0) return -1;
+        v |= x;
+    }
+    return v;
+}
+
+extern "C" int dmdqn_debug_build(void) {
+#ifdef DMDQN_DEBUG_BOUNDS
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 extern "C" const char *dmdqn_last_error(void) { return dmdqn::g_err; }
 extern "C" int dmdqn_version(void) { return 1; }

@@ -31,6 +31,40 @@ void set_error(const char *fmt, ...);
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---------------------------------------------------------------- debug-bounds build
+// Built with -DDMDQN_DEBUG_BOUNDS (python -m dmdqn_amd.build --debug ->
+// libdmdqn_hip_debug.so): kernels check the indices they derive and
+// OR a bit into a per-source-file device flag (the bad index is clamped, so
+// nothing is touched out of range); dmdqn_debug_status() returns and clears
+// the flags of every file.  The normal build compiles the checks to nothing.
+enum : int {
+    DBG_SIM_RING = 1,     // lane head / count / append slot outside its ring
+    DBG_SIM_EDGE = 2,     // a route leaves the grid where there is no exit edge
+    DBG_SAMPLE = 4,       // a replay index outside [0, n)
+    DBG_LEARN_IDX = 8,    // a deque position outside [0, cap)
+    DBG_LEARN_ACT = 16,   // a stored action outside [0, 4)
+};
+#ifdef DMDQN_DEBUG_BOUNDS
+static __device__ int g_dbg_flags;
+#define DMDQN_DBG(cond, bit)                                                   \
+    do {                                                                       \
+        if (!(cond)) atomicOr(&::dmdqn::g_dbg_flags, (int)(bit));             \
+    } while (0)
+#define DMDQN_DBG_READER(fn)                                                   \
+    int fn() {                                                                 \
+        int v = 0, z = 0;                                                      \
+        if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(::dmdqn::g_dbg_flags), sizeof(int)) != hipSuccess) \
+            return -1;                                                         \
+        if (hipMemcpyToSymbol(HIP_SYMBOL(::dmdqn::g_dbg_flags), &z, sizeof(int)) != hipSuccess) \
+            return -1;                                                         \
+        return v;                                                              \
+    }
+#else
+#define DMDQN_DBG(cond, bit) do { } while (0)
+#define DMDQN_DBG_READER(fn) \
+    int fn() { return 0; }
+#endif
+
 // ---------------------------------------------------------------- MT19937
 // One stream = 624 state words + position.  Device kernels that consume a
 // stream run ONE wave (64 lanes) per stream: the state lives in LDS, the twist

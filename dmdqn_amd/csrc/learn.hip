@@ -158,11 +158,19 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     // ---- P0: batch metadata (ReplayBuffer.sample :63-64 via deque positions)
     if (tid < B_) {
         int pos = a.idx[(size_t)agent * B_ + tid];
+        DMDQN_DBG(pos >= 0 && pos < a.cap, DBG_LEARN_IDX);
+#ifdef DMDQN_DEBUG_BOUNDS
+        if (pos < 0 || pos >= a.cap) pos = 0;
+#endif
         int s = a.start + pos;
         if (s >= a.cap) s -= a.cap;
         size_t r = (size_t)agent * a.cap + s;
         S.slot[tid] = s;
         S.act[tid] = a.ring_a[r];
+        DMDQN_DBG(S.act[tid] < NACT, DBG_LEARN_ACT);
+#ifdef DMDQN_DEBUG_BOUNDS
+        if (S.act[tid] >= NACT) S.act[tid] = 0;
+#endif
         S.r64[tid] = a.ring_r[r];
         S.dn[tid] = a.ring_d[r] ? 1.0f : 0.0f;
     }
@@ -433,6 +441,8 @@ __global__ void __launch_bounds__(256) k_q_argmax(const float *params, size_t ps
 
 int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s);   // learn_f16.hip
 int launch_learn_bf16(const dmdqn_learn_args *a, hipStream_t s);  // learn_bf16.hip
+
+DMDQN_DBG_READER(dbg_flags_learn)
 
 }  // namespace dmdqn
 

@@ -599,7 +599,12 @@ __device__ __forceinline__ void gather_commit(h16 *R2, const Rows &g) {
 __device__ __forceinline__ void batch_slots(const dmdqn_learn_args &a, int agent, const Scratch &S) {
     const int tid = threadIdx.x;
     if (tid < B_) {
-        int s = a.start + a.idx[(size_t)agent * B_ + tid];
+        int pos = a.idx[(size_t)agent * B_ + tid];
+        DMDQN_DBG(pos >= 0 && pos < a.cap, DBG_LEARN_IDX);
+#ifdef DMDQN_DEBUG_BOUNDS
+        if (pos < 0 || pos >= a.cap) pos = 0;
+#endif
+        int s = a.start + pos;
         if (s >= a.cap) s -= a.cap;
         S.slot[tid] = s;
     }
@@ -623,6 +628,10 @@ __device__ __forceinline__ void meta_commit(const Meta &m, const Scratch &S) {
     const int tid = threadIdx.x;
     if (tid < B_) {
         S.act[tid] = m.v.x & 0xffu;
+        DMDQN_DBG(S.act[tid] < NACT, DBG_LEARN_ACT);
+#ifdef DMDQN_DEBUG_BOUNDS
+        if (S.act[tid] >= NACT) S.act[tid] = 0;
+#endif
         S.dn[tid] = (m.v.x >> 8) & 0xffu ? 1.0f : 0.0f;
         S.r64[tid] = __longlong_as_double((long long)(((unsigned long long)m.v.w << 32) | m.v.z));
     }
@@ -1044,6 +1053,8 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
         STAMP(12);
     }
 }
+
+DMDQN_DBG_READER(dbg_flags)
 
 }  // namespace H16K
 

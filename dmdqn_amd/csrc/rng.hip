@@ -207,6 +207,7 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
                 for (int q = 0; q < k; q++) {
                     const uint32_t x = Sj[q];
                     const uint16_t v = P[x], last = P[n - 1 - (uint32_t)q];
+                    DMDQN_DBG(x < n - (uint32_t)q && v < n, DBG_SAMPLE);
                     o[q] = (int32_t)v;
                     P[x] = last;
                 }
@@ -258,6 +259,7 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
                 taken = need;
             }
             if (a && c < taken) {
+                DMDQN_DBG(r < n, DBG_SAMPLE);
                 idx[((size_t)e * A + j) * k + i + c] = (int32_t)r;
                 atomicOr(&bm[r >> 5], 1u << (r & 31));
             }
@@ -274,6 +276,8 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
     __syncthreads();
     w.store(g);
 }
+
+DMDQN_DBG_READER(dbg_flags_rng)
 
 }  // namespace dmdqn
 

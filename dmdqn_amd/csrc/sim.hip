@@ -157,6 +157,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             const int aj = e >> 2, d = e & 3, h = opp(d);
             const int o = out_dir(T, aj, h, d0);
             const int m = movement(h, o);
+            DMDQN_DBG(T.nbr(aj, o) >= 0 || T.exit_id[aj * 4 + o] >= 0, DBG_SIM_EDGE);
             const int e2 = next_edge(T, aj, o);
             const int k2 = lane_for(T, e2, kf, route_advance(d0), V.cnt);
             const int tl = e2 * 3 + k2;
@@ -311,6 +312,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             if (lim < xe) xe = lim;
         }
         if (xe < 0.0f) xe = 0.0f;
+        DMDQN_DBG(nc < cap, DBG_SIM_RING);  // pass B granted only with room
         int slot = V.head[tl] + nc;
         if (slot >= cap) slot -= cap;
         V.x[(size_t)tl * cap + slot] = xe;
@@ -414,7 +416,11 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
             for (int i = tid; i < 12 * A; i += nt) V.last_det[i] = G.last_det[i];
         // each thread stages its lanes' occupied slots only (~8 % of the rings)
         for (int l = tid; l < NL; l += nt) {
-            const int h = G.head[l], n = G.cnt[l];
+            int h = G.head[l], n = G.cnt[l];
+            DMDQN_DBG(h >= 0 && h < cap && n >= 0 && n <= cap, DBG_SIM_RING);
+#ifdef DMDQN_DEBUG_BOUNDS
+            if (!(h >= 0 && h < cap && n >= 0 && n <= cap)) h = n = 0;
+#endif
             V.head[l] = h;
             V.cnt[l] = n;
             const size_t base = (size_t)l * cap;
@@ -528,6 +534,8 @@ __global__ void k_sim_reset(dmdqn_sim S) {
     for (int i = threadIdx.x; i < 12 * V.A; i += blockDim.x) V.last_det[i] = kNoDetection;
     if (threadIdx.x < 4) V.stats[threadIdx.x] = 0;
 }
+
+DMDQN_DBG_READER(dbg_flags_sim)
 
 }  // namespace dmdqn
 

@@ -26,7 +26,7 @@ ENTRY_POINTS = {
     "dmdqn_q_argmax_shared": "q_argmax",
 }
 
-TORCH_LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libdmdqn_torch.so")
+TORCH_LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), f"libdmdqn_torch{_lib._SUFFIX}.so")
 _OPS = None
 
 

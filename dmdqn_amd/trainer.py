@@ -37,6 +37,7 @@ from dataclasses import dataclass
 
 import torch
 
+from . import _lib
 from .agent import AgentConfig, BatchedDQN
 from .env import EnvConfig, TrafficEnv
 
@@ -74,10 +75,20 @@ class Trainer:
         self.total_steps = 0
         self.last_loss = None
         self.last_reward = None
+        self._debug = bool(_lib.load().dmdqn_debug_build())
 
     def step(self, collect_stats=False):
         """One loop iteration for every replica; collect_stats makes the learn
-        also produce the metrics of dqn_agent.py:361-370 (agent.learn_metrics)."""
+        also produce the metrics of dqn_agent.py:361-370 (agent.learn_metrics).
+        Under the debug-bounds build (DMDQN_VARIANT=debug) every step ends with
+        a device sync and the kernels' range checks."""
+        if self._debug:
+            st = self._step(collect_stats)
+            _lib.debug_check()
+            return st
+        return self._step(collect_stats)
+
+    def _step(self, collect_stats):
         if self.overlap == "full":
             return self._step_overlap(collect_stats)
         if self.overlap == "sample":

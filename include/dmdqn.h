@@ -47,6 +47,16 @@ extern "C" {
 const char *dmdqn_last_error(void);
 int dmdqn_version(void);
 
+/* Debug-bounds build (libdmdqn_hip_debug.so, -DDMDQN_DEBUG_BOUNDS): kernels
+ * check the ring slots, edges, replay indices and stored actions they derive,
+ * clamp a bad one and record it.  dmdqn_debug_status() returns the OR of the
+ * recorded DBG_* bits (dmdqn_amd/csrc/common.hpp: 1 sim ring, 2 sim edge,
+ * 4 sample index, 8 learn index, 16 learn action) and clears them; it waits
+ * for the device (hipMemcpyFromSymbol) and returns -1 on a HIP error.  Always
+ * 0 in the normal build; dmdqn_debug_build() says which build this is. */
+int dmdqn_debug_status(void);
+int dmdqn_debug_build(void);
+
 /* A HIP stream (returned in *stream as hipStream_t) whose kernels run only on
  * the CUs set in mask[n_words] (CU i = bit i % 32 of word i / 32).  The
  * trainer's optional split schedule runs the next step's act / sim / observe /

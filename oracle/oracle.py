@@ -10,7 +10,11 @@ _LIB = None
 
 
 def build():
-    """Compile liboracle.so (gcc) if missing or stale."""
+    """Compile liboracle.so (gcc) if missing or stale.  ORACLE_LIB names another
+    build of the same sources to load instead (the sanitizer test's
+    liboracle_asan.so)."""
+    if os.environ.get("ORACLE_LIB"):
+        return os.environ["ORACLE_LIB"]
     so = os.path.join(_HERE, "liboracle.so")
     srcs = [os.path.join(_HERE, f) for f in os.listdir(_HERE)
             if f.startswith("oracle_") and f.endswith(".c")] + [os.path.join(_HERE, "oracle.h")]

@@ -22,7 +22,7 @@ def test_object_rebuilt_when_flags_change(tmp_path, monkeypatch):
     src.write_text("// kernel\n")
     os.utime(src, (1_000_000, 1_000_000))
     calls = []
-    monkeypatch.setattr(build, "OBJDIR", str(tmp_path))
+    monkeypatch.setattr(build, "objdir", lambda variant="": str(tmp_path))
     monkeypatch.setattr(build, "_headers", lambda: [])
     monkeypatch.setattr(build.subprocess, "run", _fake_hipcc(calls))
 
@@ -53,7 +53,7 @@ def test_missing_flag_stamp_forces_rebuild(tmp_path, monkeypatch):
     os.utime(src, (1_000_000, 1_000_000))
     (tmp_path / "k.hip.o").write_text("old object, built before stamps existed")
     calls = []
-    monkeypatch.setattr(build, "OBJDIR", str(tmp_path))
+    monkeypatch.setattr(build, "objdir", lambda variant="": str(tmp_path))
     monkeypatch.setattr(build, "_headers", lambda: [])
     monkeypatch.setattr(build, "EXTRA", [])
     monkeypatch.setattr(build.subprocess, "run", _fake_hipcc(calls))

@@ -41,7 +41,8 @@ def test_python_bindings_cover_header(lib):
     product path) and every entry point but the sim's struct calls has a
     ctypes signature (the C-ABI tests' path)."""
     from dmdqn_amd import _lib, agent, env, ops  # noqa: F401  (agent registers its signatures)
-    declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version"}
+    declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version", "dmdqn_debug_status",
+                                   "dmdqn_debug_build"}
     host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy"}
     assert declared - host_only <= set(ops.ENTRY_POINTS), sorted(declared - host_only -
                                                                  set(ops.ENTRY_POINTS))
@@ -71,3 +72,15 @@ def test_host_side_argument_check_without_gpu(lib):
     rc = lib.dmdqn_act(None, 0, 0, ctypes.c_double(1.0), 4, None, None, None)
     assert rc == -1
     assert b"dmdqn_act" in lib.dmdqn_last_error()
+
+
+def test_debug_build_exports_and_reports_its_variant():
+    """Both library variants export the debug entry points; only the
+    debug-bounds build says so (no GPU call: the flags are not read here)."""
+    import ctypes
+    from dmdqn_amd import build
+    build.build(verbose=False, variant="debug")
+    for variant, want in (("", 0), ("debug", 1)):
+        lib = ctypes.CDLL(os.path.join(build.LIBDIR, build.libname(variant)))
+        assert lib.dmdqn_debug_build() == want
+        assert hasattr(lib, "dmdqn_debug_status")
