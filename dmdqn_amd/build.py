@@ -14,7 +14,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 # variants: "" (the product build) and "debug" (-DDMDQN_DEBUG_BOUNDS: kernels
 # check and clamp the indices they derive, dmdqn_debug_status reports them)
-VARIANT_FLAGS = {"": [], "debug": ["-DDMDQN_DEBUG_BOUNDS"]}
+# ("prof": the sim's per-pass timers, tools/sim_profile.py; built on demand)
+VARIANT_FLAGS = {"": [], "debug": ["-DDMDQN_DEBUG_BOUNDS"], "prof": ["-DDMDQN_SIM_PROFILE"]}
 
 
 def _suffix(variant):
@@ -153,7 +154,7 @@ def build_all(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    if "--debug" in sys.argv:
-        build(force="--force" in sys.argv, variant="debug")
+    if "--debug" in sys.argv or "--prof" in sys.argv:
+        build(force="--force" in sys.argv, variant="debug" if "--debug" in sys.argv else "prof")
     else:
         build_all(force="--force" in sys.argv)

@@ -24,6 +24,8 @@
 //   D     target lanes append the vehicle they granted (its route word
 //         advanced past the junction: sim.hpp route words)
 //   E     origin queues insert one departed vehicle per edge if there is room
+#include <stdlib.h>
+#include <string.h>
 #include <type_traits>
 
 #include "common.hpp"
@@ -518,6 +520,408 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
 #endif
 }
 
+// ================================================================ register path
+// One thread per lane (NL <= NT): the lane's vehicles live in that thread's
+// registers, compacted (front at index 0, up to RCAP), for all K substeps;
+// LDS holds only what other lanes read -- per lane the vehicle count, the last
+// vehicle (x, v), the front's request and tentative move, the grant, the
+// route word of a vehicle that left, a pending insertion -- about 37 B per
+// lane instead of the ring image's 240 (4x4: 11 KB instead of 65 KB), so every
+// env of a 1024-replica launch is resident at once (4 per CU; 8x8: one
+// 1024-thread block per CU), and pass C walks registers instead of LDS.
+// Same passes, same IEEE operation order as the LDS path / oracle_sim.c
+// (bit-exact); the rings are written back compacted (head 0).
+constexpr int RCAP = 24;
+
+__device__ __forceinline__ int wave_max_uniform(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off));
+    return __builtin_amdgcn_readfirstlane(x);
+}
+
+// append a vehicle at the back of a register lane (constant indices only)
+__device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP], int (&D_)[RCAP],
+                                            int &n, float &lx, float &lv, float xv, float vv,
+                                            int dv) {
+#pragma unroll
+    for (int i = 0; i < RCAP; i++) {
+        const bool here = i == n;
+        X_[i] = here ? xv : X_[i];
+        V_[i] = here ? vv : V_[i];
+        D_[i] = here ? dv : D_[i];
+    }
+    n++;
+    lx = xv;
+    lv = vv;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT, NT <= 256 ? 2 : 1)
+k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, int t0, int K,
+               int max_time, int32_t *halt, int32_t *phase_out, int32_t *tspent, uint8_t *done) {
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    const IdmK P(Pa);
+    EnvView G(S, blockIdx.x);
+    const int A = G.A, NL = G.NL, cap = G.cap;
+    const int tid = threadIdx.x;
+    // ---- LDS: published per-lane values, signals, detector times, stats, topology
+    int32_t *s_cnt = reinterpret_cast<int32_t *>(dyn);
+    float *s_lx = reinterpret_cast<float *>(s_cnt + NL), *s_lv = s_lx + NL;
+    int32_t *s_req = reinterpret_cast<int32_t *>(s_lv + NL), *s_gfrom = s_req + NL;
+    float *s_fx = reinterpret_cast<float *>(s_gfrom + NL), *s_fv = s_fx + NL;
+    int32_t *s_mdst = reinterpret_cast<int32_t *>(s_fv + NL), *s_ins = s_mdst + NL;
+    int32_t *s_phase = s_ins + NL, *s_ts = s_phase + A, *s_ldet = s_ts + A;
+    int32_t *s_stats = s_ldet + 12 * A;  // inserted, arrived, running, pending
+    const Topo T = build_topo(s_stats + 4, S.R, S.C, S.exit_id, S.exit_ao, P.len_inner,
+                              P.len_outer);  // synced below
+
+    // ---- this thread's lane (registers) and origin queue
+    const bool own = tid < NL;
+    const int l = tid, e = tid / 3, kf = tid - 3 * (tid / 3);
+    float X_[RCAP], V_[RCAP];
+    int D_[RCAP];
+    int n = 0;
+    float lx = 0.0f, lv = 0.0f;
+    if (own) {
+        const int h = G.head[l];
+        n = G.cnt[l];
+        DMDQN_DBG(h >= 0 && h < cap && n >= 0 && n <= RCAP && n <= cap, DBG_SIM_RING);
+        const size_t base = (size_t)l * cap;
+        const int nm = wave_max_uniform(n);
+        // loop counters are wave-uniform (bounded by the wave's longest lane):
+        // the register arrays are then indexed with a scalar (s_set_gpr_idx)
+        for (int i = 0; i < nm; i++) {
+            if (i < n) {
+                int sl = h + i;
+                if (sl >= cap) sl -= cap;
+                X_[i] = G.x[base + sl];
+                V_[i] = G.v[base + sl];
+                D_[i] = G.dst[base + sl];
+            }
+        }
+        if (n > 0) {
+            lx = G.x[base + (h + n - 1 < cap ? h + n - 1 : h + n - 1 - cap)];
+            lv = G.v[base + (h + n - 1 < cap ? h + n - 1 : h + n - 1 - cap)];
+        }
+        s_cnt[l] = n;
+        s_lx[l] = lx;
+        s_lv[l] = lv;
+        s_ins[l] = -1;
+    } else {
+        const int nm = wave_max_uniform(0);
+        (void)nm;
+    }
+    const bool leader = tid < 4 * A;  // origin queue q = tid
+    int qp = 0, qend = 0, qid = 0, qdst = 0;
+    if (leader) {
+        qp = G.qptr[tid];
+        qend = G.q_off[tid + 1];
+        if (qp < qend) { qid = G.q_ids[qp]; qdst = G.q_dst[qp]; }
+    }
+    for (int a = tid; a < A; a += NT) {
+        s_phase[a] = actions ? stride * actions[(size_t)blockIdx.x * A + a] : G.phase[a];
+        s_ts[a] = actions ? t0 : G.ts[a];
+    }
+    if (S.actuated)
+        for (int i = tid; i < 12 * A; i += NT) s_ldet[i] = G.last_det[i];
+    if (tid < 2) s_stats[tid] = G.stats[tid];
+    if (tid == 2 || tid == 3) s_stats[tid] = 0;
+    __syncthreads();
+    const float len = own ? lane_length(T, e) : 0.0f;
+
+    // TL at time t: natural phase advance (and the actuated gap-out of phase 0)
+    auto tl_pass = [&](int t) {
+        for (int a = tid; a < A; a += NT) {
+            const int p = s_phase[a], el = t - s_ts[a];
+            bool sw;
+            if (S.actuated && p == 0) {
+                constexpr uint32_t gl = green_lanes(0x11BB);  // kGreen[0]
+                int last = kNoDetection;
+#pragma unroll
+                for (int k = 0; k < 12; k++)
+                    if ((gl >> k) & 1u) last = max(last, s_ldet[a * 12 + k]);
+                sw = el >= kActMax || (el >= kActMin && (float)(t - last) > P.max_gap);
+            } else {
+                sw = el >= kPhaseDur[p];
+            }
+            if (sw) {
+                s_phase[a] = (p + 1) % 12;
+                s_ts[a] = t;
+            }
+        }
+    };
+    // an insertion the lane's origin queue ordered in the previous pass E
+#define TAKE_INSERT()                                                   \
+    do {                                                                \
+        if (own) {                                                      \
+            const int d_ = s_ins[l];                                    \
+            if (d_ != -1) {                                             \
+                DMDQN_DBG(n < RCAP, DBG_SIM_RING);                      \
+                lane_append(X_, V_, D_, n, lx, lv, P.length, 0.0f, d_); \
+                s_ins[l] = -1;                                          \
+            }                                                           \
+        }                                                               \
+    } while (0)
+
+    tl_pass(t0);
+    __syncthreads();
+    for (int k = 0; k < K; k++) {
+        const int t = t0 + k;
+        TAKE_INSERT();
+        // ---- A: the front vehicle decides (route, target lane, IDM, request)
+        int rq = -1;
+        float fx = 0.0f, fv = 0.0f;
+        if (own && n > 0) {
+            const float x0 = X_[0], v0 = V_[0];
+            const int d0 = D_[0];
+            float acc;
+            if (e >= 4 * A || on_final_edge(d0, e)) {  // exit edge or last edge: free road
+                acc = idm_free(v0, P);
+                fv = clamp_speed(v0 + acc, P);
+                fx = x0 + fv;
+                rq = kArrive;
+            } else {
+                const int aj = e >> 2, d = e & 3, h = opp(d);
+                const int o = out_dir(T, aj, h, d0);
+                const int m = movement(h, o);
+                DMDQN_DBG(T.nbr(aj, o) >= 0 || T.exit_id[aj * 4 + o] >= 0, DBG_SIM_EDGE);
+                const int e2 = next_edge(T, aj, o);
+                const int k2 = lane_for(T, e2, kf, route_advance(d0), s_cnt);
+                const int tl = e2 * 3 + k2;
+                const bool green = (kGreen[s_phase[aj]] >> (d * 4 + m)) & 1;
+                if (green) {
+                    if (s_cnt[tl] > 0) {
+                        const float xl = s_lx[tl], vl = s_lv[tl];
+                        const float gap = (len - x0) + (xl - P.length);
+                        acc = idm_acc(v0, gap, v0 - vl, P);
+                    } else {
+                        acc = idm_free(v0, P);
+                    }
+                } else {
+                    const float gap = (len - x0) + P.min_gap;
+                    acc = idm_acc(v0, gap, v0, P);
+                }
+                fv = clamp_speed(v0 + acc, P);
+                fx = x0 + fv;
+                if (fx > len) {
+                    if (green) {
+                        rq = tl;
+                    } else {
+                        fx = len;
+                        fv = 0.0f;
+                    }
+                }
+            }
+            s_fx[l] = fx;
+            s_fv[l] = fv;
+        }
+        if (own) s_req[l] = rq;
+        __syncthreads();
+
+        // ---- B: this lane, as a target, grants one request if it has room
+        if (own) {
+            int as, o, g = -1;
+            if (feed_src(T, e, as, o)) {
+                int f[5];
+                uint32_t mask = 0;
+#pragma unroll
+                for (int i = 0; i < 5; i++) {
+                    f[i] = feeder(as, o, i);
+                    mask |= (s_req[f[i]] == l ? 1u : 0u) << i;
+                }
+                if (mask) {
+                    const int start = t % 5;
+                    const uint32_t rot = ((mask >> start) | (mask << (5 - start))) & 31u;
+                    int kk = start + __ffs(rot) - 1;
+                    if (kk >= 5) kk -= 5;
+                    int fsel = f[0];
+#pragma unroll
+                    for (int i = 1; i < 5; i++) fsel = kk == i ? f[i] : fsel;
+                    bool room = n < cap;
+                    if (room && n > 0) room = (lx - P.length) >= P.min_gap;
+                    if (room) g = fsel;
+                }
+            }
+            s_gfrom[l] = g;
+        }
+        __syncthreads();
+
+        // ---- C: advance this lane front to back; the front leaves or arrives
+        {
+            const int nm = wave_max_uniform(own ? n : 0);
+            if (own && n > 0) {
+                const float lead_x_old0 = X_[0], lead_v_old0 = V_[0];
+                float lead_x_new = fx, fvn = fv;
+                bool pop = false;
+                if (rq == kArrive) {
+                    pop = lead_x_new >= len;
+                    if (pop) atomicAdd(&s_stats[1], 1);
+                } else if (rq >= 0) {
+                    pop = s_gfrom[rq] == l;
+                    if (!pop) {
+                        lead_x_new = len;
+                        fvn = 0.0f;
+                    } else {
+                        s_mdst[l] = route_advance(D_[0]);
+                    }
+                }
+                if (!pop) {
+                    X_[0] = lead_x_new;
+                    V_[0] = fvn;
+                }
+                const float dp = len - P.det_dist, dpl = dp + P.length;
+                bool det = lead_x_new >= dp && lead_x_old0 < dpl;
+                float lead_x_old = lead_x_old0, lead_v_old = lead_v_old0;
+                float last_x = X_[0], last_v = V_[0];
+                for (int i = 1; i < nm; i++) {
+                    if (i < n) {
+                        const float xi = X_[i], vi = V_[i];
+                        const float gap = (lead_x_old - P.length) - xi;
+                        const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
+                        float vn = clamp_speed(vi + acc, P);
+                        float xn = xi + vn;
+                        const float lim = lead_x_new - P.length;
+                        if (xn > lim) {
+                            if (lim < xi) {
+                                xn = xi;
+                                vn = 0.0f;
+                            } else {
+                                xn = lim;
+                                vn = lim - xi;
+                            }
+                        }
+                        X_[i] = xn;
+                        V_[i] = vn;
+                        det = det || (xn >= dp && xi < dpl);
+                        lead_x_old = xi;
+                        lead_v_old = vi;
+                        lead_x_new = xn;
+                        last_x = xn;
+                        last_v = vn;
+                    }
+                }
+                if (pop) {
+#pragma unroll
+                    for (int i = 0; i < RCAP - 1; i++) {
+                        X_[i] = X_[i + 1];
+                        V_[i] = V_[i + 1];
+                        D_[i] = D_[i + 1];
+                    }
+                    n--;
+                }
+                lx = last_x;
+                lv = last_v;
+                s_cnt[l] = n;
+                s_lx[l] = lx;
+                s_lv[l] = lv;
+                if (S.actuated && det && l < 12 * A) s_ldet[l] = t + 1;
+            }
+        }
+        __syncthreads();
+
+        // ---- D: this lane appends the vehicle it granted
+        if (own) {
+            const int f = s_gfrom[l];
+            if (f >= 0) {
+                const float over = s_fx[f] - lane_length(T, f / 3);
+                const float vin = s_fv[f];
+                const int dv = s_mdst[f];
+                float xe = over;
+                if (n > 0) {
+                    const float lim = lx - P.length - P.min_gap;
+                    if (lim < xe) xe = lim;
+                }
+                if (xe < 0.0f) xe = 0.0f;
+                DMDQN_DBG(n < cap && n < RCAP, DBG_SIM_RING);  // pass B granted only with room
+                lane_append(X_, V_, D_, n, lx, lv, xe, vin, dv);
+                s_cnt[l] = n;
+                s_lx[l] = lx;
+                s_lv[l] = lv;
+            }
+        }
+        __syncthreads();
+
+        // ---- E: each origin queue inserts its next departed vehicle if there is
+        // room (the lane's owner takes it into its registers at the next pass);
+        // then the signals advance to t + 1
+        if (leader && qp < qend && (long long)qid * S.period_ms <= (long long)t * 1000) {
+            const int q = tid, d0 = qdst;
+            const int aj = q >> 2, h = opp(q & 3);
+            // a one-edge route departs on the straight lanes (its origin is its end)
+            const int m = on_final_edge(d0, q) ? (int)MV_S : movement(h, out_dir(T, aj, h, d0));
+            const int li = q * 3 + lane_for_move(m, q, s_cnt);
+            const int nc = s_cnt[li];
+            bool room = nc < cap;
+            if (room && nc > 0) room = s_lx[li] >= 2.0f * P.length + P.min_gap;
+            if (room) {
+                s_cnt[li] = nc + 1;
+                s_lx[li] = P.length;
+                s_lv[li] = 0.0f;
+                s_ins[li] = d0;
+                atomicAdd(&s_stats[0], 1);
+                qp++;
+                if (qp < qend) { qid = G.q_ids[qp]; qdst = G.q_dst[qp]; }
+            }
+        }
+        if (k + 1 < K) tl_pass(t + 1);
+        __syncthreads();
+    }
+    TAKE_INSERT();
+#undef TAKE_INSERT
+    const int t = t0 + K;
+    // ---- outputs: halting counts, signals, running / pending, done
+    int run = own ? n : 0, pend = leader ? qend - qp : 0;
+    {
+        const int nm = wave_max_uniform(own ? n : 0);
+        if (own && l < 12 * A) {
+            int hc = 0;
+            for (int i = 0; i < nm; i++)
+                if (i < n) hc += V_[i] < P.halt_speed ? 1 : 0;
+            halt[(size_t)blockIdx.x * 12 * A + l] = hc;
+        }
+    }
+    atomicAdd(&s_stats[2], run);
+    atomicAdd(&s_stats[3], pend);
+    for (int a = tid; a < A; a += NT) {
+        phase_out[(size_t)blockIdx.x * A + a] = s_phase[a];
+        tspent[(size_t)blockIdx.x * A + a] = t - s_ts[a];
+        G.phase[a] = s_phase[a];
+        G.ts[a] = s_ts[a];
+    }
+    if (S.actuated)
+        for (int i = tid; i < 12 * A; i += NT) G.last_det[i] = s_ldet[i];
+    // ---- write-back: this lane's vehicles, compacted
+    {
+        const int nm = wave_max_uniform(own ? n : 0);
+        if (own) {
+            G.head[l] = 0;
+            G.cnt[l] = n;
+            const size_t base = (size_t)l * cap;
+            for (int i = 0; i < nm; i++) {
+                if (i < n) {
+                    G.x[base + i] = X_[i];
+                    G.v[base + i] = V_[i];
+                    G.dst[base + i] = D_[i];
+                }
+            }
+        }
+    }
+    if (leader) G.qptr[tid] = qp;
+    __syncthreads();
+    if (tid == 0) {
+        G.stats[0] = s_stats[0];
+        G.stats[1] = s_stats[1];
+        G.stats[2] = s_stats[2];
+        G.stats[3] = s_stats[3];
+        done[blockIdx.x] = (t >= max_time || (s_stats[2] + s_stats[3]) == 0) ? 1 : 0;
+    }
+}
+
+__host__ inline size_t sim_reg_lds_bytes(int R, int C) {
+    const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
+    return (size_t)NL * 9 * 4 + (size_t)A * 8 + (size_t)A * 48 + 16 + topo_bytes(R, C);
+}
+
 __global__ void k_sim_reset(dmdqn_sim S) {
     EnvView V(S, blockIdx.x);
     for (int l = threadIdx.x; l < V.NL; l += blockDim.x) {
@@ -573,9 +977,40 @@ extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const 
     DMDQN_REQUIRE(idm && halt && phase && tspent && done, "dmdqn_sim_step: null output");
     DMDQN_REQUIRE(K >= 0 && t0 >= 0 && action_stride >= 0, "dmdqn_sim_step: K/t0");
     DMDQN_REQUIRE(action_stride * 3 < 12, "dmdqn_sim_step: action_stride*3 must be < 12");
+    const int A = sim->R * sim->C, NL = 3 * (4 * A + 2 * sim->R + 2 * sim->C);
     const size_t lds = sim_lds_bytes(sim->R, sim->C, sim->cap_lane);
     const size_t topo = topo_bytes(sim->R, sim->C);
-    if (lds + topo <= 160 * 1024 - 64) {
+    const bool fits_lds = lds + topo <= 160 * 1024 - 64;
+    // Path: the LDS image when the env's state fits (4x4: 0.23 ms per C3 step;
+    // the register path measured 0.34 ms there -- its 72-register lane arrays
+    // cost vector copies), else the register path when a block can own every
+    // lane (8x8: 0.22 ms vs 0.45 ms on global memory), else global memory.
+    // DMDQN_SIM_PATH=reg|lds|global forces one (A/B, tests).
+    const char *force = getenv("DMDQN_SIM_PATH");
+    const bool reg_ok = NL <= 1024 && sim->cap_lane <= RCAP;
+    bool use_reg = !fits_lds && reg_ok;
+    bool use_lds = fits_lds;
+    if (force && !strcmp(force, "reg")) { use_reg = reg_ok; use_lds = !reg_ok && fits_lds; }
+    if (force && !strcmp(force, "lds")) { use_reg = false; use_lds = fits_lds; }
+    if (force && !strcmp(force, "global")) { use_reg = false; use_lds = false; }
+    if (use_reg) {
+        const size_t rlds = sim_reg_lds_bytes(sim->R, sim->C);
+        if (NL <= 256)
+            hipLaunchKernelGGL(k_sim_step_reg<256>, dim3(sim->E), dim3(256), rlds, as_stream(stream),
+                               *sim, *idm, actions, action_stride, t0, K, max_time, halt, phase,
+                               tspent, done);
+        else if (NL <= 512)
+            hipLaunchKernelGGL(k_sim_step_reg<512>, dim3(sim->E), dim3(512), rlds, as_stream(stream),
+                               *sim, *idm, actions, action_stride, t0, K, max_time, halt, phase,
+                               tspent, done);
+        else
+            hipLaunchKernelGGL(k_sim_step_reg<1024>, dim3(sim->E), dim3(1024), rlds,
+                               as_stream(stream), *sim, *idm, actions, action_stride, t0, K,
+                               max_time, halt, phase, tspent, done);
+        DMDQN_LAUNCH_CHECK("k_sim_step_reg");
+        return DMDQN_OK;
+    }
+    if (use_lds) {
         hipLaunchKernelGGL(k_sim_step<true>, dim3(sim->E), dim3(256), lds + topo, as_stream(stream),
                            *sim, *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent,
                            done);
