@@ -42,9 +42,16 @@ __device__ __forceinline__ int last_slot(int head, int cnt, int cap) {
 // u16 in the LDS image (edge ids < 440: grids up to 10 x 10).
 template <typename DT>
 struct EnvViewT {
+    // the LDS image (u16 destinations) keeps (x, v) interleaved, one 8-byte
+    // LDS access per vehicle, and each lane's last vehicle in lastx / lastv
+    // (passes A, B, D, E read it without the head -> slot chain); the HBM view
+    // has separate x, v rings and derives the last vehicle from head / count
+    static constexpr bool kImg = std::is_same<DT, uint16_t>::value;
     const dmdqn_sim &S;
     int e, A, X, NL, cap;
     float *x, *v;
+    float2 *xv;
+    float *lastx, *lastv;
     DT *dst;
     int32_t *head, *cnt, *req, *gfrom;
     float *fx, *fv;
@@ -60,6 +67,8 @@ struct EnvViewT {
         size_t ls = (size_t)env * NL;
         x = s.x + ls * cap;
         v = s.v + ls * cap;
+        xv = nullptr;
+        lastx = lastv = nullptr;
         if constexpr (std::is_same<DT, int32_t>::value) dst = s.dst + ls * cap;
         else dst = nullptr;  // the LDS image: set up by k_sim_step
         head = s.head + ls;
@@ -77,6 +86,22 @@ struct EnvViewT {
         q_dst = s.q_dst + (size_t)env * s.nveh;
         stats = s.stats + (size_t)env * 4;
         last_det = s.last_det + (size_t)env * 12 * A;
+    }
+    __device__ __forceinline__ float2 ld(size_t i) const {
+        if constexpr (kImg) return xv[i];
+        else return make_float2(x[i], v[i]);
+    }
+    __device__ __forceinline__ void st(size_t i, float2 a) const {
+        if constexpr (kImg) xv[i] = a;
+        else { x[i] = a.x; v[i] = a.y; }
+    }
+    // the last vehicle of lane l holding nc > 0 vehicles
+    __device__ __forceinline__ float2 last(int l, int nc) const {
+        if constexpr (kImg) return make_float2(lastx[l], lastv[l]);
+        else return ld((size_t)l * cap + last_slot(head[l], nc, cap));
+    }
+    __device__ __forceinline__ void set_last(int l, float2 a) const {
+        if constexpr (kImg) { lastx[l] = a.x; lastv[l] = a.y; }
     }
 };
 using EnvView = EnvViewT<int32_t>;
@@ -146,7 +171,8 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const int e = l / 3, kf = l - 3 * e;
         const int h0 = V.head[l];
         const size_t base = (size_t)l * cap;
-        const float x0 = V.x[base + h0], v0 = V.v[base + h0];
+        const float2 f0 = V.ld(base + h0);
+        const float x0 = f0.x, v0 = f0.y;
         const int d0 = V.dst[base + h0];
         const float len = lane_length(T, e);
         float acc, vn, xn;
@@ -167,8 +193,8 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             if (green) {
                 int nc = V.cnt[tl];
                 if (nc > 0) {
-                    int ls = last_slot(V.head[tl], nc, cap);
-                    float xl = V.x[(size_t)tl * cap + ls], vl = V.v[(size_t)tl * cap + ls];
+                    const float2 lt = V.last(tl, nc);
+                    float xl = lt.x, vl = lt.y;
                     float gap = (len - x0) + (xl - P.length);
                     acc = idm_acc(v0, gap, v0 - vl, P);
                 } else {
@@ -218,10 +244,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         for (int i = 1; i < 5; i++) fsel = k == i ? f[i] : fsel;
         int nc = V.cnt[tl];
         bool room = nc < cap;
-        if (room && nc > 0) {
-            int ls = last_slot(V.head[tl], nc, cap);
-            room = (V.x[(size_t)tl * cap + ls] - P.length) >= P.min_gap;
-        }
+        if (room && nc > 0) room = (V.last(tl, nc).x - P.length) >= P.min_gap;
         if (room) V.gfrom[tl] = fsel;
     }
     __syncthreads();
@@ -236,7 +259,8 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const size_t base = (size_t)l * cap;
         int hd = V.head[l];
         // front
-        float lead_x_old = V.x[base + hd], lead_v_old = V.v[base + hd];
+        const float2 f0 = V.ld(base + hd);
+        float lead_x_old = f0.x, lead_v_old = f0.y;
         float lead_x_new = V.fx[l];
         float fvn = V.fv[l];
         const int rq = V.req[l];
@@ -252,18 +276,24 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
                 fvn = 0.0f;
             }
         }
-        if (!pop) {
-            V.x[base + hd] = lead_x_new;
-            V.v[base + hd] = fvn;
-        }
+        if (!pop) V.st(base + hd, make_float2(lead_x_new, fvn));
         // actuated mode: a vehicle's body over the detector point dp during
         // the substep (old front < dp + length, new front >= dp)
         const float dp = len - P.det_dist, dpl = dp + P.length;
         bool det = lead_x_new >= dp && lead_x_old < dpl;
+        float2 lastv2 = make_float2(lead_x_new, fvn);
+        // the next follower's (x, v) is loaded before this one is computed and
+        // stored.  (Computing a chunk of 4 followers' IDMs together -- they
+        // depend only on old values -- measured 9 % slower: 38.5 vs 35.3 us of
+        // pass C per launch, tools/sim_profile.py.)
         int s = hd;
+        int sn = (s + 1 == cap) ? 0 : s + 1;
+        float2 nxt = n > 1 ? V.ld(base + sn) : make_float2(0.0f, 0.0f);
         for (int i = 1; i < n; i++) {
-            s = (s + 1 == cap) ? 0 : s + 1;
-            const float xi = V.x[base + s], vi = V.v[base + s];
+            s = sn;
+            const float xi = nxt.x, vi = nxt.y;
+            sn = (s + 1 == cap) ? 0 : s + 1;
+            if (i + 1 < n) nxt = V.ld(base + sn);
             const float gap = (lead_x_old - P.length) - xi;
             const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
             float vn = clamp_speed(vi + acc, P);
@@ -278,8 +308,8 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
                     vn = lim - xi;
                 }
             }
-            V.x[base + s] = xn;
-            V.v[base + s] = vn;
+            V.st(base + s, make_float2(xn, vn));
+            lastv2 = make_float2(xn, vn);
             det = det || (xn >= dp && xi < dpl);
             lead_x_old = xi;
             lead_v_old = vi;
@@ -289,6 +319,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             V.head[l] = (hd + 1 == cap) ? 0 : hd + 1;
             V.cnt[l] = n - 1;
         }
+        if (n - (pop ? 1 : 0) > 0) V.set_last(l, lastv2);
         if (S.actuated && det && l < 12 * A) V.last_det[l] = t + 1;
     }
     __syncthreads();
@@ -309,17 +340,16 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         int nc = V.cnt[tl];
         float xe = over;
         if (nc > 0) {
-            int ls = last_slot(V.head[tl], nc, cap);
-            float lim = V.x[(size_t)tl * cap + ls] - P.length - P.min_gap;
+            float lim = V.last(tl, nc).x - P.length - P.min_gap;
             if (lim < xe) xe = lim;
         }
         if (xe < 0.0f) xe = 0.0f;
         DMDQN_DBG(nc < cap, DBG_SIM_RING);  // pass B granted only with room
         int slot = V.head[tl] + nc;
         if (slot >= cap) slot -= cap;
-        V.x[(size_t)tl * cap + slot] = xe;
-        V.v[(size_t)tl * cap + slot] = vin;
+        V.st((size_t)tl * cap + slot, make_float2(xe, vin));
         V.dst[(size_t)tl * cap + slot] = dv;
+        V.set_last(tl, make_float2(xe, vin));
         V.cnt[tl] = nc + 1;
     }
     __syncthreads();
@@ -346,15 +376,12 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const int l = e * 3 + k;
         const int nc = V.cnt[l];
         if (nc >= cap) continue;
-        if (nc > 0) {
-            int ls = last_slot(V.head[l], nc, cap);
-            if (V.x[(size_t)l * cap + ls] < 2.0f * P.length + P.min_gap) continue;
-        }
+        if (nc > 0 && V.last(l, nc).x < 2.0f * P.length + P.min_gap) continue;
         int slot = V.head[l] + nc;
         if (slot >= cap) slot -= cap;
-        V.x[(size_t)l * cap + slot] = P.length;
-        V.v[(size_t)l * cap + slot] = 0.0f;
+        V.st((size_t)l * cap + slot, make_float2(P.length, 0.0f));
         V.dst[(size_t)l * cap + slot] = d0;
+        V.set_last(l, make_float2(P.length, 0.0f));
         V.cnt[l] = nc + 1;
         V.qptr[e] = p + 1;
         atomicAdd(&V.stats[0], 1);
@@ -364,13 +391,13 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
     SIM_PROF(5);
 }
 
-// LDS image of one env's mutable state (kLDS path): x, v (f32) and dst (u16)
-// rings [NL][cap], then head, cnt, req, gfrom, fx, fv [NL], phase, ts [A], qptr
-// [4A], stats [4], q_off [4A+1], last_det [12A].  4x4 grid, cap 24: 65 KB -> two envs per CU, 30 KB left (a
+// LDS image of one env's mutable state (kLDS path): (x, v) f32 pairs and dst
+// (u16) rings [NL][cap], then head, cnt, req, gfrom, fx, fv, lastx, lastv [NL],
+// phase, ts [A], qptr [4A], stats [4], q_off [4A+1], last_det [12A].  4x4 grid, cap 24: 65 KB -> two envs per CU, 30 KB left (a
 // co-resident sampler wave fits, but measured no gain: it stretches the sim).
 __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
     const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
-    return (size_t)NL * cap * 10 + (size_t)NL * 6 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16 +
+    return (size_t)NL * cap * 10 + (size_t)NL * 8 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16 +
            (size_t)(4 * A + 1) * 4 + (size_t)A * 48;  // q_off, last_det
 }
 
@@ -397,16 +424,18 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
     const int tid = threadIdx.x, nt = blockDim.x;
     if constexpr (kLDS) {
         const size_t NS = (size_t)NL * cap;
-        V.x = reinterpret_cast<float *>(dyn);
-        V.v = V.x + NS;
-        V.dst = reinterpret_cast<uint16_t *>(V.v + NS);
+        V.xv = reinterpret_cast<float2 *>(dyn);
+        V.x = V.v = nullptr;
+        V.dst = reinterpret_cast<uint16_t *>(V.xv + NS);
         V.head = reinterpret_cast<int32_t *>(V.dst + NS);  // NS = NL * cap is even (NL = 6 * ...)
         V.cnt = V.head + NL;
         V.req = V.cnt + NL;
         V.gfrom = V.req + NL;
         V.fx = reinterpret_cast<float *>(V.gfrom + NL);
         V.fv = V.fx + NL;
-        V.phase = reinterpret_cast<int32_t *>(V.fv + NL);
+        V.lastx = V.fv + NL;
+        V.lastv = V.lastx + NL;
+        V.phase = reinterpret_cast<int32_t *>(V.lastv + NL);
         V.ts = V.phase + A;
         V.qptr = V.ts + A;
         V.stats = V.qptr + 4 * A;
@@ -426,11 +455,14 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
             V.head[l] = h;
             V.cnt[l] = n;
             const size_t base = (size_t)l * cap;
+            float2 lt = make_float2(0.0f, 0.0f);
             for (int i = 0, s = h; i < n; i++, s = (s + 1 == cap) ? 0 : s + 1) {
-                V.x[base + s] = G.x[base + s];
-                V.v[base + s] = G.v[base + s];
+                lt = make_float2(G.x[base + s], G.v[base + s]);
+                V.xv[base + s] = lt;
                 V.dst[base + s] = (uint16_t)G.dst[base + s];
             }
+            V.lastx[l] = lt.x;
+            V.lastv[l] = lt.y;
         }
         for (int a = tid; a < A; a += nt) {
             V.phase[a] = G.phase[a];
@@ -469,7 +501,7 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
             int h = 0, s = V.head[l];
             const size_t base = (size_t)l * cap;
             for (int i = 0; i < n; i++) {
-                h += V.v[base + s] < P.halt_speed ? 1 : 0;
+                h += V.ld(base + s).y < P.halt_speed ? 1 : 0;
                 s = (s + 1 == cap) ? 0 : s + 1;
             }
             halt[(size_t)blockIdx.x * 12 * A + l] = h;
@@ -498,8 +530,9 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
             G.cnt[l] = n;
             const size_t base = (size_t)l * cap;
             for (int i = 0, s = h; i < n; i++, s = (s + 1 == cap) ? 0 : s + 1) {
-                G.x[base + s] = V.x[base + s];
-                G.v[base + s] = V.v[base + s];
+                const float2 a = V.xv[base + s];
+                G.x[base + s] = a.x;
+                G.v[base + s] = a.y;
                 G.dst[base + s] = V.dst[base + s];
             }
         }
