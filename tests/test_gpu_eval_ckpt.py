@@ -100,3 +100,41 @@ def test_fixed_and_dqn_modes_and_cli(tmp_path):
     # deterministic policy + identical demand per seed: queues differ only by seed
     assert all(np.isfinite(r["total_reward"]) for r in rows)
     assert len({r["seed"] for r in fixed}) == 3
+
+
+def test_resume_refuses_a_different_configuration(tmp_path):
+    """checkpoint.load validates every config field that fixes the state's
+    layout or meaning: precision, replay size, loss, grid, seeds,
+    actuated mode ... and refuses a replay-less checkpoint of a filled ring."""
+    tr = _trainer("fp16")
+    _run(tr, 130)
+    path = os.path.join(str(tmp_path), "ck.pt")
+    CK.save(path, tr)
+    bad = [
+        (EnvConfig(rows=2, cols=2, num_envs=4, seed=5), dict(precision="bf16"), "precision"),
+        (EnvConfig(rows=2, cols=2, num_envs=4, seed=5), dict(precision="fp32"), "precision"),
+        (EnvConfig(rows=2, cols=2, num_envs=4, seed=5), dict(precision="fp16",
+                                                               replay_buffer_size=400),
+         "replay_buffer_size"),
+        (EnvConfig(rows=2, cols=2, num_envs=4, seed=5), dict(precision="fp16", loss="huber"),
+         "loss"),
+        (EnvConfig(rows=2, cols=2, num_envs=4, seed=6), dict(precision="fp16"), "seed"),
+        (EnvConfig(rows=2, cols=2, num_envs=4, seed=5, actuated=True), dict(precision="fp16"),
+         "actuated"),
+    ]
+    for env_cfg, agent_kw, field in bad:
+        kw = dict(replay_buffer_size=300, target_update_frequency=7, seed=3)
+        kw.update(agent_kw)
+        tr2 = Trainer(env_cfg, AgentConfig(**kw))
+        with pytest.raises(ValueError, match=field):
+            CK.load(path, tr2)
+    # a checkpoint saved without its replay cannot resume a filled ring
+    p2 = os.path.join(str(tmp_path), "noreplay.pt")
+    CK.save(p2, tr, include_replay=False)
+    with pytest.raises(ValueError, match="without its replay"):
+        CK.load(p2, _trainer("fp16"))
+    # and the 16-bit target shadow follows the restored target (not the fresh init)
+    tr3 = _trainer("fp16")
+    CK.load(path, tr3)
+    assert torch.equal(tr3.agent.target_h[:, :tr3.agent.P],
+                       tr3.agent.target.to(tr3.agent.target_h.dtype))

@@ -151,3 +151,26 @@ def test_c1_train_py_1x1_episode(tmp_path):
     assert ol.learn_steps == 240 - 127
     got = np.concatenate([w.reshape(-1) for w in agents["J_0_0"]._core.get_weights(0)])
     np.testing.assert_allclose(got, ol.params[0], atol=5e-5)
+
+
+def test_c3_overlap_schedules_bit_identical_at_size():
+    """The optional stream schedules (trainer.py: "sample", "full") at C3 size
+    (4x4 x 1024, fp16; replay 500 to bound memory): 140 steps, losses and
+    every agent's weights bit-identical to the one-stream order."""
+    res = {}
+    for sched in ("none", "full", "sample"):
+        tr = Trainer(EnvConfig(rows=4, cols=4, num_envs=1024, seed=2),
+                     AgentConfig(precision="fp16", replay_buffer_size=500, seed=2),
+                     overlap=sched)
+        losses = []
+        for _ in range(140):
+            tr.step()
+            if tr.last_loss is not None:
+                losses.append(tr.last_loss.clone())
+        torch.cuda.synchronize()
+        res[sched] = (torch.stack(losses).cpu(), tr.agent.params.cpu(), tr.obs.cpu())
+        del tr
+        torch.cuda.empty_cache()
+    for sched in ("full", "sample"):
+        for a, b in zip(res["none"], res[sched]):
+            assert torch.equal(a, b), sched
