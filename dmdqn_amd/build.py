@@ -37,8 +37,20 @@ ARCH = os.environ.get("DMDQN_ARCH", "gfx950")
 # Exact-arithmetic kernels (RNG, observe, sim, replay) must not contract a*b+c
 # into an fma: the oracle (gcc, -ffp-contract=off) computes the same IEEE
 # sequence.  The learn kernel is tolerance-checked and may contract.
+#
+# -fno-slp-vectorize: no packed-f32 VALU ops (v_pk_{add,mul,fma}_f32) in any
+# kernel.  The sim kernel's SLP-formed `v_pk_mul_f32 v[4:5], v[4:5], ...`
+# directly after `v_mov_b32 v4, <tau>` read the stale v4 while another
+# kernel's MFMA waves co-executed on the SIMD (the fp16 learn on a second
+# stream): one follower's IDM term v*tau became (x_i - x_lead)*v, its desired
+# gap clamped to min_gap -- a different vehicle state, only under concurrency
+# (tools/sim_contention.py: every run diverged within 3 steps; none with this
+# flag, nor on the register/global sim paths, nor beside a GEMM, an LDS-filler
+# or a scratch-using kernel).  The compiler inserts no wait state there, so the
+# packed ops are kept out altogether; tests/test_isa_cpu.py checks the built
+# code objects.  (Measured cost: see DESIGN.md 6.)
 COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
-          "-Wno-unused-result", "-munsafe-fp-atomics"]
+          "-Wno-unused-result", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
 PER_FILE = {
     "learn.hip": ["-ffp-contract=fast"],
     "learn_f16.hip": ["-ffp-contract=fast"],
@@ -154,7 +166,8 @@ def build_all(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    if "--debug" in sys.argv or "--prof" in sys.argv:
-        build(force="--force" in sys.argv, variant="debug" if "--debug" in sys.argv else "prof")
+    named = [v for v in VARIANT_FLAGS if v and f"--{v}" in sys.argv]
+    if named:
+        build(force="--force" in sys.argv, variant=named[0])
     else:
         build_all(force="--force" in sys.argv)
