@@ -1,11 +1,14 @@
 """ISA guard on the built gfx950 code objects (no GPU needed).
 
-The product and debug libraries are compiled with -fno-slp-vectorize
-(dmdqn_amd/build.py): no packed-f32 VALU op (v_pk_{add,mul,fma}_f32) may
-appear in any kernel.  An SLP-formed v_pk_mul_f32 in the sim read a VGPR
-written by the instruction just before it as its stale value while another
-kernel's MFMA waves co-executed on the SIMD (tools/sim_contention.py), so the
-guard is on the machine code itself, not on the flag."""
+`v_pk_mul_f32 ... op_sel:[0,1]` (the second operand's high half feeding the
+low lane) returns 0 in about 0.1 % of executions while another kernel's MFMA
+waves co-execute on the SIMD (tools/pk_hazard.hip; the plain, neg,
+op_sel:[1,0] and op_sel_hi forms measured exact).  The SLP vectorizer formed
+it in the sim, and the full overlap schedule diverged (tools/sim_contention.py).
+dmdqn_amd/build.py compiles the exact-arithmetic kernels with
+-fno-slp-vectorize; this test checks the machine code itself:
+  * no packed-f32 op with an op_sel whose second-operand bit is set, anywhere;
+  * no packed-f32 op at all in the sim, observe, RNG and replay kernels."""
 import os
 import re
 import subprocess
@@ -40,8 +43,14 @@ def _code_objects(so, tmp_path):
     return out
 
 
+EXACT = ("k_sim_step", "k_sim_reset", "k_observe", "k_seed", "k_act", "k_sample", "k_draw",
+         "k_replay")
+PK = re.compile(r"\bv_pk_\w+_f32\b")
+OPSEL_SRC1 = re.compile(r"\bop_sel:\[\d,1")
+
+
 @pytest.mark.parametrize("variant", ["", "debug"])
-def test_no_packed_f32_valu_ops(variant, tmp_path):
+def test_packed_f32_forms(variant, tmp_path):
     if not os.path.exists(f"{LLVM}/llvm-objdump"):
         pytest.skip("ROCm LLVM tools not installed")
     so = os.path.join(build.LIBDIR, build.libname(variant))
@@ -49,11 +58,21 @@ def test_no_packed_f32_valu_ops(variant, tmp_path):
         build.build(verbose=False, variant=variant)
     cos = _code_objects(so, tmp_path)
     assert len(cos) >= 6, f"expected one code object per HIP source, found {len(cos)}"
-    kernels, bad = set(), []
+    kernels, opsel, exact = set(), [], []
     for co in cos:
         dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(co)], check=True,
                              capture_output=True, text=True).stdout
-        kernels.update(re.findall(r"^[0-9a-f]+ <(\w+)>:", dis, re.M))
-        bad += [ln.strip() for ln in dis.splitlines() if re.search(r"\bv_pk_\w+_f32\b", ln)]
+        fn = ""
+        for ln in dis.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(\w+)>:", ln)
+            if m:
+                fn = m.group(1)
+                kernels.add(fn)
+            elif PK.search(ln):
+                if OPSEL_SRC1.search(ln):
+                    opsel.append((fn, ln.strip()))
+                if any(k in fn for k in EXACT):
+                    exact.append((fn, ln.strip()))
     assert any("k_sim_step" in k for k in kernels) and any("k_learn_f16" in k for k in kernels)
-    assert not bad, f"{len(bad)} packed-f32 VALU ops, e.g. {bad[:3]}"
+    assert not opsel, f"{len(opsel)} packed-f32 ops with op_sel on the second operand: {opsel[:3]}"
+    assert not exact, f"{len(exact)} packed-f32 ops in exact-arithmetic kernels: {exact[:3]}"
