@@ -37,25 +37,27 @@ ARCH = os.environ.get("DMDQN_ARCH", "gfx950")
 # Exact-arithmetic kernels (RNG, observe, sim, replay) must not contract a*b+c
 # into an fma: the oracle (gcc, -ffp-contract=off) computes the same IEEE
 # sequence.  The learn kernel is tolerance-checked and may contract.
-COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
-          "-Wno-unused-result", "-munsafe-fp-atomics"]
-PER_FILE = {
-    "learn.hip": ["-ffp-contract=fast"],
-    "learn_f16.hip": ["-ffp-contract=fast"],
-    "learn_bf16.hip": ["-ffp-contract=fast"],
-}
-# -fno-slp-vectorize on the exact-arithmetic kernels: the SLP vectorizer formed
+#
+# -fno-slp-vectorize everywhere: the SLP vectorizer formed
 # `v_pk_mul_f32 v[4:5], v[4:5], v[8:9] op_sel:[0,1]` in the sim (the IDM terms
 # v*tau and v*dv as one packed op, v taken from the high half of the second
 # operand).  With another kernel's MFMA waves co-executing on the SIMD that
 # encoding returns 0 in about 0.1 % of executions (tools/pk_hazard.hip: only
 # op_sel with the second operand's high half; the plain, neg, op_sel:[1,0] and
-# op_sel_hi forms are exact), so one follower's desired gap collapsed to
+# op_sel_hi forms measured exact), so one follower's desired gap collapsed to
 # min_gap and the full overlap schedule diverged (tools/sim_contention.py).
-# The learn kernels' packed ops (Adam, bias, ReLU) never use that form and keep
-# SLP (measured: 2.41 vs 2.69 ms per C3 learn without it);
-# tests/test_isa_cpu.py rejects the form in every built code object.
-DEFAULT_FP = ["-ffp-contract=off", "-fno-slp-vectorize"]
+# Without SLP no kernel has a packed-f32 op at all; the learn kernels (whose
+# packed ops never used that form) measured the same with and without it
+# (same-box A/B, tools/ab_learn.sh: 2.41-2.63 vs 2.46-2.67 ms, box drift
+# larger than any difference).  tests/test_isa_cpu.py checks the built code.
+COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
+          "-Wno-unused-result", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
+PER_FILE = {
+    "learn.hip": ["-ffp-contract=fast"],
+    "learn_f16.hip": ["-ffp-contract=fast"],
+    "learn_bf16.hip": ["-ffp-contract=fast"],
+}
+DEFAULT_FP = ["-ffp-contract=off"]
 # experiment hook: extra flags for every file (e.g. -D switches while tuning)
 EXTRA = os.environ.get("DMDQN_EXTRA_FLAGS", "").split()
 

@@ -5,10 +5,12 @@ low lane) returns 0 in about 0.1 % of executions while another kernel's MFMA
 waves co-execute on the SIMD (tools/pk_hazard.hip; the plain, neg,
 op_sel:[1,0] and op_sel_hi forms measured exact).  The SLP vectorizer formed
 it in the sim, and the full overlap schedule diverged (tools/sim_contention.py).
-dmdqn_amd/build.py compiles the exact-arithmetic kernels with
--fno-slp-vectorize; this test checks the machine code itself:
+dmdqn_amd/build.py compiles every kernel with -fno-slp-vectorize; this test
+checks the machine code itself:
   * no packed-f32 op with an op_sel whose second-operand bit is set, anywhere;
-  * no packed-f32 op at all in the sim, observe, RNG and replay kernels."""
+  * no packed-f32 op at all in the sim, observe, RNG and replay kernels (the
+    learn kernels may use the measured-exact forms, should a later change
+    write packed vector code by hand)."""
 import os
 import re
 import subprocess
