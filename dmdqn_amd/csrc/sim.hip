@@ -38,21 +38,36 @@ __device__ __forceinline__ int last_slot(int head, int cnt, int cap) {
     return s >= cap ? s - cap : s;
 }
 
+// Positions of each lane held in the LDS image (kImg view); positions past it
+// stay in the HBM arrays.  4x4 at 12: a 38 KB image, four env blocks per CU.
+#ifndef DMDQN_LDS_POS
+#define DMDQN_LDS_POS 12
+#endif
+constexpr int kLdsPos = DMDQN_LDS_POS;
+constexpr int kOvPre = 8;  // HBM positions pass C loads ahead
+
 // DT: element type of the destination rings -- int32 in HBM (dmdqn_sim.dst),
 // u16 in the LDS image (edge ids < 440: grids up to 10 x 10).
+//
+// HBM view: per-lane rings [cap] addressed from head (a pop advances head).
+// LDS image (kImg): each lane COMPACTED, front at position 0 (a pop shifts the
+// followers down one position during pass C's walk, which rewrites every
+// vehicle anyway); positions < C1 (= min(cap, kLdsPos)) live in LDS as an
+// interleaved (x, v) pair and a u16 route word, positions >= C1 (long queues
+// only) in the HBM arrays at the same lane position.  Each lane's last vehicle
+// is kept in lastx / lastv, and pdst holds the route word of a front that left
+// during this substep (pass D reads it).
 template <typename DT>
 struct EnvViewT {
-    // the LDS image (u16 destinations) keeps (x, v) interleaved, one 8-byte
-    // LDS access per vehicle, and each lane's last vehicle in lastx / lastv
-    // (passes A, B, D, E read it without the head -> slot chain); the HBM view
-    // has separate x, v rings and derives the last vehicle from head / count
     static constexpr bool kImg = std::is_same<DT, uint16_t>::value;
     const dmdqn_sim &S;
-    int e, A, X, NL, cap;
+    int e, A, X, NL, cap, C1;
     float *x, *v;
     float2 *xv;
     float *lastx, *lastv;
     DT *dst;
+    int32_t *gdst;
+    uint16_t *pdst;
     int32_t *head, *cnt, *req, *gfrom;
     float *fx, *fv;
     int32_t *phase, *ts, *qptr, *stats, *last_det;
@@ -64,12 +79,15 @@ struct EnvViewT {
         X = 2 * s.R + 2 * s.C;
         NL = 3 * (4 * A + X);
         cap = s.cap_lane;
+        C1 = cap < kLdsPos ? cap : kLdsPos;
         size_t ls = (size_t)env * NL;
         x = s.x + ls * cap;
         v = s.v + ls * cap;
+        gdst = s.dst + ls * cap;
         xv = nullptr;
         lastx = lastv = nullptr;
-        if constexpr (std::is_same<DT, int32_t>::value) dst = s.dst + ls * cap;
+        pdst = nullptr;
+        if constexpr (std::is_same<DT, int32_t>::value) dst = gdst;
         else dst = nullptr;  // the LDS image: set up by k_sim_step
         head = s.head + ls;
         cnt = s.cnt + ls;
@@ -87,13 +105,30 @@ struct EnvViewT {
         stats = s.stats + (size_t)env * 4;
         last_det = s.last_det + (size_t)env * 12 * A;
     }
-    __device__ __forceinline__ float2 ld(size_t i) const {
-        if constexpr (kImg) return xv[i];
-        else return make_float2(x[i], v[i]);
+    // HBM rings: slot i of the lane block
+    __device__ __forceinline__ float2 ld(size_t i) const { return make_float2(x[i], v[i]); }
+    __device__ __forceinline__ void st(size_t i, float2 a) const { x[i] = a.x; v[i] = a.y; }
+    // LDS image: position i of lane l (i < C1 in LDS, else in HBM)
+    __device__ __forceinline__ float2 getp(int l, int i) const {
+        if (i < C1) return xv[l * C1 + i];
+        const size_t k = (size_t)l * cap + i;
+        return make_float2(x[k], v[k]);
     }
-    __device__ __forceinline__ void st(size_t i, float2 a) const {
-        if constexpr (kImg) xv[i] = a;
-        else { x[i] = a.x; v[i] = a.y; }
+    __device__ __forceinline__ void putp(int l, int i, float2 a) const {
+        if (i < C1) {
+            xv[l * C1 + i] = a;
+        } else {
+            const size_t k = (size_t)l * cap + i;
+            x[k] = a.x;
+            v[k] = a.y;
+        }
+    }
+    __device__ __forceinline__ int dstp(int l, int i) const {
+        return i < C1 ? (int)dst[l * C1 + i] : gdst[(size_t)l * cap + i];
+    }
+    __device__ __forceinline__ void set_dstp(int l, int i, int d) const {
+        if (i < C1) dst[l * C1 + i] = (DT)d;
+        else gdst[(size_t)l * cap + i] = d;
     }
     // the last vehicle of lane l holding nc > 0 vehicles
     __device__ __forceinline__ float2 last(int l, int nc) const {
@@ -169,11 +204,18 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         int n = V.cnt[l];
         if (n == 0) continue;
         const int e = l / 3, kf = l - 3 * e;
-        const int h0 = V.head[l];
-        const size_t base = (size_t)l * cap;
-        const float2 f0 = V.ld(base + h0);
+        float2 f0;
+        int d0;
+        if constexpr (View::kImg) {
+            f0 = V.xv[l * V.C1];
+            d0 = V.dst[l * V.C1];
+        } else {
+            const int h0 = V.head[l];
+            const size_t base = (size_t)l * cap;
+            f0 = V.ld(base + h0);
+            d0 = V.dst[base + h0];
+        }
         const float x0 = f0.x, v0 = f0.y;
-        const int d0 = V.dst[base + h0];
         const float len = lane_length(T, e);
         float acc, vn, xn;
         if (e >= 4 * A || on_final_edge(d0, e)) {  // exit edge or last edge: free road
@@ -257,9 +299,19 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const int e = l / 3;
         const float len = lane_length(T, e);
         const size_t base = (size_t)l * cap;
-        int hd = V.head[l];
+        const int hd = View::kImg ? 0 : V.head[l];
+        // LDS image, long queue: the HBM positions' (x, v) are loaded together
+        // here, so their latency overlaps the front and the LDS walk instead of
+        // one L2 round trip per vehicle
+        float2 ov[kOvPre];
+        const int no = View::kImg ? n - V.C1 : 0;
+        if (View::kImg && no > 0) {
+#pragma unroll
+            for (int j = 0; j < kOvPre; j++)
+                if (j < no) ov[j] = make_float2(V.x[base + V.C1 + j], V.v[base + V.C1 + j]);
+        }
         // front
-        const float2 f0 = V.ld(base + hd);
+        const float2 f0 = View::kImg ? V.xv[l * V.C1] : V.ld(base + hd);
         float lead_x_old = f0.x, lead_v_old = f0.y;
         float lead_x_new = V.fx[l];
         float fvn = V.fv[l];
@@ -276,24 +328,20 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
                 fvn = 0.0f;
             }
         }
-        if (!pop) V.st(base + hd, make_float2(lead_x_new, fvn));
+        if constexpr (View::kImg) {
+            if (!pop) V.xv[l * V.C1] = make_float2(lead_x_new, fvn);
+            else V.pdst[l] = V.dst[l * V.C1];  // the leaving front's route word, for pass D
+        } else {
+            if (!pop) V.st(base + hd, make_float2(lead_x_new, fvn));
+        }
         // actuated mode: a vehicle's body over the detector point dp during
         // the substep (old front < dp + length, new front >= dp)
         const float dp = len - P.det_dist, dpl = dp + P.length;
         bool det = lead_x_new >= dp && lead_x_old < dpl;
         float2 lastv2 = make_float2(lead_x_new, fvn);
-        // the next follower's (x, v) is loaded before this one is computed and
-        // stored.  (Computing a chunk of 4 followers' IDMs together -- they
-        // depend only on old values -- measured 9 % slower: 38.5 vs 35.3 us of
-        // pass C per launch, tools/sim_profile.py.)
-        int s = hd;
-        int sn = (s + 1 == cap) ? 0 : s + 1;
-        float2 nxt = n > 1 ? V.ld(base + sn) : make_float2(0.0f, 0.0f);
-        for (int i = 1; i < n; i++) {
-            s = sn;
-            const float xi = nxt.x, vi = nxt.y;
-            sn = (s + 1 == cap) ? 0 : s + 1;
-            if (i + 1 < n) nxt = V.ld(base + sn);
+        // one follower: IDM against the old leader state, no overlap with the
+        // leader's new position
+        auto follow = [&](float xi, float vi) -> float2 {
             const float gap = (lead_x_old - P.length) - xi;
             const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
             float vn = clamp_speed(vi + acc, P);
@@ -308,15 +356,73 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
                     vn = lim - xi;
                 }
             }
-            V.st(base + s, make_float2(xn, vn));
             lastv2 = make_float2(xn, vn);
             det = det || (xn >= dp && xi < dpl);
             lead_x_old = xi;
             lead_v_old = vi;
             lead_x_new = xn;
+            return lastv2;
+        };
+        if constexpr (View::kImg) {
+            // positions 1 .. m-1 in LDS (branch-free walk; a popped front shifts
+            // each follower and its route word down one position), then the
+            // HBM positions of a long queue
+            const int C1 = V.C1, m = n < C1 ? n : C1, sh = pop ? 1 : 0;
+            float2 *xl = V.xv + l * C1;
+            uint16_t *dl = V.dst + l * C1;
+            float2 nxt = m > 1 ? xl[1] : make_float2(0.0f, 0.0f);
+            // route words ride along (rewritten in place when nothing popped:
+            // no divergent branch in the walk)
+            uint16_t dn = m > 1 ? dl[1] : 0;
+            for (int i = 1; i < m; i++) {
+                const float2 cur = nxt;
+                const uint16_t dc = dn;
+                if (i + 1 < m) {
+                    nxt = xl[i + 1];
+                    dn = dl[i + 1];
+                }
+                xl[i - sh] = follow(cur.x, cur.y);
+                dl[i - sh] = dc;
+            }
+            if (no > 0) {
+                // a pop shifts the HBM route words too: loaded together first
+                int od[kOvPre];
+                if (sh) {
+#pragma unroll
+                    for (int j = 0; j < kOvPre; j++)
+                        if (j < no) od[j] = V.gdst[base + C1 + j];
+                }
+#pragma unroll
+                for (int j = 0; j < kOvPre; j++) {
+                    if (j < no) {
+                        const int i = C1 + j;
+                        V.putp(l, i - sh, follow(ov[j].x, ov[j].y));
+                        if (sh) V.set_dstp(l, i - 1, od[j]);
+                    }
+                }
+                for (int i = C1 + kOvPre; i < n; i++) {  // cap > C1 + kOvPre only
+                    const float2 cur = V.getp(l, i);
+                    V.putp(l, i - sh, follow(cur.x, cur.y));
+                    if (sh) V.set_dstp(l, i - 1, V.dstp(l, i));
+                }
+            }
+        } else {
+            // the next follower's (x, v) is loaded before this one is computed
+            // and stored.  (Computing a chunk of 4 followers' IDMs together --
+            // they depend only on old values -- measured 9 % slower.)
+            int s = hd;
+            int sn = (s + 1 == cap) ? 0 : s + 1;
+            float2 nxt = n > 1 ? V.ld(base + sn) : make_float2(0.0f, 0.0f);
+            for (int i = 1; i < n; i++) {
+                s = sn;
+                const float2 cur = nxt;
+                sn = (s + 1 == cap) ? 0 : s + 1;
+                if (i + 1 < n) nxt = V.ld(base + sn);
+                V.st(base + s, follow(cur.x, cur.y));
+            }
         }
         if (pop) {
-            V.head[l] = (hd + 1 == cap) ? 0 : hd + 1;
+            if constexpr (!View::kImg) V.head[l] = (hd + 1 == cap) ? 0 : hd + 1;
             V.cnt[l] = n - 1;
         }
         if (n - (pop ? 1 : 0) > 0) V.set_last(l, lastv2);
@@ -334,9 +440,14 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const float over = V.fx[f] - lane_length(T, f / 3);
         const float vin = V.fv[f];
         // the source lane already popped its front; read its (old) destination
-        // from the slot it vacated
-        const int fh = V.head[f] == 0 ? cap - 1 : V.head[f] - 1;
-        const int dv = route_advance(V.dst[(size_t)f * cap + fh]);
+        // from the slot it vacated (LDS image: from pdst)
+        int dv;
+        if constexpr (View::kImg) {
+            dv = route_advance(V.pdst[f]);
+        } else {
+            const int fh = V.head[f] == 0 ? cap - 1 : V.head[f] - 1;
+            dv = route_advance(V.dst[(size_t)f * cap + fh]);
+        }
         int nc = V.cnt[tl];
         float xe = over;
         if (nc > 0) {
@@ -345,10 +456,15 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         }
         if (xe < 0.0f) xe = 0.0f;
         DMDQN_DBG(nc < cap, DBG_SIM_RING);  // pass B granted only with room
-        int slot = V.head[tl] + nc;
-        if (slot >= cap) slot -= cap;
-        V.st((size_t)tl * cap + slot, make_float2(xe, vin));
-        V.dst[(size_t)tl * cap + slot] = dv;
+        if constexpr (View::kImg) {
+            V.putp(tl, nc, make_float2(xe, vin));
+            V.set_dstp(tl, nc, dv);
+        } else {
+            int slot = V.head[tl] + nc;
+            if (slot >= cap) slot -= cap;
+            V.st((size_t)tl * cap + slot, make_float2(xe, vin));
+            V.dst[(size_t)tl * cap + slot] = dv;
+        }
         V.set_last(tl, make_float2(xe, vin));
         V.cnt[tl] = nc + 1;
     }
@@ -377,10 +493,15 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const int nc = V.cnt[l];
         if (nc >= cap) continue;
         if (nc > 0 && V.last(l, nc).x < 2.0f * P.length + P.min_gap) continue;
-        int slot = V.head[l] + nc;
-        if (slot >= cap) slot -= cap;
-        V.st((size_t)l * cap + slot, make_float2(P.length, 0.0f));
-        V.dst[(size_t)l * cap + slot] = d0;
+        if constexpr (View::kImg) {
+            V.putp(l, nc, make_float2(P.length, 0.0f));
+            V.set_dstp(l, nc, d0);
+        } else {
+            int slot = V.head[l] + nc;
+            if (slot >= cap) slot -= cap;
+            V.st((size_t)l * cap + slot, make_float2(P.length, 0.0f));
+            V.dst[(size_t)l * cap + slot] = d0;
+        }
         V.set_last(l, make_float2(P.length, 0.0f));
         V.cnt[l] = nc + 1;
         V.qptr[e] = p + 1;
@@ -391,23 +512,26 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
     SIM_PROF(5);
 }
 
-// LDS image of one env's mutable state (kLDS path): (x, v) f32 pairs and dst
-// (u16) rings [NL][cap], then head, cnt, req, gfrom, fx, fv, lastx, lastv [NL],
-// phase, ts [A], qptr [4A], stats [4], q_off [4A+1], last_det [12A].  4x4 grid, cap 24: 65 KB -> two envs per CU, 30 KB left (a
-// co-resident sampler wave fits, but measured no gain: it stretches the sim).
+// LDS image of one env's mutable state (kLDS path): compacted lanes' first C1
+// positions as (x, v) f32 pairs [NL][C1], their u16 route words [NL][C1] and
+// pdst [NL], then cnt, req, gfrom, fx, fv, lastx, lastv [NL], phase, ts [A],
+// qptr [4A], stats [4], q_off [4A+1], last_det [12A].  4x4 grid: 37.4 KB (+1.1 KB
+// of topology) -> four env blocks per CU, all 1024 envs of C3 resident at once
+// (the full-ring image was 65 KB: two per CU, two rounds).
 __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
     const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
-    return (size_t)NL * cap * 10 + (size_t)NL * 8 * 4 + (size_t)A * 8 + (size_t)A * 16 + 16 +
-           (size_t)(4 * A + 1) * 4 + (size_t)A * 48;  // q_off, last_det
+    const int C1 = cap < kLdsPos ? cap : kLdsPos;
+    return (size_t)NL * C1 * 8 + (size_t)NL * (C1 + 1) * 2 + (size_t)NL * 7 * 4 + (size_t)A * 8 +
+           (size_t)A * 16 + 16 + (size_t)(4 * A + 1) * 4 + (size_t)A * 48;  // q_off, last_det
 }
 
 // One RL step per env (block).  kLDS: the env's state is staged into LDS for
 // the K substeps (every pass is then an LDS-latency loop instead of an L2 one:
-// pass C walks each lane's vehicles front to back) and only occupied ring
-// slots move between HBM and LDS.  !kLDS: the same passes on global memory,
-// for grids whose state exceeds LDS.
+// pass C walks each lane's vehicles front to back); only occupied positions
+// move between HBM and LDS, and the lanes are written back compacted (head 0).
+// !kLDS: the same passes on global memory rings.
 template <bool kLDS>
-__global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions,
+__global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions,
                                                   int stride, int t0, int K, int max_time,
                                                   int32_t *halt, int32_t *phase_out,
                                                   int32_t *tspent, uint8_t *done) {
@@ -423,12 +547,13 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
     const int A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
     if constexpr (kLDS) {
-        const size_t NS = (size_t)NL * cap;
+        const int C1 = V.C1;
+        const size_t NS = (size_t)NL * C1;
         V.xv = reinterpret_cast<float2 *>(dyn);
-        V.x = V.v = nullptr;
         V.dst = reinterpret_cast<uint16_t *>(V.xv + NS);
-        V.head = reinterpret_cast<int32_t *>(V.dst + NS);  // NS = NL * cap is even (NL = 6 * ...)
-        V.cnt = V.head + NL;
+        V.pdst = V.dst + NS;
+        V.head = nullptr;  // compacted lanes: position 0 is the front
+        V.cnt = reinterpret_cast<int32_t *>(V.pdst + NL);  // NL(C1 + 1) u16: NL = 6 * ... is even
         V.req = V.cnt + NL;
         V.gfrom = V.req + NL;
         V.fx = reinterpret_cast<float *>(V.gfrom + NL);
@@ -445,22 +570,46 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
         V.last_det = qoff + 4 * A + 1;
         if (S.actuated)
             for (int i = tid; i < 12 * A; i += nt) V.last_det[i] = G.last_det[i];
-        // each thread stages its lanes' occupied slots only (~8 % of the rings)
+        // each thread stages its lanes' occupied positions < C1 (~8 % of the
+        // rings).  A lane whose ring does not start at slot 0 (written by the
+        // HBM path, or a checkpoint of it) is first rotated in place in HBM
+        // (cycle-leader rotation by head: scalar temporaries only).
         for (int l = tid; l < NL; l += nt) {
             int h = G.head[l], n = G.cnt[l];
             DMDQN_DBG(h >= 0 && h < cap && n >= 0 && n <= cap, DBG_SIM_RING);
 #ifdef DMDQN_DEBUG_BOUNDS
             if (!(h >= 0 && h < cap && n >= 0 && n <= cap)) h = n = 0;
 #endif
-            V.head[l] = h;
             V.cnt[l] = n;
             const size_t base = (size_t)l * cap;
-            float2 lt = make_float2(0.0f, 0.0f);
-            for (int i = 0, s = h; i < n; i++, s = (s + 1 == cap) ? 0 : s + 1) {
-                lt = make_float2(G.x[base + s], G.v[base + s]);
-                V.xv[base + s] = lt;
-                V.dst[base + s] = (uint16_t)G.dst[base + s];
+            if (h != 0 && n > 0) {
+                int g = cap, b = h;  // gcd(cap, h) cycles
+                while (b) { const int r = g % b; g = b; b = r; }
+                for (int c = 0; c < g; c++) {
+                    const float tx = G.x[base + c], tv = G.v[base + c];
+                    const int td = G.dst[base + c];
+                    int j = c;
+                    for (;;) {
+                        int k = j + h;
+                        if (k >= cap) k -= cap;
+                        if (k == c) break;
+                        G.x[base + j] = G.x[base + k];
+                        G.v[base + j] = G.v[base + k];
+                        G.dst[base + j] = G.dst[base + k];
+                        j = k;
+                    }
+                    G.x[base + j] = tx;
+                    G.v[base + j] = tv;
+                    G.dst[base + j] = td;
+                }
             }
+            float2 lt = make_float2(0.0f, 0.0f);
+            for (int i = 0; i < n && i < C1; i++) {
+                lt = make_float2(G.x[base + i], G.v[base + i]);
+                V.xv[l * C1 + i] = lt;
+                V.dst[l * C1 + i] = (uint16_t)G.dst[base + i];
+            }
+            if (n > C1) lt = make_float2(G.x[base + n - 1], G.v[base + n - 1]);
             V.lastx[l] = lt.x;
             V.lastv[l] = lt.y;
         }
@@ -498,11 +647,16 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
         const int n = V.cnt[l];
         run += n;
         if (l < 12 * A) {
-            int h = 0, s = V.head[l];
-            const size_t base = (size_t)l * cap;
-            for (int i = 0; i < n; i++) {
-                h += V.ld(base + s).y < P.halt_speed ? 1 : 0;
-                s = (s + 1 == cap) ? 0 : s + 1;
+            int h = 0;
+            if constexpr (kLDS) {
+                for (int i = 0; i < n; i++) h += V.getp(l, i).y < P.halt_speed ? 1 : 0;
+            } else {
+                int s = V.head[l];
+                const size_t base = (size_t)l * cap;
+                for (int i = 0; i < n; i++) {
+                    h += V.ld(base + s).y < P.halt_speed ? 1 : 0;
+                    s = (s + 1 == cap) ? 0 : s + 1;
+                }
             }
             halt[(size_t)blockIdx.x * 12 * A + l] = h;
         }
@@ -523,17 +677,18 @@ __global__ void __launch_bounds__(256) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, con
         done[blockIdx.x] = (t >= max_time || (s_running + s_pending) == 0) ? 1 : 0;
     }
     if constexpr (kLDS) {
-        // write back: occupied slots, lane heads/counts, signals, queues
+        // write back: occupied LDS positions (the rest are in HBM already),
+        // lane counts (head 0), signals, queues
         for (int l = tid; l < NL; l += nt) {
-            const int h = V.head[l], n = V.cnt[l];
-            G.head[l] = h;
+            const int n = V.cnt[l], C1 = V.C1;
+            G.head[l] = 0;
             G.cnt[l] = n;
             const size_t base = (size_t)l * cap;
-            for (int i = 0, s = h; i < n; i++, s = (s + 1 == cap) ? 0 : s + 1) {
-                const float2 a = V.xv[base + s];
-                G.x[base + s] = a.x;
-                G.v[base + s] = a.y;
-                G.dst[base + s] = V.dst[base + s];
+            for (int i = 0; i < n && i < C1; i++) {
+                const float2 a = V.xv[l * C1 + i];
+                G.x[base + i] = a.x;
+                G.v[base + i] = a.y;
+                G.dst[base + i] = V.dst[l * C1 + i];
             }
         }
         for (int a = tid; a < A; a += nt) {
@@ -1014,15 +1169,16 @@ extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const 
     const size_t lds = sim_lds_bytes(sim->R, sim->C, sim->cap_lane);
     const size_t topo = topo_bytes(sim->R, sim->C);
     const bool fits_lds = lds + topo <= 160 * 1024 - 64;
-    // Path: the LDS image when the env's state fits (4x4: 0.23 ms per C3 step;
-    // the register path measured 0.34 ms there -- its 72-register lane arrays
-    // cost vector copies), else the register path when a block can own every
-    // lane (8x8: 0.22 ms vs 0.45 ms on global memory), else global memory.
+    const bool lds_2cu = 2 * (lds + topo + 16) <= 160 * 1024;
+    // Path: the LDS image when at least two env blocks fit per CU (4x4: 38.5 KB,
+    // four per CU), else the register path when a block can own every lane
+    // (8x8: 0.22 ms vs 0.45 ms on global memory; its 139 KB image would run one
+    // block per CU), else the LDS image if it fits at all, else global memory.
     // DMDQN_SIM_PATH=reg|lds|global forces one (A/B, tests).
     const char *force = getenv("DMDQN_SIM_PATH");
     const bool reg_ok = NL <= 1024 && sim->cap_lane <= RCAP;
-    bool use_reg = !fits_lds && reg_ok;
-    bool use_lds = fits_lds;
+    bool use_reg = !lds_2cu && reg_ok;
+    bool use_lds = fits_lds && !use_reg;
     if (force && !strcmp(force, "reg")) { use_reg = reg_ok; use_lds = !reg_ok && fits_lds; }
     if (force && !strcmp(force, "lds")) { use_reg = false; use_lds = fits_lds; }
     if (force && !strcmp(force, "global")) { use_reg = false; use_lds = false; }

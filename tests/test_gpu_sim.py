@@ -11,13 +11,20 @@ from dmdqn_amd.env import EnvConfig, TrafficEnv  # noqa: E402
 
 
 def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_at=(),
-         scenario=None, actuated=False):
+         scenario=None, actuated=False, action_fn=None, path_at=None, period_ms=None):
+    """Step E replicas through the HIP sim and the oracle side by side.
+    action_fn(step, rng) -> [E, A] actions (default: uniform random);
+    path_at {step: "reg" | "lds" | "global"} switches DMDQN_SIM_PATH before
+    that step (the kernel reads it per launch)."""
+    import os
+    max_cnt = 0
     cfg = EnvConfig(rows=R, cols=C, num_envs=E, seed=seed, signal_features=mode,
-                    scenario=scenario, actuated=actuated)
+                    scenario=scenario, actuated=actuated, period_ms=period_ms)
     env = TrafficEnv(cfg)
     R, C = env.R, env.C
     obs = env.reset()
-    refs = [O.OracleEnv(R, C, seed + e, actuated=actuated) for e in range(E)]
+    refs = [O.OracleEnv(R, C, seed + e, period_ms=period_ms or 0, actuated=actuated)
+            for e in range(E)]
     if scenario is not None:
         from dmdqn_amd.sumo_scenario import scenario_tables
         q, off, vd, _, period = scenario_tables(env.scenario, 1)
@@ -30,8 +37,12 @@ def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_a
     rng = np.random.RandomState(seed)
     t = 0
     for step in range(steps):
-        acts = rng.randint(0, 4, size=(E, A)).astype(np.int32)
+        if path_at and step in path_at:
+            os.environ["DMDQN_SIM_PATH"] = path_at[step]
+        acts = (action_fn(step, rng) if action_fn else
+                rng.randint(0, 4, size=(E, A))).astype(np.int32)
         obs, rew, done, info = env.step(torch.from_numpy(acts).cuda())
+        max_cnt = max(max_cnt, int(env.t_cnt.max()))
         if step % check_every and step not in full_state_at and step != steps - 1:
             for e in range(E):
                 halt, ph, ts, _ = refs[e].step(acts[e], 3, t, 10, 2400)
@@ -74,6 +85,7 @@ def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_a
             st = env.stats()
             for e in range(E):
                 np.testing.assert_array_equal(st[e], refs[e].info()[4:8])
+    env.max_cnt_seen = max_cnt
     return env
 
 
@@ -132,6 +144,21 @@ def test_sim_actuated_shipped_scenario():
     import os
     _run(0, 0, E=2, steps=240, check_every=20, actuated=True,
          scenario=os.path.join(GOLDEN, "grid_3x3_p06_scenario.npz"))
+
+
+def test_lds_image_long_queues_and_path_switches(monkeypatch):
+    """The LDS image keeps each lane's first 12 positions in LDS and the rest
+    in HBM, lanes compacted.  Heavy demand with the signals held (phase 0 only:
+    the E-W approaches queue to capacity) drives lanes past 12 vehicles; the
+    path changes mid-episode (global rings with a rotated head -> LDS image,
+    which compacts them -> register lanes -> LDS image), bit-exact vs the
+    oracle throughout."""
+    monkeypatch.setenv("DMDQN_SIM_PATH", "global")
+    hold = lambda step, rng: np.zeros((3, 16))  # noqa: E731
+    env = _run(4, 4, E=3, steps=90, check_every=5, full_state_at=(29, 30, 59, 60),
+               action_fn=hold, period_ms=150,
+               path_at={0: "global", 30: "lds", 45: "reg", 60: "lds"})
+    assert env.max_cnt_seen > 12, env.max_cnt_seen
 
 
 @pytest.mark.parametrize("path", ["reg", "lds", "global"])
