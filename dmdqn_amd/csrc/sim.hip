@@ -50,13 +50,13 @@ constexpr int kOvPre = 8;  // HBM positions pass C loads ahead
 // u16 in the LDS image (edge ids < 440: grids up to 10 x 10).
 //
 // HBM view: per-lane rings [cap] addressed from head (a pop advances head).
-// LDS image (kImg): each lane COMPACTED, front at position 0 (a pop shifts the
-// followers down one position during pass C's walk, which rewrites every
-// vehicle anyway); positions < C1 (= min(cap, kLdsPos)) live in LDS as an
-// interleaved (x, v) pair and a u16 route word, positions >= C1 (long queues
-// only) in the HBM arrays at the same lane position.  Each lane's last vehicle
-// is kept in lastx / lastv, and pdst holds the route word of a front that left
-// during this substep (pass D reads it).
+// LDS image (kImg): a lane's first C1 (= min(cap, kLdsPos)) positions are a
+// ring of C1 LDS slots from head[l] -- an interleaved (x, v) pair and a u16
+// route word per slot; positions >= C1 (long queues only) sit compacted in the
+// HBM arrays at their lane position.  A pop advances the LDS head and moves the
+// first HBM vehicle into the freed slot (the HBM tail shifts down one).  Each
+// lane's last vehicle is kept in lastx / lastv, and pdst holds the route word
+// of a front that left during this substep (pass D reads it).
 template <typename DT>
 struct EnvViewT {
     static constexpr bool kImg = std::is_same<DT, uint16_t>::value;
@@ -108,15 +108,19 @@ struct EnvViewT {
     // HBM rings: slot i of the lane block
     __device__ __forceinline__ float2 ld(size_t i) const { return make_float2(x[i], v[i]); }
     __device__ __forceinline__ void st(size_t i, float2 a) const { x[i] = a.x; v[i] = a.y; }
-    // LDS image: position i of lane l (i < C1 in LDS, else in HBM)
+    // LDS image: position i of lane l (i < C1: LDS ring slot, else HBM)
+    __device__ __forceinline__ int lslot(int l, int i) const {
+        const int s = head[l] + i;
+        return l * C1 + (s >= C1 ? s - C1 : s);
+    }
     __device__ __forceinline__ float2 getp(int l, int i) const {
-        if (i < C1) return xv[l * C1 + i];
+        if (i < C1) return xv[lslot(l, i)];
         const size_t k = (size_t)l * cap + i;
         return make_float2(x[k], v[k]);
     }
     __device__ __forceinline__ void putp(int l, int i, float2 a) const {
         if (i < C1) {
-            xv[l * C1 + i] = a;
+            xv[lslot(l, i)] = a;
         } else {
             const size_t k = (size_t)l * cap + i;
             x[k] = a.x;
@@ -124,10 +128,10 @@ struct EnvViewT {
         }
     }
     __device__ __forceinline__ int dstp(int l, int i) const {
-        return i < C1 ? (int)dst[l * C1 + i] : gdst[(size_t)l * cap + i];
+        return i < C1 ? (int)dst[lslot(l, i)] : gdst[(size_t)l * cap + i];
     }
     __device__ __forceinline__ void set_dstp(int l, int i, int d) const {
-        if (i < C1) dst[l * C1 + i] = (DT)d;
+        if (i < C1) dst[lslot(l, i)] = (DT)d;
         else gdst[(size_t)l * cap + i] = d;
     }
     // the last vehicle of lane l holding nc > 0 vehicles
@@ -166,9 +170,20 @@ __device__ __forceinline__ QNext next_vehicle(const View &V, int p) {
 #define SIM_PROF(i) do { } while (0)
 #endif
 
+// The routing decision of a lane's front is a function of the lane and the
+// front's route word only (static topology): the movement m at the junction
+// ahead, the next edge e2 and the movement there (mv2 < 0: keep the lane
+// index).  Each thread keeps it for its first lane (l = tid) across substeps
+// and recomputes it only when the front's route word changes -- a front
+// waits at the stop line for many substeps.
+struct RouteCache {
+    int d0, m, e2, mv2;
+};
+
 template <typename View>
 __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, int t,
-                                        QNext qn[QSLOTS], uint64_t *prof, uint64_t &prof_t) {
+                                        QNext qn[QSLOTS], RouteCache &rc, uint64_t *prof,
+                                        uint64_t &prof_t) {
     const dmdqn_sim &S = V.S;
     const int A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -180,14 +195,14 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const int p = V.phase[a], el = t - V.ts[a];
         bool sw;
         if (S.actuated && p == 0) {
-            constexpr uint32_t gl = green_lanes(0x11BB);  // kGreen[0]
+            constexpr uint32_t gl = green_lanes(0x11BB);  // green_mask(0)
             int last = kNoDetection;
 #pragma unroll
             for (int k = 0; k < 12; k++)
                 if ((gl >> k) & 1u) last = max(last, V.last_det[a * 12 + k]);
             sw = el >= kActMax || (el >= kActMin && (float)(t - last) > P.max_gap);
         } else {
-            sw = el >= kPhaseDur[p];
+            sw = el >= phase_dur(p);
         }
         if (sw) {
             V.phase[a] = (p + 1) % 12;
@@ -207,8 +222,9 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         float2 f0;
         int d0;
         if constexpr (View::kImg) {
-            f0 = V.xv[l * V.C1];
-            d0 = V.dst[l * V.C1];
+            const int k0 = l * V.C1 + V.head[l];
+            f0 = V.xv[k0];
+            d0 = V.dst[k0];
         } else {
             const int h0 = V.head[l];
             const size_t base = (size_t)l * cap;
@@ -225,13 +241,28 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             V.req[l] = kArrive;
         } else {
             const int aj = e >> 2, d = e & 3, h = opp(d);
-            const int o = out_dir(T, aj, h, d0);
-            const int m = movement(h, o);
-            DMDQN_DBG(T.nbr(aj, o) >= 0 || T.exit_id[aj * 4 + o] >= 0, DBG_SIM_EDGE);
-            const int e2 = next_edge(T, aj, o);
-            const int k2 = lane_for(T, e2, kf, route_advance(d0), V.cnt);
+            int m, e2, mv2;
+            if (l == tid && rc.d0 == d0) {
+                m = rc.m;
+                e2 = rc.e2;
+                mv2 = rc.mv2;
+            } else {
+                const int o = out_dir(T, aj, h, d0);
+                m = movement(h, o);
+                DMDQN_DBG(T.nbr(aj, o) >= 0 || T.exit_id[aj * 4 + o] >= 0, DBG_SIM_EDGE);
+                e2 = next_edge(T, aj, o);
+                // lane_for: connections keep the lane index onto exit / final edges
+                const int w2 = route_advance(d0);
+                mv2 = -1;
+                if (!(e2 >= 4 * A || on_final_edge(w2, e2))) {
+                    const int h2 = opp(e2 & 3);
+                    mv2 = movement(h2, out_dir(T, e2 >> 2, h2, w2));
+                }
+                if (l == tid) rc = RouteCache{d0, m, e2, mv2};
+            }
+            const int k2 = mv2 < 0 ? kf : lane_for_move(mv2, e2, V.cnt);
             const int tl = e2 * 3 + k2;
-            const bool green = (kGreen[V.phase[aj]] >> (d * 4 + m)) & 1;
+            const bool green = (green_mask(V.phase[aj]) >> (d * 4 + m)) & 1;
             if (green) {
                 int nc = V.cnt[tl];
                 if (nc > 0) {
@@ -299,7 +330,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         const int e = l / 3;
         const float len = lane_length(T, e);
         const size_t base = (size_t)l * cap;
-        const int hd = View::kImg ? 0 : V.head[l];
+        const int hd = V.head[l];  // HBM ring head, or the LDS ring head (image)
         // LDS image, long queue: the HBM positions' (x, v) are loaded together
         // here, so their latency overlaps the front and the LDS walk instead of
         // one L2 round trip per vehicle
@@ -311,7 +342,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
                 if (j < no) ov[j] = make_float2(V.x[base + V.C1 + j], V.v[base + V.C1 + j]);
         }
         // front
-        const float2 f0 = View::kImg ? V.xv[l * V.C1] : V.ld(base + hd);
+        const float2 f0 = View::kImg ? V.xv[l * V.C1 + hd] : V.ld(base + hd);
         float lead_x_old = f0.x, lead_v_old = f0.y;
         float lead_x_new = V.fx[l];
         float fvn = V.fv[l];
@@ -329,8 +360,8 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             }
         }
         if constexpr (View::kImg) {
-            if (!pop) V.xv[l * V.C1] = make_float2(lead_x_new, fvn);
-            else V.pdst[l] = V.dst[l * V.C1];  // the leaving front's route word, for pass D
+            if (!pop) V.xv[l * V.C1 + hd] = make_float2(lead_x_new, fvn);
+            else V.pdst[l] = V.dst[l * V.C1 + hd];  // the leaving front's route word, for pass D
         } else {
             if (!pop) V.st(base + hd, make_float2(lead_x_new, fvn));
         }
@@ -364,28 +395,22 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             return lastv2;
         };
         if constexpr (View::kImg) {
-            // positions 1 .. m-1 in LDS (branch-free walk; a popped front shifts
-            // each follower and its route word down one position), then the
-            // HBM positions of a long queue
+            // positions 1 .. m-1: the LDS ring, updated in place; then the HBM
+            // positions of a long queue (after a pop the first of them moves
+            // into the slot the front left, the rest shift down one)
             const int C1 = V.C1, m = n < C1 ? n : C1, sh = pop ? 1 : 0;
             float2 *xl = V.xv + l * C1;
             uint16_t *dl = V.dst + l * C1;
-            float2 nxt = m > 1 ? xl[1] : make_float2(0.0f, 0.0f);
-            // route words ride along (rewritten in place when nothing popped:
-            // no divergent branch in the walk)
-            uint16_t dn = m > 1 ? dl[1] : 0;
+            int sl = hd + 1 == C1 ? 0 : hd + 1;
+            float2 nxt = m > 1 ? xl[sl] : make_float2(0.0f, 0.0f);
             for (int i = 1; i < m; i++) {
                 const float2 cur = nxt;
-                const uint16_t dc = dn;
-                if (i + 1 < m) {
-                    nxt = xl[i + 1];
-                    dn = dl[i + 1];
-                }
-                xl[i - sh] = follow(cur.x, cur.y);
-                dl[i - sh] = dc;
+                const int sc = sl;
+                sl = sl + 1 == C1 ? 0 : sl + 1;
+                if (i + 1 < m) nxt = xl[sl];
+                xl[sc] = follow(cur.x, cur.y);
             }
             if (no > 0) {
-                // a pop shifts the HBM route words too: loaded together first
                 int od[kOvPre];
                 if (sh) {
 #pragma unroll
@@ -395,15 +420,24 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
 #pragma unroll
                 for (int j = 0; j < kOvPre; j++) {
                     if (j < no) {
-                        const int i = C1 + j;
-                        V.putp(l, i - sh, follow(ov[j].x, ov[j].y));
-                        if (sh) V.set_dstp(l, i - 1, od[j]);
+                        const float2 r = follow(ov[j].x, ov[j].y);
+                        const size_t k = base + C1 + j - sh;
+                        if (sh && j == 0) {
+                            xl[hd] = r;
+                            dl[hd] = (uint16_t)od[0];
+                        } else {
+                            V.x[k] = r.x;
+                            V.v[k] = r.y;
+                            if (sh) V.gdst[k] = od[j];
+                        }
                     }
                 }
                 for (int i = C1 + kOvPre; i < n; i++) {  // cap > C1 + kOvPre only
-                    const float2 cur = V.getp(l, i);
-                    V.putp(l, i - sh, follow(cur.x, cur.y));
-                    if (sh) V.set_dstp(l, i - 1, V.dstp(l, i));
+                    const size_t k = base + i;
+                    const float2 r = follow(V.x[k], V.v[k]);
+                    V.x[k - sh] = r.x;
+                    V.v[k - sh] = r.y;
+                    if (sh) V.gdst[k - 1] = V.gdst[k];
                 }
             }
         } else {
@@ -422,7 +456,8 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             }
         }
         if (pop) {
-            if constexpr (!View::kImg) V.head[l] = (hd + 1 == cap) ? 0 : hd + 1;
+            const int ring = View::kImg ? V.C1 : cap;
+            V.head[l] = (hd + 1 == ring) ? 0 : hd + 1;
             V.cnt[l] = n - 1;
         }
         if (n - (pop ? 1 : 0) > 0) V.set_last(l, lastv2);
@@ -514,14 +549,14 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
 
 // LDS image of one env's mutable state (kLDS path): compacted lanes' first C1
 // positions as (x, v) f32 pairs [NL][C1], their u16 route words [NL][C1] and
-// pdst [NL], then cnt, req, gfrom, fx, fv, lastx, lastv [NL], phase, ts [A],
-// qptr [4A], stats [4], q_off [4A+1], last_det [12A].  4x4 grid: 37.4 KB (+1.1 KB
-// of topology) -> four env blocks per CU, all 1024 envs of C3 resident at once
-// (the full-ring image was 65 KB: two per CU, two rounds).
+// pdst [NL], then head, cnt, req, gfrom, fx, fv, lastx, lastv [NL], phase, ts
+// [A], qptr [4A], stats [4], q_off [4A+1], last_det [12A].  4x4 grid: 38.4 KB
+// (+1.1 KB of topology) -> four env blocks per CU, all 1024 envs of C3 resident
+// at once (the full-ring image was 65 KB: two per CU, two rounds).
 __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
     const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
     const int C1 = cap < kLdsPos ? cap : kLdsPos;
-    return (size_t)NL * C1 * 8 + (size_t)NL * (C1 + 1) * 2 + (size_t)NL * 7 * 4 + (size_t)A * 8 +
+    return (size_t)NL * C1 * 8 + (size_t)NL * (C1 + 1) * 2 + (size_t)NL * 8 * 4 + (size_t)A * 8 +
            (size_t)A * 16 + 16 + (size_t)(4 * A + 1) * 4 + (size_t)A * 48;  // q_off, last_det
 }
 
@@ -552,8 +587,8 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         V.xv = reinterpret_cast<float2 *>(dyn);
         V.dst = reinterpret_cast<uint16_t *>(V.xv + NS);
         V.pdst = V.dst + NS;
-        V.head = nullptr;  // compacted lanes: position 0 is the front
-        V.cnt = reinterpret_cast<int32_t *>(V.pdst + NL);  // NL(C1 + 1) u16: NL = 6 * ... is even
+        V.head = reinterpret_cast<int32_t *>(V.pdst + NL);  // NL(C1 + 1) u16: NL = 6 * ... is even
+        V.cnt = V.head + NL;
         V.req = V.cnt + NL;
         V.gfrom = V.req + NL;
         V.fx = reinterpret_cast<float *>(V.gfrom + NL);
@@ -581,6 +616,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
             if (!(h >= 0 && h < cap && n >= 0 && n <= cap)) h = n = 0;
 #endif
             V.cnt[l] = n;
+            V.head[l] = 0;
             const size_t base = (size_t)l * cap;
             if (h != 0 && n > 0) {
                 int g = cap, b = h;  // gcd(cap, h) cycles
@@ -636,7 +672,8 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
     }
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memrealtime();
     prof[6] = prof_t - prof_t0;  // staging
-    for (int k = 0; k < K; k++) substep(V, T, P, t0 + k, qn, prof, prof_t);
+    RouteCache rc{-1, 0, 0, 0};
+    for (int k = 0; k < K; k++) substep(V, T, P, t0 + k, qn, rc, prof, prof_t);
     const int t = t0 + K;
     // halting counts on the observed (incoming) lanes + bookkeeping
     __shared__ int s_running, s_pending;
@@ -684,11 +721,11 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
             G.head[l] = 0;
             G.cnt[l] = n;
             const size_t base = (size_t)l * cap;
-            for (int i = 0; i < n && i < C1; i++) {
-                const float2 a = V.xv[l * C1 + i];
+            for (int i = 0, sl = V.head[l]; i < n && i < C1; i++, sl = sl + 1 == C1 ? 0 : sl + 1) {
+                const float2 a = V.xv[l * C1 + sl];
                 G.x[base + i] = a.x;
                 G.v[base + i] = a.y;
-                G.dst[base + i] = V.dst[l * C1 + i];
+                G.dst[base + i] = V.dst[l * C1 + sl];
             }
         }
         for (int a = tid; a < A; a += nt) {
@@ -823,14 +860,14 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             const int p = s_phase[a], el = t - s_ts[a];
             bool sw;
             if (S.actuated && p == 0) {
-                constexpr uint32_t gl = green_lanes(0x11BB);  // kGreen[0]
+                constexpr uint32_t gl = green_lanes(0x11BB);  // green_mask(0)
                 int last = kNoDetection;
 #pragma unroll
                 for (int k = 0; k < 12; k++)
                     if ((gl >> k) & 1u) last = max(last, s_ldet[a * 12 + k]);
                 sw = el >= kActMax || (el >= kActMin && (float)(t - last) > P.max_gap);
             } else {
-                sw = el >= kPhaseDur[p];
+                sw = el >= phase_dur(p);
             }
             if (sw) {
                 s_phase[a] = (p + 1) % 12;
@@ -876,7 +913,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 const int e2 = next_edge(T, aj, o);
                 const int k2 = lane_for(T, e2, kf, route_advance(d0), s_cnt);
                 const int tl = e2 * 3 + k2;
-                const bool green = (kGreen[s_phase[aj]] >> (d * 4 + m)) & 1;
+                const bool green = (green_mask(s_phase[aj]) >> (d * 4 + m)) & 1;
                 if (green) {
                     if (s_cnt[tl] > 0) {
                         const float xl = s_lx[tl], vl = s_lv[tl];

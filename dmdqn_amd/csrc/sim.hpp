@@ -5,14 +5,25 @@
 namespace dmdqn {
 
 // 12-phase program of every tlLogic in grid_3x3.net.xml:893-906 (actuated
-// min/max of phase 0 ignored: fixed 25 s).
-__constant__ int kPhaseDur[12] = {25, 6, 2, 20, 6, 2, 25, 6, 2, 20, 6, 2};
+// min/max of phase 0 ignored: fixed 25 s): 25, 6, 2, 20, 6, 2, 25, 6, 2, 20,
+// 6, 2.  Computed with selects instead of a table: a per-lane index into a
+// __constant__ array is a vector memory load (L2 latency inside every pass).
+__device__ __forceinline__ int phase_dur(int p) {
+    const int r = p - 3 * (p / 3);
+    return r == 1 ? 6 : r == 2 ? 2 : (p == 3 || p == 9) ? 20 : 25;
+}
 // Green movements per phase: bit (d*4 + m), approach d = 0 n,1 s,2 e,3 w
 // (side the vehicle comes from), movement m = 0 right,1 straight,2 left,
 // 3 U-turn.  'G' and 'g' are green, 'y' and 'r' stop.  Derived from the
 // phase strings with the link layout of grid_3x3.net.xml:1375-1461
-// (per approach: r, s, s, -, l, t).
-__constant__ uint32_t kGreen[12] = {0x11BB, 0, 0, 0x11DD, 0, 0, 0xBB11, 0, 0, 0xDD11, 0, 0};
+// (per approach: r, s, s, -, l, t): phases 0, 3, 6, 9 -> 0x11BB, 0x11DD,
+// 0xBB11, 0xDD11, the rest none.
+__device__ __forceinline__ uint32_t green_mask(int p) {
+    uint32_t g = p == 0 ? 0x11BBu : 0u;
+    g = p == 3 ? 0x11DDu : g;
+    g = p == 6 ? 0xBB11u : g;
+    return p == 9 ? 0xDD11u : g;
+}
 // Actuated mode (dmdqn_sim.actuated): phase 0 carries minDur 5 / maxDur 50
 // (grid_3x3.net.xml:894); the others have no actuation range.
 constexpr int kActMin = 5, kActMax = 50;

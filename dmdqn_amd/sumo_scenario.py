@@ -32,7 +32,7 @@ import numpy as np
 from .scenario import Grid, neighbor
 
 DIR = {"N": 0, "S": 1, "E": 2, "W": 3}
-PHASE_DURATIONS = [25, 6, 2, 20, 6, 2, 25, 6, 2, 20, 6, 2]  # sim.hpp kPhaseDur
+PHASE_DURATIONS = [25, 6, 2, 20, 6, 2, 25, 6, 2, 20, 6, 2]  # sim.hpp phase_dur
 
 _J = re.compile(r"^J_(\d+)_(\d+)$")
 _APPROACH = re.compile(r"^END_([NSEW])_(\d+)_(\d+)_to_J_(\d+)_(\d+)$")
