@@ -8,6 +8,7 @@
 // Draw order contract: per env, agents j = 0..A-1 in junction (J_r_c,
 // row-major) order, exactly as train.py:211-222 / :274-282 iterate them.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.hpp"
 
@@ -136,7 +137,7 @@ __device__ __forceinline__ uint32_t py_randbelow(MTWave &w, uint32_t n) {
 //    on its own u16 pool in LDS (only the swap chain is sequential).
 //  * set branch: out-of-range words and words already selected (LDS bitmap)
 //    are rejected in parallel; a repeat within the chunk is rejected when an
-//    earlier lane holds the same value (lane-shuffle compare); positions in
+//    earlier lane holds the same value (LDS first-lane table); positions in
 //    the sample come from the popcount prefix.
 // In both branches the agent whose k-th pick falls inside a chunk consumes
 // the chunk only up to that lane; the next agent starts at the lane after.
@@ -150,7 +151,7 @@ __device__ __forceinline__ uint64_t lanes_below() {
 }
 
 __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32_t n, int k,
-                                               uint32_t setsize, int first_table, int32_t *idx) {
+                                               uint32_t setsize, int tlog, int32_t *idx) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *mt = smem, *tmp = smem + MT_N, *aux = smem + 2 * MT_N;
     MTWave w{mt, tmp, 0};
@@ -217,13 +218,17 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
     } else {
         uint32_t *bm = aux;  // selected bitmap, n bits
         const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
-        // first[r]: the lowest lane of the current chunk that drew r (all ones
-        // between chunks) -- the in-chunk repeat test in 3 LDS operations
-        // instead of 63 dependent lane shuffles (used when n words fit in LDS)
+        // first[r & (T-1)]: (r >> tlog) << 6 | lowest lane of the current chunk
+        // that drew r (all ones between chunks): the in-chunk repeat test in 3
+        // LDS operations instead of 63 dependent lane shuffles.  T = 2^tlog
+        // entries (<= 32 KB for C3's n = 10000: four sampler blocks per CU, the
+        // 1024 env waves in one round); values r that share a slot resolve in
+        // turn -- the smallest r >> tlog first -- in a wave-uniform loop that
+        // almost always runs once.
         uint32_t *first = bm + words;
+        const uint32_t tmask = (1u << tlog) - 1u;
         for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
-        if (first_table)
-            for (uint32_t t = l; t < n; t += 64) first[t] = 0xffffffffu;
+        for (uint32_t t = l; t <= tmask; t += 64) first[t] = 0xffffffffu;
         __syncthreads();
         int j = 0, i = 0;
         while (j < A) {
@@ -233,20 +238,18 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
             const uint32_t r = getbits(tmp[w.mti + (live ? l : 0)], kb);
             bool cand = live && r < n;
             if (cand) cand = !((bm[r >> 5] >> (r & 31)) & 1u);
-            // a repeat of an earlier candidate lane in the same chunk is rejected
-            bool dup = false;
-            if (first_table) {
-                // one wave: its LDS operations complete in issue order, so the
-                // read sees every lane's min and the reset follows the read
-                if (cand) atomicMin(&first[r], (uint32_t)l);
-                if (cand) dup = first[r] != (uint32_t)l;
-                if (cand) first[r] = 0xffffffffu;
-            } else {
-                const uint32_t key = cand ? r : (0x80000000u | (uint32_t)l);
-                for (int d = 1; d < cnt; d++) {
-                    const uint32_t o = __shfl(key, (l - d) & 63);
-                    dup |= (l >= d) && (o == key);
-                }
+            // a repeat of an earlier candidate lane in the same chunk is rejected.
+            // One wave: its LDS operations complete in issue order, so the read
+            // sees every lane's min and the reset follows every lane's read.
+            bool dup = false, pend = cand;
+            const uint32_t slot = r & tmask, key = ((r >> tlog) << 6) | (uint32_t)l;
+            while (__ballot(pend)) {
+                if (pend) atomicMin(&first[slot], key);
+                const uint32_t win = pend ? first[slot] : 0u;
+                const bool mine = pend && (win >> 6) == (key >> 6);  // the winner drew r too
+                if (mine) dup = win != key;
+                if (pend) first[slot] = 0xffffffffu;
+                pend = pend && !mine;
             }
             const bool a = cand && !dup;
             const uint64_t acc = __ballot(a);
@@ -329,12 +332,22 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
     size_t aux_bytes = pool ? (((size_t)A * k + 1) & ~(size_t)1) * 2 + (size_t)(A < 64 ? A : 64) * n * 2
                             : (size_t)((n + 31) / 32) * 4;
     size_t lds = 2 * MT_N * sizeof(uint32_t) + aux_bytes;
+    // set branch: the first-lane table, 2^tlog u32 entries: no more than n
+    // needs, within 39 KB per block in all (four blocks per CU) when that
+    // leaves at least 4 KB for it, else up to 32 KB; DMDQN_SAMPLE_TLOG caps it
+    // (tests: collisions in every chunk)
+    int tlog = 0;
+    if (!pool) {
+        const size_t quad = 39 * 1024;
+        const size_t room = (quad >= lds + 4096) ? quad - lds : 32 * 1024;
+        while (tlog < 20 && ((size_t)4 << (tlog + 1)) <= room && (1u << tlog) < (uint32_t)n) tlog++;
+        const char *cap = getenv("DMDQN_SAMPLE_TLOG");
+        if (cap && atoi(cap) >= 0 && atoi(cap) < tlog) tlog = atoi(cap);
+        lds += (size_t)4 << tlog;
+    }
     DMDQN_REQUIRE(lds <= 160 * 1024, "dmdqn_replay_sample: n=%d too large for LDS", n);
-    // set branch: the first-lane table (4n bytes) when it fits in 64 KB of LDS
-    const int first_table = !pool && lds + (size_t)n * 4 <= 64 * 1024;
-    if (first_table) lds += (size_t)n * 4;
     hipLaunchKernelGGL(k_sample, dim3(E), dim3(64), lds, as_stream(stream), py_state, A,
-                       (uint32_t)n, k, setsize, first_table, idx);
+                       (uint32_t)n, k, setsize, tlog, idx);
     DMDQN_LAUNCH_CHECK("k_sample");
     return DMDQN_OK;
 }

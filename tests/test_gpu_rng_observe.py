@@ -69,7 +69,8 @@ def test_replay_sample_matches_cpython(n):
 
 @pytest.mark.parametrize("A,n,k", [(64, 200, 128), (70, 300, 32), (3, 21, 5), (3, 22, 5),
                                    (5, 7, 7), (2, 3000, 1000), (64, 10000, 128), (1, 128, 128),
-                                   (4, 20000, 128)])
+                                   (4, 20000, 128), (3, 16385, 128), (2, 40000, 256),
+                                   (2, 100000, 128)])
 def test_replay_sample_shapes(A, n, k):
     """Agent groups beyond one wave (A > 64), small k (setsize 21), k = n and
     large k: every branch and chunk-boundary case of the chunked sampler."""
@@ -81,6 +82,21 @@ def test_replay_sample_shapes(A, n, k):
         for e in range(len(seeds)):
             for j in range(A):
                 np.testing.assert_array_equal(idx[e, j], O.py_sample(refs[e], n, k))
+
+
+@pytest.mark.parametrize("tlog", [0, 3, 6, 10])
+def test_replay_sample_table_collisions(tlog, monkeypatch):
+    """Set branch with the first-lane table capped at 2^tlog entries: values
+    sharing a slot (r = r' mod 2^tlog) in almost every chunk resolve in turn."""
+    monkeypatch.setenv("DMDQN_SAMPLE_TLOG", str(tlog))
+    seeds = [8, 9]
+    st = K.seed_streams(seeds, "py")
+    refs = [O.py_stream(s) for s in seeds]
+    for n in (1046, 10000):
+        idx = K.replay_sample(st, 16, n, 128).cpu().numpy().reshape(len(seeds), 16, 128)
+        for e in range(len(seeds)):
+            for j in range(16):
+                np.testing.assert_array_equal(idx[e, j], O.py_sample(refs[e], n, 128))
 
 
 @pytest.mark.parametrize("grid", [(1, 1), (2, 2), (3, 3), (4, 4), (8, 8), (2, 3)])
