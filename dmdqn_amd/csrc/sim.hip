@@ -180,7 +180,7 @@ struct RouteCache {
     int d0, m, e2, mv2;
 };
 
-template <typename View>
+template <bool kAct, typename View>
 __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, int t,
                                         QNext qn[QSLOTS], RouteCache &rc, uint64_t *prof,
                                         uint64_t &prof_t) {
@@ -372,27 +372,24 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         float2 lastv2 = make_float2(lead_x_new, fvn);
         // one follower: IDM against the old leader state, no overlap with the
         // leader's new position
-        auto follow = [&](float xi, float vi) -> float2 {
+        // (selects, no branches: the LDS walk below runs it for every lane of
+        // the wave up to the wave's longest lane, `act` false past a lane's end)
+        auto follow = [&](float xi, float vi, bool act = true) -> float2 {
             const float gap = (lead_x_old - P.length) - xi;
             const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
-            float vn = clamp_speed(vi + acc, P);
-            float xn = xi + vn;
-            const float lim = lead_x_new - P.length;
-            if (xn > lim) {
-                if (lim < xi) {
-                    xn = xi;
-                    vn = 0.0f;
-                } else {
-                    xn = lim;
-                    vn = lim - xi;
-                }
-            }
-            lastv2 = make_float2(xn, vn);
-            det = det || (xn >= dp && xi < dpl);
-            lead_x_old = xi;
-            lead_v_old = vi;
-            lead_x_new = xn;
-            return lastv2;
+            const float vc = clamp_speed(vi + acc, P);
+            const float xc = xi + vc;
+            const float lim = lead_x_new - P.length, dl = lim - xi;
+            const bool over = xc > lim, back = lim < xi;
+            const float xn = over ? (back ? xi : lim) : xc;
+            const float vn = over ? (back ? 0.0f : dl) : vc;
+            if (kAct) det = det || (act && xn >= dp && xi < dpl);
+            const float2 r = make_float2(xn, vn);
+            lastv2 = act ? r : lastv2;
+            lead_x_old = act ? xi : lead_x_old;
+            lead_v_old = act ? vi : lead_v_old;
+            lead_x_new = act ? xn : lead_x_new;
+            return r;
         };
         if constexpr (View::kImg) {
             // positions 1 .. m-1: the LDS ring, updated in place; then the HBM
@@ -401,14 +398,16 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             const int C1 = V.C1, m = n < C1 ? n : C1, sh = pop ? 1 : 0;
             float2 *xl = V.xv + l * C1;
             uint16_t *dl = V.dst + l * C1;
+            // wave-uniform trip count (ballot): a lane past its end keeps its
+            // state and writes into its own unoccupied ring slots (i < C1)
             int sl = hd + 1 == C1 ? 0 : hd + 1;
-            float2 nxt = m > 1 ? xl[sl] : make_float2(0.0f, 0.0f);
-            for (int i = 1; i < m; i++) {
+            float2 nxt = xl[sl];
+            for (int i = 1; __ballot(i < m); i++) {
                 const float2 cur = nxt;
                 const int sc = sl;
                 sl = sl + 1 == C1 ? 0 : sl + 1;
-                if (i + 1 < m) nxt = xl[sl];
-                xl[sc] = follow(cur.x, cur.y);
+                if (i + 1 < C1) nxt = xl[sl];
+                xl[sc] = follow(cur.x, cur.y, i < m);
             }
             if (no > 0) {
                 int od[kOvPre];
@@ -461,7 +460,7 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
             V.cnt[l] = n - 1;
         }
         if (n - (pop ? 1 : 0) > 0) V.set_last(l, lastv2);
-        if (S.actuated && det && l < 12 * A) V.last_det[l] = t + 1;
+        if (kAct && det && l < 12 * A) V.last_det[l] = t + 1;
     }
     __syncthreads();
     SIM_PROF(3);
@@ -565,7 +564,7 @@ __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
 // pass C walks each lane's vehicles front to back); only occupied positions
 // move between HBM and LDS, and the lanes are written back compacted (head 0).
 // !kLDS: the same passes on global memory rings.
-template <bool kLDS>
+template <bool kLDS, bool kAct>
 __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions,
                                                   int stride, int t0, int K, int max_time,
                                                   int32_t *halt, int32_t *phase_out,
@@ -673,7 +672,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memrealtime();
     prof[6] = prof_t - prof_t0;  // staging
     RouteCache rc{-1, 0, 0, 0};
-    for (int k = 0; k < K; k++) substep(V, T, P, t0 + k, qn, rc, prof, prof_t);
+    for (int k = 0; k < K; k++) substep<kAct>(V, T, P, t0 + k, qn, rc, prof, prof_t);
     const int t = t0 + K;
     // halting counts on the observed (incoming) lanes + bookkeeping
     __shared__ int s_running, s_pending;
@@ -1236,13 +1235,17 @@ extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const 
         DMDQN_LAUNCH_CHECK("k_sim_step_reg");
         return DMDQN_OK;
     }
+    // kAct: the actuated-mode detector bookkeeping is compiled in only when used
+    auto launch = [&](auto kern, size_t bytes) {
+        hipLaunchKernelGGL(kern, dim3(sim->E), dim3(256), bytes, as_stream(stream), *sim, *idm,
+                           actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+    };
     if (use_lds) {
-        hipLaunchKernelGGL(k_sim_step<true>, dim3(sim->E), dim3(256), lds + topo, as_stream(stream),
-                           *sim, *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent,
-                           done);
+        if (sim->actuated) launch(k_sim_step<true, true>, lds + topo);
+        else launch(k_sim_step<true, false>, lds + topo);
     } else {
-        hipLaunchKernelGGL(k_sim_step<false>, dim3(sim->E), dim3(256), topo, as_stream(stream), *sim,
-                           *idm, actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+        if (sim->actuated) launch(k_sim_step<false, true>, topo);
+        else launch(k_sim_step<false, false>, topo);
     }
     DMDQN_LAUNCH_CHECK("k_sim_step");
     return DMDQN_OK;

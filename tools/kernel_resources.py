@@ -10,7 +10,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 LLVM = "/opt/rocm/lib/llvm/bin"
-so = sys.argv[1] if len(sys.argv) > 1 else str(ROOT / "dmdqn_amd/lib/libdmdqn_hip.so")
+so = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] else str(ROOT / "dmdqn_amd/lib/libdmdqn_hip.so")
 filt = sys.argv[2] if len(sys.argv) > 2 else ""
 sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
 from test_isa_cpu import _code_objects  # noqa: E402
