@@ -212,12 +212,16 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
     __syncthreads();
     SIM_PROF(0);
 
-    // ---- A: front vehicles decide
+    // ---- A: front vehicles decide.  One IDM evaluation per front (free
+    // road: no interaction term; green with a vehicle on the target lane: that
+    // vehicle; red/yellow: the stop line), its inputs chosen by selects.
     for (int l = tid; l < NL; l += nt) {
-        V.req[l] = -1;
         V.gfrom[l] = -1;
         int n = V.cnt[l];
-        if (n == 0) continue;
+        if (n == 0) {
+            V.req[l] = -1;
+            continue;
+        }
         const int e = l / 3, kf = l - 3 * e;
         float2 f0;
         int d0;
@@ -233,13 +237,12 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
         }
         const float x0 = f0.x, v0 = f0.y;
         const float len = lane_length(T, e);
-        float acc, vn, xn;
-        if (e >= 4 * A || on_final_edge(d0, e)) {  // exit edge or last edge: free road
-            acc = idm_free(v0, P);
-            vn = clamp_speed(v0 + acc, P);
-            xn = x0 + vn;
-            V.req[l] = kArrive;
-        } else {
+        // exit edge or last edge: free road
+        const bool free_road = e >= 4 * A || on_final_edge(d0, e);
+        bool green = false, lead = false;
+        int tl = -1;
+        float xl = 0.0f, vl = 0.0f;
+        if (!free_road) {
             const int aj = e >> 2, d = e & 3, h = opp(d);
             int m, e2, mv2;
             if (l == tid && rc.d0 == d0) {
@@ -261,35 +264,29 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
                 if (l == tid) rc = RouteCache{d0, m, e2, mv2};
             }
             const int k2 = mv2 < 0 ? kf : lane_for_move(mv2, e2, V.cnt);
-            const int tl = e2 * 3 + k2;
-            const bool green = (green_mask(V.phase[aj]) >> (d * 4 + m)) & 1;
-            if (green) {
-                int nc = V.cnt[tl];
-                if (nc > 0) {
-                    const float2 lt = V.last(tl, nc);
-                    float xl = lt.x, vl = lt.y;
-                    float gap = (len - x0) + (xl - P.length);
-                    acc = idm_acc(v0, gap, v0 - vl, P);
-                } else {
-                    acc = idm_free(v0, P);
-                }
-            } else {
-                float gap = (len - x0) + P.min_gap;
-                acc = idm_acc(v0, gap, v0, P);
-            }
-            vn = clamp_speed(v0 + acc, P);
-            xn = x0 + vn;
-            if (xn > len) {
-                if (green) {
-                    V.req[l] = tl;
-                } else {
-                    xn = len;
-                    vn = 0.0f;
-                }
+            tl = e2 * 3 + k2;
+            green = (green_mask(V.phase[aj]) >> (d * 4 + m)) & 1;
+            const int nc = V.cnt[tl];
+            lead = green && nc > 0;
+            if constexpr (View::kImg) {  // per-lane last-vehicle arrays: always readable
+                xl = V.lastx[tl];
+                vl = V.lastv[tl];
+            } else if (lead) {
+                const float2 lt = V.last(tl, nc);
+                xl = lt.x;
+                vl = lt.y;
             }
         }
-        V.fx[l] = xn;
-        V.fv[l] = vn;
+        const bool nofront = free_road || (green && !lead);
+        const float gap = (len - x0) + (green ? (xl - P.length) : P.min_gap);
+        const float acc = idm_sel(v0, gap, v0 - (lead ? vl : 0.0f), nofront, P);
+        float vn = clamp_speed(v0 + acc, P);
+        float xn = x0 + vn;
+        const bool over = xn > len;
+        V.req[l] = free_road ? kArrive : (over && green ? tl : -1);
+        const bool stop = !free_road && over && !green;
+        V.fx[l] = stop ? len : xn;
+        V.fv[l] = stop ? 0.0f : vn;
     }
     __syncthreads();
     SIM_PROF(1);

@@ -247,6 +247,23 @@ __device__ __forceinline__ float idm_acc(float v, float s, float dv, const IdmK 
     return P.accel * (t1 - q * q);
 }
 
+// idm_acc, or idm_free when nofront, from one evaluation: free road is the
+// same expression without the interaction term, accel * ((1 - r^4) - 0) ==
+// accel * (1 - r^4) exactly; red is idm_acc(v, s, v) = dv of v - 0.
+__device__ __forceinline__ float idm_sel(float v, float s, float dv, bool nofront,
+                                         const IdmK &P) {
+    float r = v * P.inv_vmax;
+    float r2 = r * r;
+    float r4 = r2 * r2;
+    float ss = v * P.tau + (v * dv) * P.inv_two_sqrt_ab;
+    ss = ss < 0.0f ? 0.0f : ss;
+    float sstar = P.min_gap + ss;
+    s = s < 0.01f ? 0.01f : s;
+    float q = sstar / s;
+    float t1 = 1.0f - r4;
+    return P.accel * (t1 - (nofront ? 0.0f : q * q));
+}
+
 __device__ __forceinline__ float clamp_speed(float v, const IdmK &P) {
     if (v < 0.0f) return 0.0f;
     if (v > P.vmax) return P.vmax;
