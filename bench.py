@@ -141,7 +141,7 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
             "unit": "GB/s", "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 5),
             "traffic": traffic, "bytes_per_launch": int(b), "mean_running_vehicles": round(vbar, 1),
             "avg_launch_ms": round(t * 1e3, 4),
-            "timed_over": f"{SIM_PROBE_STEPS} steps after the timed region",
+            "timed_over": f"{SIM_PROBE_STEPS} back-to-back launches after the timed region",
             "note": "latency-bound: the per-env working set is cache-resident; bytes are "
                     "20 B per vehicle-substep as SURVEY 8d defines them"}
 
@@ -270,28 +270,37 @@ def main():
     tr.agent.learn_hook = None
     n_learn = tr.agent.learn_launches - learn_before
 
-    # Sim probe, after the timed region: k_sim_step durations (HIP events on the
-    # stream the sim runs on) and the running vehicles per env after each step
-    # (V-bar for the sim's algorithmic bytes).  Kept out of the timed region:
-    # the extra records and the per-step reduction around the sim cost
-    # 0.1-0.6 ms per step there (measured).
-    sim_starts, sim_ends = [], []
+    # Sim probe, after the timed region.  Timing (the envs advance without
+    # being observed): SIM_PROBE_STEPS k_sim_step launches back to back between
+    # two HIP events on the sim's stream, enqueued behind a GPU sleep so the
+    # host has submitted them all before the first runs (per-launch events
+    # around a sim inside the loop measured 30-80 us more than rocprof's kernel
+    # duration: the event marker and the host's submission land inside them).
+    # Before that, V-bar for the sim's algorithmic bytes: the running vehicles
+    # per env after each of SIM_PROBE_STEPS more training steps, untimed.
+    env = tr.env
+    stream = torch.cuda.current_stream(dev)
     vsum = torch.zeros(E, dtype=torch.int64, device=dev)
-
-    def sim_hook(before):
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record(torch.cuda.current_stream(dev))
-        (sim_starts if before else sim_ends).append(ev)
-        if not before:
-            vsum.add_(tr.env.t_stats[:, 2])
-
-    tr.env.sim_hook = sim_hook
     for _ in range(SIM_PROBE_STEPS):
         tr.step()
-    torch.cuda.synchronize(dev)
-    tr.env.sim_hook = None
-    sim_ms = [s.elapsed_time(e) for s, e in zip(sim_starts, sim_ends)]
+        vsum.add_(env.t_stats[:, 2])
     vbar = float(vsum.double().mean().item()) / SIM_PROBE_STEPS
+    torch.cuda.synchronize(dev)
+
+    def sim_launch():
+        env._ops.sim_step(env._sim_state, env._sim_tables, env._sim_dims, env._idm, None,
+                          env.cfg.action_stride, env.t, env.cfg.step_duration,
+                          env.cfg.max_sim_time, env.halt, env.phase, env.tspent, env.done_u8)
+        env.t += env.cfg.step_duration
+
+    torch.cuda._sleep(int(3e6))  # ~1 ms of GPU time while the launches queue up
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0.record(stream)
+    for _ in range(SIM_PROBE_STEPS):
+        sim_launch()
+    s1.record(stream)
+    torch.cuda.synchronize(dev)
+    sim_ms = [s0.elapsed_time(s1) / SIM_PROBE_STEPS]
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     el_max = D.max_over_ranks(el, device=dev)

@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
     } else {
         uint32_t *bm = aux;  // selected bitmap, n bits
         const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
-        // first[r & (T-1)]: (r >> tlog) << 6 | lowest lane of the current chunk
+        // first[r & (T-1)]: (r >> tlog) << 7 | lowest word of the current chunk
         // that drew r (all ones between chunks): the in-chunk repeat test in 3
         // LDS operations instead of 63 dependent lane shuffles.  T = 2^tlog
         // entries (<= 32 KB for C3's n = 10000: four sampler blocks per CU, the
@@ -230,41 +230,70 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
         for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
         for (uint32_t t = l; t <= tmask; t += 64) first[t] = 0xffffffffu;
         __syncthreads();
+        // Two words per lane per iteration (a 128-word chunk, word q = 64h + l):
+        // half the dependent rounds of LDS traffic per drawn index.
+        constexpr int HW = 2;
         int j = 0, i = 0;
         while (j < A) {
             if (w.mti >= MT_N) w.refill();
-            const int cnt = min(64, MT_N - w.mti);
-            const bool live = l < cnt;
-            const uint32_t r = getbits(tmp[w.mti + (live ? l : 0)], kb);
-            bool cand = live && r < n;
-            if (cand) cand = !((bm[r >> 5] >> (r & 31)) & 1u);
-            // a repeat of an earlier candidate lane in the same chunk is rejected.
-            // One wave: its LDS operations complete in issue order, so the read
-            // sees every lane's min and the reset follows every lane's read.
-            bool dup = false, pend = cand;
-            const uint32_t slot = r & tmask, key = ((r >> tlog) << 6) | (uint32_t)l;
-            while (__ballot(pend)) {
-                if (pend) atomicMin(&first[slot], key);
-                const uint32_t win = pend ? first[slot] : 0u;
-                const bool mine = pend && (win >> 6) == (key >> 6);  // the winner drew r too
-                if (mine) dup = win != key;
-                if (pend) first[slot] = 0xffffffffu;
-                pend = pend && !mine;
+            const int cnt = min(64 * HW, MT_N - w.mti);
+            uint32_t r[HW], slot[HW], key[HW];
+            bool cand[HW], dup[HW], pend[HW];
+#pragma unroll
+            for (int h = 0; h < HW; h++) {
+                const int q = 64 * h + l;
+                const bool live = q < cnt;
+                r[h] = getbits(tmp[w.mti + (live ? q : 0)], kb);
+                cand[h] = live && r[h] < n;
+                if (cand[h]) cand[h] = !((bm[r[h] >> 5] >> (r[h] & 31)) & 1u);
+                slot[h] = r[h] & tmask;
+                key[h] = ((r[h] >> tlog) << 7) | (uint32_t)q;
+                dup[h] = false;
+                pend[h] = cand[h];
             }
-            const bool a = cand && !dup;
-            const uint64_t acc = __ballot(a);
-            const int c = __popcll(acc & lanes_below());
-            const int total = __popcll(acc), need = k - i;
+            // a repeat of an earlier candidate word in the same chunk is rejected.
+            // One wave: its LDS operations complete in issue order, so the reads
+            // see every word's min and the resets follow every read.
+            while (__ballot(pend[0] || pend[1])) {
+#pragma unroll
+                for (int h = 0; h < HW; h++)
+                    if (pend[h]) atomicMin(&first[slot[h]], key[h]);
+                uint32_t win[HW];
+#pragma unroll
+                for (int h = 0; h < HW; h++) win[h] = pend[h] ? first[slot[h]] : 0u;
+#pragma unroll
+                for (int h = 0; h < HW; h++)
+                    if (pend[h]) first[slot[h]] = 0xffffffffu;
+#pragma unroll
+                for (int h = 0; h < HW; h++) {
+                    const bool mine = pend[h] && (win[h] >> 7) == (key[h] >> 7);  // same r
+                    if (mine) dup[h] = win[h] != key[h];
+                    pend[h] = pend[h] && !mine;
+                }
+            }
+            const bool a0 = cand[0] && !dup[0], a1 = cand[1] && !dup[1];
+            const uint64_t acc0 = __ballot(a0), acc1 = __ballot(a1);
+            const int p0 = __popcll(acc0);
+            const int c0 = __popcll(acc0 & lanes_below()), c1 = p0 + __popcll(acc1 & lanes_below());
+            const int total = p0 + __popcll(acc1), need = k - i;
             int taken = total, consumed = cnt;
             if (total >= need) {
-                const uint64_t last = __ballot(a && c == need - 1);
-                consumed = __ffsll((unsigned long long)last);
                 taken = need;
+                if (need <= p0) {
+                    consumed = __ffsll((unsigned long long)__ballot(a0 && c0 == need - 1));
+                } else {
+                    consumed = 64 + __ffsll((unsigned long long)__ballot(a1 && c1 == need - 1));
+                }
             }
-            if (a && c < taken) {
-                DMDQN_DBG(r < n, DBG_SAMPLE);
-                idx[((size_t)e * A + j) * k + i + c] = (int32_t)r;
-                atomicOr(&bm[r >> 5], 1u << (r & 31));
+            if (a0 && c0 < taken) {
+                DMDQN_DBG(r[0] < n, DBG_SAMPLE);
+                idx[((size_t)e * A + j) * k + i + c0] = (int32_t)r[0];
+                atomicOr(&bm[r[0] >> 5], 1u << (r[0] & 31));
+            }
+            if (a1 && c1 < taken) {
+                DMDQN_DBG(r[1] < n, DBG_SAMPLE);
+                idx[((size_t)e * A + j) * k + i + c1] = (int32_t)r[1];
+                atomicOr(&bm[r[1] >> 5], 1u << (r[1] & 31));
             }
             w.mti += consumed;
             i += taken;
