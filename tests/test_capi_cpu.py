@@ -74,6 +74,17 @@ def test_host_side_argument_check_without_gpu(lib):
     assert b"dmdqn_act" in lib.dmdqn_last_error()
 
 
+def test_replay_sample_lds_limit_checked_on_host(lib):
+    """The sampler's LDS plan (MT state + n-bit bitmap + first-lane table) is
+    checked before launch: an n whose bitmap alone exceeds LDS is refused."""
+    dummy = ctypes.c_void_p(16)  # never dereferenced: the check fails first
+    rc = lib.dmdqn_replay_sample(dummy, 1, 1, 2_000_000, 128, dummy, None)
+    assert rc == -1
+    assert b"too large for LDS" in lib.dmdqn_last_error()
+    rc = lib.dmdqn_replay_sample(dummy, 1, 1, 100, 128, dummy, None)  # k > n
+    assert rc == -1 and b"1 <= k <= n" in lib.dmdqn_last_error()
+
+
 def test_debug_build_exports_and_reports_its_variant():
     """Both library variants export the debug entry points; only the
     debug-bounds build says so (no GPU call: the flags are not read here)."""
