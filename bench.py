@@ -287,17 +287,11 @@ def main():
     vbar = float(vsum.double().mean().item()) / SIM_PROBE_STEPS
     torch.cuda.synchronize(dev)
 
-    def sim_launch():
-        env._ops.sim_step(env._sim_state, env._sim_tables, env._sim_dims, env._idm, None,
-                          env.cfg.action_stride, env.t, env.cfg.step_duration,
-                          env.cfg.max_sim_time, env.halt, env.phase, env.tspent, env.done_u8)
-        env.t += env.cfg.step_duration
-
     torch.cuda._sleep(int(3e6))  # ~1 ms of GPU time while the launches queue up
     s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s0.record(stream)
     for _ in range(SIM_PROBE_STEPS):
-        sim_launch()
+        env.advance()
     s1.record(stream)
     torch.cuda.synchronize(dev)
     sim_ms = [s0.elapsed_time(s1) / SIM_PROBE_STEPS]

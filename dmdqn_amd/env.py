@@ -168,6 +168,16 @@ class TrafficEnv:
                                             self.mode)
         return self.obs
 
+    def advance(self):
+        """K substeps for every replica with the signals running their program
+        (no setPhase, no observation): the sim launch alone.  Diagnostics only
+        (bench.py times k_sim_step with it); a training loop calls step()."""
+        cfg = self.cfg
+        self._ops.sim_step(self._sim_state, self._sim_tables, self._sim_dims, self._idm, None,
+                           cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time,
+                           self.halt, self.phase, self.tspent, self.done_u8)
+        self.t += cfg.step_duration
+
     def step(self, actions):
         """One RL step for all replicas (train.py:225-270).
         actions int32 [E,A] on the device.  Returns (obs', reward, done, info):

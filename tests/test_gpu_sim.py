@@ -169,3 +169,29 @@ def test_every_sim_path_matches_oracle(grid, path, monkeypatch):
     actuated mode included."""
     monkeypatch.setenv("DMDQN_SIM_PATH", path)
     _run(*grid, E=3, steps=100, check_every=9, full_state_at=(50,), actuated=(path != "lds"))
+
+
+def test_advance_matches_oracle():
+    """TrafficEnv.advance (the bench's sim probe: K substeps with the signals
+    on their program, no setPhase) is the oracle's step with no actions."""
+    R, C, E, seed = 2, 3, 4, 21
+    env = TrafficEnv(EnvConfig(rows=R, cols=C, num_envs=E, seed=seed))
+    env.reset()
+    refs = [O.OracleEnv(R, C, seed + e) for e in range(E)]
+    rng = np.random.RandomState(seed)
+    t = 0
+    for step in range(12):
+        if step % 3 == 0:  # interleave RL steps (setPhase) with bare advances
+            acts = rng.randint(0, 4, size=(E, R * C)).astype(np.int32)
+            env.step(torch.from_numpy(acts).cuda())
+            outs = [refs[e].step(acts[e], 3, t, 10, 2400) for e in range(E)]
+        else:
+            env.advance()
+            outs = [refs[e].step(None, 3, t, 10, 2400) for e in range(E)]
+        t += 10
+        halt_g, ph_g, ts_g = env.halt.cpu().numpy(), env.phase.cpu().numpy(), env.tspent.cpu().numpy()
+        for e in range(E):
+            np.testing.assert_array_equal(halt_g[e], outs[e][0], err_msg=f"halt env {e} step {step}")
+            np.testing.assert_array_equal(ph_g[e], outs[e][1])
+            np.testing.assert_array_equal(ts_g[e], outs[e][2])
+    assert env.t == t
