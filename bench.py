@@ -287,7 +287,9 @@ def main():
     vbar = float(vsum.double().mean().item()) / SIM_PROBE_STEPS
     torch.cuda.synchronize(dev)
 
-    torch.cuda._sleep(int(3e6))  # ~1 ms of GPU time while the launches queue up
+    gpu_sleep = getattr(torch.cuda, "_sleep", None)
+    if gpu_sleep is not None:
+        gpu_sleep(int(3e6))  # ~1 ms of GPU time while the launches queue up
     s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s0.record(stream)
     for _ in range(SIM_PROBE_STEPS):
