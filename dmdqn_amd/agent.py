@@ -45,10 +45,10 @@ class CLearn(C.Structure):
 # directly (c_learn_args); the product path goes through torch.ops.dmdqn
 _lib.register({
     "dmdqn_learn": [C.POINTER(CLearn), C.c_void_p],
-    "dmdqn_q_argmax": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                       C.c_void_p],
-    "dmdqn_q_argmax_shared": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                              C.c_void_p, C.c_void_p],
+    "dmdqn_q_argmax": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                       C.c_void_p, C.c_void_p],
+    "dmdqn_q_argmax_shared": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                              C.c_void_p, C.c_void_p, C.c_void_p],
     "dmdqn_learn_shared_grad": [C.POINTER(CLearn), C.c_void_p, C.c_int, C.c_void_p, C.c_float,
                                 C.c_void_p],
     "dmdqn_adam": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -342,8 +342,9 @@ class BatchedDQN:
         eps = self.current_epsilon() if eps is None else float(eps)
         greedy = None
         if eps < 1.0:
-            self._ops.q_argmax(self.params, self.H, obs.reshape(self.NA, D_IN).contiguous(),
-                               self.greedy, None, self.shared)
+            self._ops.q_argmax(self.params, self.H, PRECISIONS[self.cfg.precision],
+                               obs.reshape(self.NA, D_IN).contiguous(), self.greedy, None,
+                               self.shared)
             greedy = self.greedy
         self.actions = self._act_bufs[1] if self.actions is self._act_bufs[0] else self._act_bufs[0]
         return K.act(self.np_state, self.A, eps=eps, n_actions=N_ACTIONS, greedy=greedy,

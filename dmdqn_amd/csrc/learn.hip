@@ -126,6 +126,7 @@ struct AdamK {
 // Keras-3 Adam (keras/src/optimizers/adam.py update_step) for one element.
 __device__ __forceinline__ void adam_el(float *w, float *m, float *v, float *tgt, size_t i,
                                         float g, const AdamK &K, bool sync) {
+#pragma clang fp contract(off)  // each op rounded as TF's separate kernels
     float mi = m[i], vi = v[i], wi = w[i];
     mi = mi + (g - mi) * K.c1;
     vi = vi + (g * g - vi) * K.c2;
@@ -400,33 +401,45 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
 }
 
 // ------------------------------------------------------------------ greedy act
-template <int H>
+// The online forward of select_action's greedy branch (dqn_agent.py:268-273)
+// under the learn's precision policy: PREC 0 f32; 1 / 2 Keras mixed_float16 /
+// mixed_bfloat16 (learn_h16.hpp): weights, biases and inputs cast to 16 bits,
+// f32 sums, each matmul result rounded, the bias add rounded again, 16-bit
+// Q values -- so the argmax (first max) sees the values Keras' would.
+template <int PREC>
+__device__ __forceinline__ float rq(float x) {
+    if constexpr (PREC == 1) return (float)(_Float16)x;
+    else if constexpr (PREC == 2) return (float)(__bf16)x;
+    else return x;
+}
+
+template <int H, int PREC>
 __global__ void __launch_bounds__(256) k_q_argmax(const float *params, size_t pstride,
                                                   const float *obs, int32_t *out, float *q_out) {
     using L = Lay<H>;
     __shared__ float x[D_], h1[H], h2[H], q[NACT];
     const int agent = blockIdx.x, tid = threadIdx.x;
     const float *Wp = params + (size_t)agent * pstride;  // pstride 0: one shared net
-    for (int i = tid; i < D_; i += blockDim.x) x[i] = obs[(size_t)agent * D_ + i];
+    for (int i = tid; i < D_; i += blockDim.x) x[i] = rq<PREC>(obs[(size_t)agent * D_ + i]);
     __syncthreads();
     for (int j = tid; j < H; j += blockDim.x) {
         float s = 0.0f;
-        for (int i = 0; i < D_; i++) s += x[i] * Wp[L::oW1T + qn_w1<H>(j, i)];
-        s += Wp[L::ob1 + j];
+        for (int i = 0; i < D_; i++) s += x[i] * rq<PREC>(Wp[L::oW1T + qn_w1<H>(j, i)]);
+        s = rq<PREC>(rq<PREC>(s) + rq<PREC>(Wp[L::ob1 + j]));
         h1[j] = s > 0.0f ? s : 0.0f;
     }
     __syncthreads();
     for (int k = tid; k < H; k += blockDim.x) {
         float s = 0.0f;
-        for (int j = 0; j < H; j++) s += h1[j] * Wp[L::oW2T + qn_wt(k, j, H)];
-        s += Wp[L::ob2 + k];
+        for (int j = 0; j < H; j++) s += h1[j] * rq<PREC>(Wp[L::oW2T + qn_wt(k, j, H)]);
+        s = rq<PREC>(rq<PREC>(s) + rq<PREC>(Wp[L::ob2 + k]));
         h2[k] = s > 0.0f ? s : 0.0f;
     }
     __syncthreads();
     if (tid < NACT) {
         float s = 0.0f;
-        for (int k = 0; k < H; k++) s += h2[k] * Wp[L::oW3T + tid * H + k];
-        q[tid] = s + Wp[L::ob3 + tid];
+        for (int k = 0; k < H; k++) s += h2[k] * rq<PREC>(Wp[L::oW3T + tid * H + k]);
+        q[tid] = rq<PREC>(rq<PREC>(s) + rq<PREC>(Wp[L::ob3 + tid]));
     }
     __syncthreads();
     if (tid == 0) {
@@ -475,17 +488,23 @@ extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
     return DMDQN_OK;
 }
 
-static int q_argmax(const float *params, size_t pstride, int NA, int P, int hidden,
+template <int H>
+static void launch_q_argmax(int precision, int NA, const float *params, size_t pstride,
+                            const float *obs, int32_t *out, float *q_out, void *stream) {
+    auto k = precision == 1 ? k_q_argmax<H, 1> : precision == 2 ? k_q_argmax<H, 2> : k_q_argmax<H, 0>;
+    hipLaunchKernelGGL(k, dim3(NA), dim3(H), 0, as_stream(stream), params, pstride, obs, out, q_out);
+}
+
+static int q_argmax(const float *params, size_t pstride, int NA, int P, int hidden, int precision,
                     const float *obs, int32_t *out, float *q_out, void *stream) {
     DMDQN_REQUIRE(params && obs && out && NA > 0, "dmdqn_q_argmax: bad args");
+    DMDQN_REQUIRE(precision >= 0 && precision <= 2, "dmdqn_q_argmax: precision %d", precision);
     if (hidden == 128) {
         DMDQN_REQUIRE(P == Lay<128>::P, "dmdqn_q_argmax: P");
-        hipLaunchKernelGGL(k_q_argmax<128>, dim3(NA), dim3(128), 0, as_stream(stream), params,
-                           pstride, obs, out, q_out);
+        launch_q_argmax<128>(precision, NA, params, pstride, obs, out, q_out, stream);
     } else if (hidden == 64) {
         DMDQN_REQUIRE(P == Lay<64>::P, "dmdqn_q_argmax: P");
-        hipLaunchKernelGGL(k_q_argmax<64>, dim3(NA), dim3(64), 0, as_stream(stream), params,
-                           pstride, obs, out, q_out);
+        launch_q_argmax<64>(precision, NA, params, pstride, obs, out, q_out, stream);
     } else {
         DMDQN_REQUIRE(false, "dmdqn_q_argmax: hidden must be 64 or 128");
     }
@@ -493,14 +512,14 @@ static int q_argmax(const float *params, size_t pstride, int NA, int P, int hidd
     return DMDQN_OK;
 }
 
-extern "C" int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, const float *obs,
-                              int32_t *out, float *q_out, void *stream) {
-    return q_argmax(params, (size_t)P, NA, P, hidden, obs, out, q_out, stream);
+extern "C" int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, int precision,
+                              const float *obs, int32_t *out, float *q_out, void *stream) {
+    return q_argmax(params, (size_t)P, NA, P, hidden, precision, obs, out, q_out, stream);
 }
 
-extern "C" int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden,
+extern "C" int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, int precision,
                                      const float *obs, int32_t *out, float *q_out, void *stream) {
-    return q_argmax(params, 0, NA, P, hidden, obs, out, q_out, stream);
+    return q_argmax(params, 0, NA, P, hidden, precision, obs, out, q_out, stream);
 }
 
 // Hard target sync outside a learn (dqn_agent.py:382-387, update_target_network):

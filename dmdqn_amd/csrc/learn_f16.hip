@@ -148,6 +148,7 @@ __global__ void __launch_bounds__(256) k_adam(float *W, float *M, float *V, floa
                                               _Float16 *TH, _Float16 *WH, const float *G, int n,
                                               float gscale,
                                               float alpha, float c1, float c2, float eps, int sync) {
+#pragma clang fp contract(off)  // each op rounded as TF's separate kernels
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float g = G[i] * gscale;

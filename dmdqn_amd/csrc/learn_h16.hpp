@@ -3,8 +3,15 @@
 // reference's tf.keras mixed_float16 policy, train.py:61) and learn_bf16.hip
 // (bf16, v_mfma_f32_16x16x32_bf16: the same algorithm under a mixed_bfloat16
 // policy, BASELINE config C2).  Both keep f32 accumulation and f32 master
-// weights + Adam slots; every value Keras would cast to the compute dtype
-// (weights, activations, Q, dL/dQ, activation gradients) is rounded to h16.
+// weights + Adam slots, and round where Keras 3 / TF do under the mixed
+// policy (tests/golden/tf_shim.py states the sources; tests/golden/
+// learn_mixed.npz is the reference's own learn run that way):
+//   * weights and biases: the f32 variables cast to h16 at each use;
+//   * Dense: z = h16(h16(x W) + b) -- the matmul result is rounded, then the
+//     16-bit bias add rounds again; relu; Q is the h16 output of layer 3;
+//   * dL/dQ rounded to h16 (the gradient of the learn's tf.cast);
+//   * dH = h16(dZ W^T) masked by relu; dW = h16(X^T dZ), db = h16(sum dZ):
+//     the gradients Adam receives are 16-bit values (no loss scaling).
 // The includer defines DMDQN_H16_BF16 (0 or 1) first.
 //
 // One workgroup (8 waves) per agent, TWO workgroups per CU: 74 KB of LDS and
@@ -224,9 +231,18 @@ __device__ __forceinline__ half8 w1frag(const h16 *W1, int n0, int s) {
 }
 
 __device__ __forceinline__ float4 ld_bias4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float r16(float x) { return (float)(h16)x; }
+// A bias read for a forward: the f32 variable cast to h16 (Keras' autocast),
+// kept packed (2 VGPRs for 4 neurons).
+__device__ __forceinline__ half4v ld_bias4_h(const float *p) {
+    return __builtin_convertvector(*reinterpret_cast<const f32x4 *>(p), half4v);
+}
 __device__ __forceinline__ float4 ld_bias4(const h16 *p) {
     const half4v h = *reinterpret_cast<const half4v *>(p);
     return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+}
+__device__ __forceinline__ half4v ld_bias4_h(const h16 *p) {
+    return *reinterpret_cast<const half4v *>(p);
 }
 
 __device__ __forceinline__ half8 ones8() {
@@ -249,7 +265,7 @@ struct Scratch {
 // network runs (the online net serves both the S' and the S forward).
 struct Frags {
     half8 w1[3], w2[4];
-    float4 b1, b2;
+    half4v b1, b2;
 };
 
 // The output layer (4 x 128) of a network as an f16 LDS image + f32 bias,
@@ -266,7 +282,7 @@ __device__ __forceinline__ void load_w1(const T *Wg, Frags &f) {
     const int w = threadIdx.x >> 6, lg = (threadIdx.x & 63) >> 4;
 #pragma unroll
     for (int s = 0; s < 3; s++) f.w1[s] = w1frag(Wg + L::oW1T, 16 * w, s);
-    f.b1 = ld_bias4(Wg + L::ob1 + 16 * w + 4 * lg);
+    f.b1 = ld_bias4_h(Wg + L::ob1 + 16 * w + 4 * lg);
 }
 
 template <typename T>
@@ -274,7 +290,7 @@ __device__ __forceinline__ void load_w2(const T *Wg, Frags &f) {
     const int w = threadIdx.x >> 6, lg = (threadIdx.x & 63) >> 4;
 #pragma unroll
     for (int s = 0; s < 4; s++) f.w2[s] = wfrag(Wg + L::oW2T, H, 16 * w, 32 * s);
-    f.b2 = ld_bias4(Wg + L::ob2 + 16 * w + 4 * lg);
+    f.b2 = ld_bias4_h(Wg + L::ob2 + 16 * w + 4 * lg);
 }
 
 // Stage W3T (f16) and b3 of one network into LDS (threads 0..127; caller syncs).
@@ -287,7 +303,7 @@ __device__ __forceinline__ void stage_out(const T *Wg, h16 *w3, float *b3) {
         hv[0] = (h16)v.x; hv[1] = (h16)v.y; hv[2] = (h16)v.z; hv[3] = (h16)v.w;
         *reinterpret_cast<half4v *>(w3 + 4 * t) = hv;
     } else if (t < NACT * H / 4 + NACT) {
-        b3[t - NACT * H / 4] = (float)Wg[L::ob3 + t - NACT * H / 4];
+        b3[t - NACT * H / 4] = (float)(h16)Wg[L::ob3 + t - NACT * H / 4];
     }
 }
 
@@ -301,12 +317,14 @@ struct NoHook {
     __device__ void operator()(Frags &) const {}
 };
 
-__device__ __forceinline__ half4v relu_h4(f32x4 acc, float4 b) {
+// Dense + relu under the mixed policy: relu(h16(h16(acc) + b)) -- the
+// matmul result rounded, then the correctly rounded 16-bit bias add (f16:
+// packed v_pk_add_f16; bf16: an f32 add rounded once, the same value).
+__device__ __forceinline__ half4v relu_h4(f32x4 acc, half4v b) {
+    const half4v z = __builtin_convertvector(acc, half4v) + b;
     half4v hv;
-    hv[0] = (h16)fmaxf(acc[0] + b.x, 0.0f);
-    hv[1] = (h16)fmaxf(acc[1] + b.y, 0.0f);
-    hv[2] = (h16)fmaxf(acc[2] + b.z, 0.0f);
-    hv[3] = (h16)fmaxf(acc[3] + b.w, 0.0f);
+#pragma unroll
+    for (int e = 0; e < 4; e++) hv[e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
     return hv;
 }
 
@@ -345,7 +363,7 @@ __device__ void forward_x(Frags &f, const OutL o, const h16 *X, h16 *H1b, h16 *H
             for (int s = 0; s < 4; s++) c = mfma(f.w2[s], frag_row_h(H1b, 16 * t, 32 * s), c);
             acc[t] = c;
         }
-        const float4 b2 = f.b2;
+        const half4v b2 = f.b2;
         after_l2(f);
         __syncthreads();  // every wave has read H1
 #pragma unroll
@@ -376,14 +394,29 @@ __device__ void forward_x(Frags &f, const OutL o, const h16 *X, h16 *H1b, h16 *H
         }
         if (lg == 0) {
             float4 q;
-            q.x = (float)(h16)(acc[0] + o.b3[0]);
-            q.y = (float)(h16)(acc[1] + o.b3[1]);
-            q.z = (float)(h16)(acc[2] + o.b3[2]);
-            q.w = (float)(h16)(acc[3] + o.b3[3]);
+            q.x = r16(r16(acc[0]) + o.b3[0]);
+            q.y = r16(r16(acc[1]) + o.b3[1]);
+            q.z = r16(r16(acc[2]) + o.b3[2]);
+            q.w = r16(r16(acc[3]) + o.b3[3]);
             *reinterpret_cast<float4 *>(qout + (16 * w + lr) * NACT) = q;
         }
     }
     __syncthreads();
+}
+
+// A gradient entry as Adam receives it under the mixed policy: 16-bit.
+__device__ __forceinline__ float gval(const f32x4 &g, int e) { return r16(g[e]); }
+
+// Keras-3 Adam (keras/src/optimizers/adam.py update_step) on one parameter,
+// every op rounded on its own as TF's separate elementwise kernels do: no fma
+// contraction (this file is built with -ffp-contract=fast for the MFMA
+// epilogues), correctly rounded sqrt and divide (HIP's default).
+__device__ __forceinline__ void adam_el(float &w, float &m, float &v, float g, float alpha,
+                                        float c1, float c2, float eps) {
+#pragma clang fp contract(off)
+    m = m + (g - m) * c1;
+    v = v + (g * g - v) * c2;
+    w = w - (m * alpha) / (sqrtf(v) + eps);
 }
 
 struct AdamC {
@@ -412,12 +445,8 @@ __device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, c
     for (int q = 0; q < NT; q++) {
         float *pw = &w[q].x, *pm = &m[q].x, *pv = &v[q].x;
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            float ge = g[q][e];
-            pm[e] = pm[e] + (ge - pm[e]) * k.c1;
-            pv[e] = pv[e] + (ge * ge - pv[e]) * k.c2;
-            pw[e] = pw[e] - (pm[e] * k.alpha) / (sqrtf(pv[e]) + k.eps);
-        }
+        for (int e = 0; e < 4; e++)
+            adam_el(pw[e], pm[e], pv[e], gval(g[q], e), k.alpha, k.c1, k.c2, k.eps);
     }
 #pragma unroll
     for (int q = 0; q < NT; q++) {
@@ -468,9 +497,10 @@ struct AllValid {
     __device__ constexpr bool operator()(int) const { return true; }
 };
 
-template <int NB, int NT, bool EARLY, typename Index, typename Grad, typename Valid = AllValid>
+template <int NB, int NT, bool EARLY, typename Index, typename GT, typename Grad,
+          typename Valid = AllValid>
 __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T, Index ix,
-                                          const f32x4 *g, const AdamC &k, Grad grad,
+                                          const GT *g, const AdamC &k, Grad grad,
                                           Valid valid = {}) {
     float4 w[2][NT], m[2][NT], v[2][NT];
     if constexpr (!EARLY) grad();
@@ -508,14 +538,10 @@ __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T
 #pragma unroll
         for (int q = 0; q < NT; q++) {
             float *pw = &w[c][q].x, *pm = &m[c][q].x, *pv = &v[c][q].x;
-            const f32x4 gq = g[h * NT + q];
+            const GT gq = g[h * NT + q];
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const float ge = gq[e];
-                pm[e] = pm[e] + (ge - pm[e]) * k.c1;
-                pv[e] = pv[e] + (ge * ge - pv[e]) * k.c2;
-                pw[e] = pw[e] - (pm[e] * k.alpha) / (sqrtf(pv[e]) + k.eps);
-            }
+            for (int e = 0; e < 4; e++)
+                adam_el(pw[e], pm[e], pv[e], gval(gq, e), k.alpha, k.c1, k.c2, k.eps);
         }
 #pragma unroll
         for (int q = 0; q < NT; q++) {
@@ -545,9 +571,7 @@ __device__ __forceinline__ void adam4(float *W, float *M, float *V, float *T, si
 __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, size_t i, float g,
                                       const AdamC &k) {
     float m = M[i], v = V[i], w = W[i];
-    m = m + (g - m) * k.c1;
-    v = v + (g * g - v) * k.c2;
-    w = w - (m * k.alpha) / (sqrtf(v) + k.eps);
+    adam_el(w, m, v, r16(g), k.alpha, k.c1, k.c2, k.eps);  // the 16-bit gradient
     M[i] = m;
     V[i] = v;
     W[i] = w;
@@ -816,7 +840,9 @@ __device__ __forceinline__ void bwd_dh1(h16 *R1, const h16 *R2, const Frags &fr,
 
 // dZ1 = dH1 masked by ReLU(H1) -> R1 (lane: neurons j..j+3 of row b).
 __device__ __forceinline__ void bwd_dz1(h16 *R1, const uint32_t *mask, const f32x4 d1[8]) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
+    // lane ids from fresh_tid: the addresses are recomputed here instead of
+    // being kept (or spilled) from the forwards that use the same expressions
+    const int tx = fresh_tid(), w = tx >> 6, l = tx & 63, lr = l & 15, lg = l >> 4;
     const int j = 16 * w + 4 * lg;
 #pragma unroll
     for (int t = 0; t < 8; t++) {
@@ -928,12 +954,8 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
         if (lr < NACT) {
             float *pw = &w3.x, *pm = &m3.x, *pv = &v3.x;
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const float ge = acc[e];
-                pm[e] = pm[e] + (ge - pm[e]) * AK.c1;
-                pv[e] = pv[e] + (ge * ge - pv[e]) * AK.c2;
-                pw[e] = pw[e] - (pm[e] * AK.alpha) / (sqrtf(pv[e]) + AK.eps);
-            }
+            for (int e = 0; e < 4; e++)
+                adam_el(pw[e], pm[e], pv[e], r16(acc[e]), AK.alpha, AK.c1, AK.c2, AK.eps);
             *reinterpret_cast<float4 *>(Wp + i3) = w3;
             *reinterpret_cast<float4 *>(Mp + i3) = m3;
             *reinterpret_cast<float4 *>(Vp + i3) = v3;

@@ -311,8 +311,8 @@ void target_sync(const Tensor &params, Tensor &target, const OptT &target_h, int
           "dmdqn_target_sync");
 }
 
-void q_argmax(const Tensor &params, int64_t hidden, const Tensor &obs, Tensor &out, const OptT &q,
-              bool shared) {
+void q_argmax(const Tensor &params, int64_t hidden, int64_t precision, const Tensor &obs,
+              Tensor &out, const OptT &q, bool shared) {
     const int64_t NA = out.numel();
     const int64_t P = shared ? params.numel() : params.numel() / NA;
     auto p = dptr<float>(params, at::kFloat, "params");
@@ -320,9 +320,10 @@ void q_argmax(const Tensor &params, int64_t hidden, const Tensor &obs, Tensor &o
     auto g = dptr<int32_t>(out, at::kInt, "out", NA);
     auto qq = optr<float>(q, at::kFloat, "q", NA * 4);
     c10::hip::HIPGuardMasqueradingAsCUDA gd(params.device());
-    check(shared ? dmdqn_q_argmax_shared(p, (int)NA, (int)P, (int)hidden, o, g, qq,
+    check(shared ? dmdqn_q_argmax_shared(p, (int)NA, (int)P, (int)hidden, (int)precision, o, g, qq,
                                          stream_of(params))
-                 : dmdqn_q_argmax(p, (int)NA, (int)P, (int)hidden, o, g, qq, stream_of(params)),
+                 : dmdqn_q_argmax(p, (int)NA, (int)P, (int)hidden, (int)precision, o, g, qq,
+                                  stream_of(params)),
           "dmdqn_q_argmax");
 }
 
@@ -351,7 +352,7 @@ void learn_shared_grad_meta(const Tensor &, const Tensor &, const Tensor &, cons
 void adam_meta(Tensor &, Tensor &, Tensor &, Tensor &, const OptT &, const OptT &, const Tensor &,
                double, double, double, double, double, bool) {}
 void target_sync_meta(const Tensor &, Tensor &, const OptT &, int64_t) {}
-void q_argmax_meta(const Tensor &, int64_t, const Tensor &, Tensor &, const OptT &, bool) {}
+void q_argmax_meta(const Tensor &, int64_t, int64_t, const Tensor &, Tensor &, const OptT &, bool) {}
 
 }  // namespace
 
@@ -397,8 +398,8 @@ TORCH_LIBRARY(dmdqn, m) {
     // DQNAgent.update_target_network (dqn_agent.py:382-387)
     m.def("target_sync(Tensor params, Tensor(a!) target, Tensor(b!)? target_h, int precision) -> ()");
     // the greedy branch of select_action (dqn_agent.py:268-273)
-    m.def("q_argmax(Tensor params, int hidden, Tensor obs, Tensor(a!) out, Tensor(b!)? q, "
-          "bool shared) -> ()");
+    m.def("q_argmax(Tensor params, int hidden, int precision, Tensor obs, Tensor(a!) out, "
+          "Tensor(b!)? q, bool shared) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmdqn, CUDA, m) {

@@ -254,14 +254,17 @@ int dmdqn_learn(const dmdqn_learn_args *args, void *stream);
 int dmdqn_target_sync(const float *params, float *target, uint16_t *target_h, int NW, int P,
                       int Ph, int precision, void *stream);
 
-/* Greedy actions argmax_a Q_online(obs) for NA agents (dqn_agent.py:268-273);
- * obs f32 [NA][89]; out int32 [NA].  Used by dmdqn_act when eps < 1. */
-int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, const float *obs,
-                   int32_t *out, float *q_out, void *stream);
+/* Greedy actions argmax_a Q_online(obs) for NA agents (dqn_agent.py:268-273,
+ * first max on ties); obs f32 [NA][89]; out int32 [NA]; q_out (optional)
+ * f32 [NA][4].  precision as dmdqn_learn: 0 f32; 1 / 2 the forward Keras runs
+ * under mixed_float16 / mixed_bfloat16 (16-bit weights and activations, f32
+ * sums, 16-bit Q).  Used by dmdqn_act when eps < 1. */
+int dmdqn_q_argmax(const float *params, int NA, int P, int hidden, int precision,
+                   const float *obs, int32_t *out, float *q_out, void *stream);
 
 /* dmdqn_q_argmax with ONE parameter set shared by all NA agents (C5). */
-int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, const float *obs,
-                          int32_t *out, float *q_out, void *stream);
+int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, int precision,
+                          const float *obs, int32_t *out, float *q_out, void *stream);
 
 /* ------------------------------------------------------------------ shared-parameter DQN
  * Configuration C5 (NOT in the reference, which trains one network

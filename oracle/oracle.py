@@ -326,6 +326,111 @@ def learn(p, target, m, v, S, A, Rn, S2, Dn, t, gamma=0.99, lr=1e-3, H1=128, H2=
     return (loss, grad) if want_grad else loss
 
 
+def round_f16(x):
+    """f32 -> IEEE half -> f32, round to nearest even."""
+    return np.asarray(x, np.float32).astype(np.float16).astype(np.float32)
+
+
+def round_bf16(x):
+    """f32 -> bfloat16 -> f32, round to nearest even (finite inputs)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32)
+
+
+MIXED_ROUND = {"fp16": round_f16, "bf16": round_bf16}
+
+
+def _mixed_split(w, rnd, H):
+    sizes = [89 * H, H, H * H, H, H * 4, 4]
+    offs = np.cumsum([0] + sizes)
+    W1, b1, W2, b2, W3, b3 = (np.asarray(w[offs[i]:offs[i + 1]], np.float32) for i in range(6))
+    return (rnd(W1.reshape(89, H)), rnd(b1), rnd(W2.reshape(H, H)), rnd(b2),
+            rnd(W3.reshape(H, 4)), rnd(b3))
+
+
+def _mixed_fwd(ws, X, rnd):
+    def dense(x, W, b):
+        return rnd(rnd(np.matmul(x, W, dtype=np.float32)) + b)
+    W1, b1, W2, b2, W3, b3 = ws
+    h1 = np.maximum(dense(X, W1, b1), 0)
+    h2 = np.maximum(dense(h1, W2, b2), 0)
+    return h1, h2, dense(h2, W3, b3)
+
+
+def qnet_forward_mixed(p, x, precision="fp16", H=128):
+    """The Keras Sequential forward under mixed_float16 / mixed_bfloat16 on
+    Keras-order flat f32 weights: 16-bit Q [B, 4] (as f32 values); see learn_mixed."""
+    rnd = MIXED_ROUND[precision]
+    return _mixed_fwd(_mixed_split(p, rnd, H), rnd(np.asarray(x, np.float32)), rnd)[2]
+
+
+def learn_mixed(p, target, m, v, S, A, Rn, S2, Dn, t, precision="fp16", gamma=0.99, lr=1e-3,
+                H=128, loss_kind=0, round_grad=True, want_grad=False, w3_bwd=None):
+    """DQNAgent.learn (dqn_agent.py:328-380) under Keras 3's mixed precision
+    policy (train.py:61 sets mixed_float16; "bf16" = mixed_bfloat16), in numpy,
+    on Keras-order flat f32 parameters (TEST INFRASTRUCTURE, the checker of the
+    16-bit learn kernels).  In place on p, m, v; returns the f32 loss (and the
+    f32-widened gradient with want_grad).
+
+    Rounding points (rnd = round to the 16-bit compute type; every matmul is
+    f32 products + f32 sums, rounded once; tests/golden/tf_shim.py states the
+    Keras / TF sources):
+      Dense:   z = rnd(rnd(x @ rnd(W)) + rnd(b)), h = relu(z)      (3 layers)
+      Q (f16) -> argmax (first max) of online(S'); target(S')[a*] widened;
+      y = Rn + (gamma (1 - d)) q_t  and  the MSE / Huber loss in f32;
+      dQ = rnd(dL/dq) at the taken action (the gradient of tf.cast);
+      dW = rnd(h_in^T @ dZ), db = rnd(sum_batch dZ), dh_in = rnd(dZ @ rnd(W)^T),
+      dZ = dh * (h > 0);  Adam (Keras 3) in f32 on the widened gradients.
+    round_grad=False keeps dW / db in f32 (the shared-network configuration
+    C5 sums its per-agent gradients before any rounding).  w3_bwd [H, 4]
+    replaces the W3 backprop multiplies dQ by (a test hook)."""
+    rnd = MIXED_ROUND[precision]
+    f32 = np.float32
+
+    def split(w):
+        return _mixed_split(w, rnd, H)
+
+    def fwd(ws, X):
+        return _mixed_fwd(ws, X, rnd)
+
+    S, S2 = rnd(np.asarray(S, f32)), rnd(np.asarray(S2, f32))
+    Rn, Dn = np.asarray(Rn, f32), np.asarray(Dn, f32)
+    A = np.asarray(A, np.int64)
+    B = S.shape[0]
+    rows = np.arange(B)
+    wo, wt = split(np.asarray(p, f32)), split(np.asarray(target, f32))
+    a_star = fwd(wo, S2)[2].argmax(1)
+    q_t = fwd(wt, S2)[2][rows, a_star]
+    y = Rn + (f32(gamma) * (f32(1.0) - Dn)) * q_t
+    h1, h2, q = fwd(wo, S)
+    e = q[rows, A] - y
+    if loss_kind == 1:
+        ae = np.abs(e)
+        loss = np.mean(np.where(ae <= 1, f32(0.5) * e * e, ae - f32(0.5)), dtype=f32)
+        dq = np.where(ae <= 1, e, np.sign(e)).astype(f32) * f32(1.0 / B)
+    else:
+        loss = np.mean(e * e, dtype=f32)
+        dq = f32(2.0) * e * f32(1.0 / B)
+    DQ = np.zeros((B, 4), f32)
+    DQ[rows, A] = rnd(dq)
+    W1, b1, W2, b2, W3, b3 = wo
+    gr = rnd if round_grad else (lambda x: np.asarray(x, f32))
+    gW3, gb3 = gr(np.matmul(h2.T, DQ, dtype=f32)), gr(DQ.sum(0, dtype=f32))
+    if w3_bwd is not None:
+        W3 = rnd(np.asarray(w3_bwd, f32))
+    dz2 = np.where(h2 > 0, rnd(np.matmul(DQ, W3.T, dtype=f32)), f32(0))
+    gW2, gb2 = gr(np.matmul(h1.T, dz2, dtype=f32)), gr(dz2.sum(0, dtype=f32))
+    dz1 = np.where(h1 > 0, rnd(np.matmul(dz2, W2.T, dtype=f32)), f32(0))
+    gW1, gb1 = gr(np.matmul(S.T, dz1, dtype=f32)), gr(dz1.sum(0, dtype=f32))
+    g = np.concatenate([gW1.ravel(), gb1, gW2.ravel(), gb2, gW3.ravel(), gb3]).astype(f32)
+    alpha, c1, c2, eps = keras_adam_consts(t, lr)
+    m += (g - m) * c1
+    v += (g * g - v) * c2
+    p -= (m * alpha) / (np.sqrt(v) + eps)
+    return (f32(loss), g) if want_grad else f32(loss)
+
+
 def keras_init(rng, H1=128, H2=128, NA=4):
     """HeNormal (truncated, stddev sqrt(2/fan_in)/0.8796) hidden kernels,
     GlorotUniform output kernel, zero biases (dqn_agent.py:160-181)."""

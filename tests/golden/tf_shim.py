@@ -23,12 +23,38 @@ semantics:
   Adam             keras/src/optimizers/adam.py update_step:
                    m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);
                    w -= m * alpha / (sqrt(v) + eps),
-                   alpha = lr sqrt(1 - b2^t) / (1 - b1^t), constants in f32
+                   alpha = lr sqrt(1 - b2^t) / (1 - b1^t), constants in f32,
+                   sqrt correctly rounded
   reduce_std       population standard deviation
 
-Everything is fp32 (the reference sets mixed_float16 in train.py:61; the shim
-does not emulate that policy -- the fp32 fixture pins the fp32 oracle, and the
-16-bit kernels are checked against it with stated tolerances).
+Precision policy.  By default everything is fp32.  After
+keras.mixed_precision.set_global_policy("mixed_float16") -- what train.py:61
+does at import -- (or "mixed_bfloat16") the Dense layers built afterwards follow
+Keras 3's mixed-precision semantics (keras/src/layers/layer.py __call__ input
+autocast + AutocastScope; keras/src/layers/core/dense.py call):
+
+  * the layer casts its floating input to the compute dtype (f16 / bf16);
+  * each read of a kernel / bias variable inside the call is the variable's
+    f32 value cast (round to nearest even) to the compute dtype; the variables
+    and Adam's slots stay f32, and the gradient reaching a variable is the
+    16-bit gradient of its cast, widened exactly;
+  * x @ kernel is tf.matmul on 16-bit operands as TF runs it on a GPU: f32
+    products and sums (TF's default f32 compute type for half GEMMs), ONE
+    rounding of the result to the compute dtype; its gradient ops
+    (MatMulGrad) are the same kind of matmul: dX = dY kernel^T and
+    dkernel = X^T dY, each rounded once;
+  * + bias is an elementwise 16-bit add (exact sum, one rounding); the bias
+    gradient is the reduce_sum of dY over the batch (f32 accumulation, one
+    rounding) -- TF's _AddGrad for the broadcast operand;
+  * relu and its gradient are exact in 16 bits; the network's output is
+    16-bit, so the reference's own tf.argmax (dqn_agent.py:342, :273) sees
+    16-bit Q values and its tf.cast(..., tf.float32) (:345, :350) widens them
+    (the gradient of that cast rounds dL/dQ to 16 bits).
+
+The loss, the TD target, one_hot and Adam stay f32 (the reference builds
+them from f32 tensors).  There is no loss scaling: the reference's custom
+loop applies the raw gradients (no LossScaleOptimizer).  What stays unpinned
+is TF's f32 summation order inside a matmul / reduction (torch CPU's is used).
 """
 import contextlib
 import sys
@@ -39,6 +65,13 @@ import torch
 
 _REC = [0]          # >0 while a GradientTape is recording
 SUMMARIES = []      # (name, value, step) from tf.summary.* calls
+_POLICY = {"compute": None}  # None: float32; torch.float16 / torch.bfloat16 (mixed)
+POLICIES = {"float32": None, "mixed_float16": torch.float16, "mixed_bfloat16": torch.bfloat16}
+
+
+def set_global_policy(policy):
+    """keras.mixed_precision.set_global_policy: layers built afterwards use it."""
+    _POLICY["compute"] = POLICIES[policy if isinstance(policy, str) else policy.name]
 
 
 def _t(x, dtype=None):
@@ -93,6 +126,36 @@ class Input:
         self.shape = shape
 
 
+class _MatMul16(torch.autograd.Function):
+    """tf.matmul of two 16-bit operands with f32 accumulation, rounded once;
+    MatMulGrad: dX = dY W^T, dW = X^T dY, the same kind of matmul."""
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return (x.float() @ w.float()).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        gf = g.float()
+        gx = (gf @ w.float().T).to(x.dtype) if ctx.needs_input_grad[0] else None
+        gw = (x.float().T @ gf).to(w.dtype) if ctx.needs_input_grad[1] else None
+        return gx, gw
+
+
+class _BiasAdd16(torch.autograd.Function):
+    """y + b on 16-bit tensors (b broadcast over the batch): exact sum, one
+    rounding.  Gradient: dy as is; db = reduce_sum(dy, batch) accumulated in
+    f32, rounded once."""
+    @staticmethod
+    def forward(ctx, y, b):
+        return (y.float() + b.float()).to(y.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g.float().sum(0).to(g.dtype)
+
+
 class Dense:
     def __init__(self, units, activation=None, kernel_initializer=None, bias_initializer=None,
                  name=None):
@@ -100,6 +163,7 @@ class Dense:
         self.kinit = kernel_initializer or _Init("glorot")
         self.binit = bias_initializer or _Init("zeros")
         self.kernel = self.bias = None
+        self.compute = _POLICY["compute"]  # the dtype policy in force at construction
 
     def build(self, fan_in):
         self.kernel = Variable(self.kinit((fan_in, self.units)))
@@ -107,7 +171,14 @@ class Dense:
 
     def __call__(self, x):
         with _graph():
-            y = _t(x, torch.float32) @ self.kernel.t + self.bias.t
+            cd = self.compute
+            if cd is None:
+                y = _t(x, torch.float32) @ self.kernel.t + self.bias.t
+            else:
+                x = _t(x)
+                if x.is_floating_point():
+                    x = x.to(cd)  # input autocast
+                y = _BiasAdd16.apply(_MatMul16.apply(x, self.kernel.t.to(cd)), self.bias.t.to(cd))
             if self.activation == "relu":
                 y = torch.relu(y)
             return y if _REC[0] else y.detach()
@@ -179,12 +250,17 @@ class Adam:
         alpha = f(f(self.lr) * np.sqrt(f(1) - b2p, dtype=np.float32)) / f(f(1) - b1p)
         c1, c2 = torch.tensor(f(1 - self.b1)), torch.tensor(f(1 - self.b2))
         a, eps = torch.tensor(alpha), torch.tensor(f(self.eps))
+        self.last_grads = []  # the gradients of this step (fixture generator reads them)
         with torch.no_grad():
             for g, var in grads_and_vars:
+                self.last_grads.append(g.detach().clone())
                 m, v = self.slots.setdefault(id(var), (torch.zeros_like(var.t), torch.zeros_like(var.t)))
                 m += (g - m) * c1
                 v += (torch.square(g) - v) * c2
-                var.t -= (m * a) / (torch.sqrt(v) + eps)
+                # sqrt correctly rounded, as TF's (Eigen's sqrt on CPU and GPU):
+                # torch's vectorised f32 CPU sqrt is off by one ulp in ~0.7 %
+                # of inputs; the f64 root rounded to f32 is exact
+                var.t -= (m * a) / (torch.sqrt(v.double()).float() + eps)
         self.iterations += 1
 
 
@@ -262,6 +338,7 @@ def install():
     """Register the shim as `tensorflow` (and tensorflow.keras*) in sys.modules."""
     tf = types.ModuleType("tensorflow")
     tf.float32, tf.int32, tf.float16 = torch.float32, torch.int32, torch.float16
+    tf.bfloat16 = torch.bfloat16
     tf.convert_to_tensor, tf.argmax, tf.stack, tf.range = convert_to_tensor, argmax, stack, range_
     tf.gather_nd, tf.cast, tf.reduce_sum, tf.reduce_mean = gather_nd, cast, reduce_sum, reduce_mean
     tf.one_hot, tf.GradientTape = one_hot, GradientTape
@@ -283,7 +360,7 @@ def install():
     keras.layers = layers
     keras.losses = types.SimpleNamespace(MeanSquaredError=MeanSquaredError, Huber=Huber)
     keras.optimizers = types.SimpleNamespace(Adam=Adam)
-    keras.mixed_precision = types.SimpleNamespace(set_global_policy=lambda p: None)
+    keras.mixed_precision = types.SimpleNamespace(set_global_policy=set_global_policy)
     tf.keras = keras
     sys.modules["tensorflow"] = tf
     sys.modules["tensorflow.keras"] = keras

@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 import oracle as O  # noqa: E402
 from dmdqn_amd import kernels as K  # noqa: E402
-from dmdqn_amd.agent import AgentConfig, BatchedDQN, keras_to_kernel, kernel_to_keras  # noqa: E402
+from dmdqn_amd.agent import (AgentConfig, BatchedDQN, PRECISIONS, keras_to_kernel,  # noqa: E402
+                             kernel_to_keras)
 
 DEV = "cuda"
 
@@ -94,12 +95,41 @@ def test_learn_gate_and_q_argmax():
     obs = torch.from_numpy(rng.randint(-1, 24, size=(1, 3, 89)).astype(np.float32)).to(DEV)
     from dmdqn_amd._lib import call, ptr, stream_of
     qd = torch.empty((3, 4), dtype=torch.float32, device=DEV)
-    call("dmdqn_q_argmax", ptr(ag.params), 3, ag.P, ag.H, ptr(obs), ptr(ag.greedy), ptr(qd),
+    call("dmdqn_q_argmax", ptr(ag.params), 3, ag.P, ag.H, 0, ptr(obs), ptr(ag.greedy), ptr(qd),
          stream_of())
     pk = ag.keras_params("params")
     q_ref = np.stack([O.qnet_forward(pk[j], obs[0, j:j + 1].cpu().numpy())[0] for j in range(3)])
     np.testing.assert_allclose(qd.cpu().numpy(), q_ref, rtol=1e-5, atol=1e-5)
     np.testing.assert_array_equal(ag.greedy.cpu().numpy().reshape(-1), q_ref.argmax(1))
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_q_argmax_mixed_policy(precision):
+    """The greedy forward under mixed_float16 / mixed_bfloat16 (precision 1 / 2)
+    vs oracle.qnet_forward_mixed: 16-bit Q values equal except where an f32
+    summation-order difference flips one 16-bit rounding (one ulp), and the
+    argmax (first max on ties) equal on every row without a top-2 gap of at
+    most one ulp.  200 agents of random weights."""
+    NA = 200
+    ag = BatchedDQN(1, NA, AgentConfig(replay_buffer_size=200, precision=precision, seed=3))
+    rng = np.random.RandomState(5)
+    obs = torch.from_numpy(rng.randint(-1, 24, size=(1, NA, 89)).astype(np.float32)).to(DEV)
+    from dmdqn_amd._lib import call, ptr, stream_of
+    qd = torch.empty((NA, 4), dtype=torch.float32, device=DEV)
+    call("dmdqn_q_argmax", ptr(ag.params), NA, ag.P, ag.H, PRECISIONS[precision], ptr(obs),
+         ptr(ag.greedy), ptr(qd), stream_of())
+    pk = ag.keras_params("params")
+    q_ref = np.stack([O.qnet_forward_mixed(pk[j], obs[0, j:j + 1].cpu().numpy(), precision)[0]
+                      for j in range(NA)])
+    q = qd.cpu().numpy()
+    rnd = ROUND[precision]
+    assert np.array_equal(rnd(q), q), "16-bit Q values"
+    ulp = np.abs(q_ref) * (2.0 ** -10 if precision == "fp16" else 2.0 ** -7)
+    assert (np.abs(q - q_ref) <= ulp + 1e-6).all()
+    assert np.mean(q == q_ref) >= 0.97
+    top = np.sort(q_ref, 1)
+    safe = (top[:, -1] - top[:, -2]) > ulp.max(1)
+    np.testing.assert_array_equal(ag.greedy.cpu().numpy().reshape(-1)[safe], q_ref.argmax(1)[safe])
 
 
 # ---------------------------------------------------------------------------
@@ -119,56 +149,18 @@ ROUND = {"fp16": _f16r, "bf16": _bf16r}
 
 
 def _mixed_emulation(p, tgt, m, v, S, Aa, Rn, S2, D, t, H=128, gamma=0.99, lr=1e-3,
-                     w3_dz2=None, rnd=_f16r):
-    """numpy restatement of the kernel's rounding points: 16-bit operands (rnd:
-    f16 or bf16), f32 accumulation, 16-bit activations / Q / activation-gradients,
-    f32 Adam.  w3_dz2 overrides the W3 [H][4] that backprop uses for dZ2 (test
-    hook: the correct value is the pre-update W3)."""
-    f32 = np.float32
-
-    def split(w):
-        sizes = [89 * H, H, H * H, H, H * 4, 4]
-        out, o = [], 0
-        for s in sizes:
-            out.append(w[o:o + s])
-            o += s
-        W1, b1, W2, b2, W3, b3 = out
-        return (rnd(W1.reshape(89, H)), b1, rnd(W2.reshape(H, H)), b2, rnd(W3.reshape(H, 4)), b3)
-
-    def fwd(ws, X):
-        W1, b1, W2, b2, W3, b3 = ws
-        h1 = rnd(np.maximum(X @ W1 + b1, 0))
-        h2 = rnd(np.maximum(h1 @ W2 + b2, 0))
-        q = rnd(h2 @ W3 + b3)
-        return h1, h2, q
-
-    wo, wt = split(p), split(tgt)
-    _, _, q2 = fwd(wo, S2)
-    _, _, qt = fwd(wt, S2)
-    a_star = q2.argmax(1)
-    y = Rn + f32(gamma) * (1.0 - D) * qt[np.arange(128), a_star]
-    h1, h2, q = fwd(wo, S)
-    pred = q[np.arange(128), Aa]
-    dq = (2.0 * (pred - y) / 128).astype(f32)
-    loss = np.mean((y - pred) ** 2)
-    dq16 = rnd(dq)
-    DQ = np.zeros((128, 4), f32)
-    DQ[np.arange(128), Aa] = dq16
-    W1, b1, W2, b2, W3, b3 = wo
-    gW3 = h2.T @ DQ
-    gb3 = DQ.sum(0)
-    W3b = W3 if w3_dz2 is None else rnd(w3_dz2)
-    dz2 = rnd(np.where(h2 > 0, (dq16[:, None] * W3b[:, Aa].T), 0))
-    gb2 = dz2.sum(0)
-    gW2 = h1.T @ dz2
-    dz1 = rnd(np.where(h1 > 0, dz2 @ W2.T, 0))
-    gb1 = dz1.sum(0)
-    gW1 = S.T @ dz1
-    g = np.concatenate([gW1.ravel(), gb1, gW2.ravel(), gb2, gW3.ravel(), gb3]).astype(f32)
-    alpha, c1, c2, eps = O.keras_adam_consts(t, lr)
-    m2 = m + (g - m) * c1
-    v2 = v + (g * g - v) * c2
-    p2 = p - (m2 * alpha) / (np.sqrt(v2) + eps)
+                     w3_dz2=None, rnd=_f16r, loss_kind=0, round_grad=True):
+    """One learn under Keras 3's mixed policy: oracle.learn_mixed (the checker
+    pinned to the reference's own DQNAgent run under mixed_float16 /
+    mixed_bfloat16, tests/test_learn_mixed_golden_cpu.py) on copies of the
+    state.  Returns (loss, 16-bit gradient, w', m', v').  w3_dz2 overrides the
+    W3 [H][4] that backprop uses for dZ2 (test hook: the correct value is the
+    pre-update W3)."""
+    precision = "fp16" if rnd is _f16r else "bf16"
+    p2, m2, v2 = (np.array(x, np.float32, copy=True) for x in (p, m, v))
+    loss, g = O.learn_mixed(p2, tgt, m2, v2, S, Aa, Rn, S2, D, t, precision=precision,
+                            gamma=gamma, lr=lr, H=H, loss_kind=loss_kind, round_grad=round_grad,
+                            want_grad=True, w3_bwd=w3_dz2)
     return loss, g, p2, m2, v2
 
 

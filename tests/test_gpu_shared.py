@@ -46,7 +46,8 @@ def test_shared_gradient_is_mean_of_agent_gradients():
     ges, les = [], []
     for j in range(ag.NA):
         S, Aa, Rn, S2, D = _host_batch(ag, j, idx[j])
-        l_e, g_e, _, _, _ = _mixed_emulation(p0, t0, zero, zero.copy(), S, Aa, Rn, S2, D, 1)
+        l_e, g_e, _, _, _ = _mixed_emulation(p0, t0, zero, zero.copy(), S, Aa, Rn, S2, D, 1,
+                                             round_grad=False)
         ges.append(g_e)
         les.append(l_e)
     np.testing.assert_allclose(loss, np.array(les), rtol=2e-3)
@@ -80,11 +81,11 @@ def test_shared_greedy_act_matches_replicated_argmax():
                            .astype(np.float32)).to(DEV)
     from dmdqn_amd._lib import call, ptr, stream_of
     out = torch.empty(6, dtype=torch.int32, device=DEV)
-    call("dmdqn_q_argmax_shared", ptr(ag.params), 6, ag.P, ag.H, ptr(obs), ptr(out), None,
+    call("dmdqn_q_argmax_shared", ptr(ag.params), 6, ag.P, ag.H, 0, ptr(obs), ptr(out), None,
          stream_of())
     rep = ag.params.expand(6, ag.P).contiguous()
     ref = torch.empty(6, dtype=torch.int32, device=DEV)
-    call("dmdqn_q_argmax", ptr(rep), 6, ag.P, ag.H, ptr(obs), ptr(ref), None, stream_of())
+    call("dmdqn_q_argmax", ptr(rep), 6, ag.P, ag.H, 0, ptr(obs), ptr(ref), None, stream_of())
     np.testing.assert_array_equal(out.cpu().numpy(), ref.cpu().numpy())
     pk = ag.keras_params("params")[0]
     q_ref = O.qnet_forward(pk, obs.reshape(6, 89).cpu().numpy())
