@@ -107,15 +107,35 @@ def cpu_baseline(rows, cols, steps=60, seed=0):
 
 
 def read_traffic(workload_key):
-    """Per-launch HBM bytes of the learn kernel from the committed PMC pass
-    (profiles/learn_pmc.json, written by tools/pmc_learn.py), or None."""
+    """(per-launch HBM bytes, where they come from) for a kernel from the
+    committed PMC passes (profiles/learn_pmc.json, written by tools/pmc_learn.py
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench).
+    The counters cannot be read inside this process, so the figure is NOT
+    measured in this run: traffic_source names the pass it comes from.
+    (None, None) when no pass exists for this workload."""
     p = os.path.join(ROOT, "profiles", "learn_pmc.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(workload_key)
     except Exception:
-        return None
+        e = None
+    if not e:
+        return None, None
+    src = (f"profiles/learn_pmc.json[{workload_key}]: committed rocprofv3 PMC pass "
+           f"({e.get('source', 'tools/profile_bench.sh')}; FETCH_SIZE x2 + WRITE_SIZE, "
+           f"mean of {e['dispatches'][0]} launches), not measured in this run")
+    return e.get("hbm_bytes_per_launch"), src
+
+
+def config_name(rows, cols, envs, precision, shared, world):
+    """Which BASELINE.json configuration a run is (C1 is the CPU drop-in)."""
+    if shared and (rows, cols) == (8, 8):
+        return "C5"
+    if (rows, cols, envs) == (4, 4, 1024):
+        return "C4 shard" if world > 1 else "C3"
+    if (rows, cols, envs, precision) == (2, 2, 256, "bf16"):
+        return "C2"
+    return "custom"
 
 
 def sim_state_fits_lds(rows, cols, cap=24):
@@ -127,7 +147,7 @@ def sim_state_fits_lds(rows, cols, cap=24):
     return state + topo <= 160 * 1024 - 64
 
 
-def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
+def _sim_roofline(E, K, vbar, sim_ms, traffic, traffic_src, in_lds=True):
     """Sim-only HBM figure: 20*K*V-bar algorithmic bytes per env
     step over the average k_sim_step duration (HIP events over the
     SIM_PROBE_STEPS untimed steps that follow the timed region)."""
@@ -139,7 +159,8 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, in_lds=True):
     return {"kernel": f"k_sim_step (K IDM substeps per launch, {where})",
             "bound": "hbm", "achieved": round(b / t / 1e9, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 5),
-            "traffic": traffic, "bytes_per_launch": int(b), "mean_running_vehicles": round(vbar, 1),
+            "traffic": traffic, "traffic_source": traffic_src,
+            "bytes_per_launch": int(b), "mean_running_vehicles": round(vbar, 1),
             "avg_launch_ms": round(t * 1e3, 4),
             "timed_over": f"{SIM_PROBE_STEPS} back-to-back launches after the timed region",
             "note": "latency-bound: the per-env working set is cache-resident; bytes are "
@@ -310,11 +331,13 @@ def main():
         avg_learn_s = float(np.mean(learn_ms)) / 1e3 if learn_ms else float("nan")
         achieved = bpl / avg_learn_s / 1e9
         wl = f"{args.rows}x{args.cols}x{args.envs}"
-        traffic = read_traffic(f"{wl}_{args.precision}")
+        traffic, traffic_src = read_traffic(f"{wl}_{args.precision}" +
+                                            ("_shared" if args.shared else ""))
+        sim_traffic, sim_src = read_traffic(f"{wl}_sim")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.rows, args.cols, args.cpu_steps)
-        cname = "C5" if args.shared else "C3"
+        cname = config_name(args.rows, args.cols, args.envs, args.precision, args.shared, world)
         learn_desc = ("shared-network Double-DQN learn (mean per-agent loss"
                       + (", RCCL gradient all-reduce" if world > 1 else "") + ") + one Adam"
                       if args.shared else "Double-DQN learn + Adam")
@@ -360,6 +383,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_launch": bpl,
                 "avg_launch_ms": round(avg_learn_s * 1e3, 4),
                 "learn_share_of_step": round(avg_learn_s / (el_max / args.steps), 3),
@@ -371,7 +395,7 @@ def main():
             "step_roofline": _step_roofline(value, tr.env.cfg.step_duration, vbar, A, P,
                                             args.shared, NA),
             "sim_roofline": _sim_roofline(E, tr.env.cfg.step_duration, vbar, sim_ms,
-                                          read_traffic(f"{wl}_sim"),
+                                          sim_traffic, sim_src,
                                           sim_state_fits_lds(args.rows, args.cols)),
             "mfma": {
                 "kernel": ("k_learn_shared_f16" if args.shared else LEARN_KERNELS[args.precision]) +

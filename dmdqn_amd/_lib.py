@@ -24,6 +24,7 @@ SIGNATURES = {
     "dmdqn_mt_seed_py": [vp, vp, i32, vp],
     "dmdqn_mt_draw_u32": [vp, i32, i32, vp, vp],
     "dmdqn_act": [vp, i32, i32, f64, i32, vp, vp, vp],
+    "dmdqn_act_uniform": [vp, i32, i32, i32, vp, vp],
     "dmdqn_observe": [i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "dmdqn_replay_store": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dmdqn_replay_sample": [vp, i32, i32, i32, i32, vp, vp],

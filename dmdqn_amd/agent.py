@@ -50,7 +50,7 @@ _lib.register({
     "dmdqn_q_argmax_shared": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                               C.c_void_p, C.c_void_p, C.c_void_p],
     "dmdqn_learn_shared_grad": [C.POINTER(CLearn), C.c_void_p, C.c_int, C.c_void_p, C.c_float,
-                                C.c_void_p],
+                                C.c_void_p, C.c_void_p],
     "dmdqn_adam": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                    C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
                    C.c_int, C.c_void_p],
@@ -292,6 +292,8 @@ class BatchedDQN:
             self.n_slabs = max(1, min(NA, n_cu))
             self.slab = torch.empty((self.n_slabs, self.P), dtype=torch.float32, device=dev)
             self.grad = torch.zeros(self.P, dtype=torch.float32, device=dev)
+            # each batch row's TD target + action between the shared learn's two passes
+            self.shared_work = torch.empty(NA * cfg.batch_size * 5, dtype=torch.uint8, device=dev)
         self.adam_m = torch.zeros_like(self.params)
         self.adam_v = torch.zeros_like(self.params)
         self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev)
@@ -461,7 +463,7 @@ class BatchedDQN:
         self._ops.learn_shared_grad(ring.s, ring.n, ring.a, ring.d, ring.r, self.idx, self.params,
                                     self.target, self.target_h, self.params_h, self.loss,
                                     ring.start, cfg.gamma, LOSSES[cfg.loss], qstats, self.rn_out,
-                                    self.slab, self.grad, 1.0 / self.NA)
+                                    self.slab, self.grad, 1.0 / self.NA, work=self.shared_work)
         world = 1
         if dist.is_available() and dist.is_initialized():
             world = dist.get_world_size()

@@ -26,10 +26,12 @@ import os
 import numpy as np
 import torch
 
-FORMAT = "dmdqn-ckpt-5"  # 5: + the actuated-mode detector times; 4: 128-B replay rows, unpadded W1T
+# 6: + per-replica clocks and episode counters; 5: + the actuated-mode detector
+# times; 4: 128-B replay rows, unpadded W1T
+FORMAT = "dmdqn-ckpt-6"
 
 _ENV_TENSORS = ["t_x", "t_v", "t_dst", "t_head", "t_cnt", "t_phase_state", "t_ts", "t_qptr",
-                "t_stats", "t_last_det", "halt", "phase", "tspent", "done_u8"]
+                "t_stats", "t_last_det", "t_env", "halt", "phase", "tspent", "done_u8"]
 _AGENT_TENSORS = ["params", "target", "adam_m", "adam_v", "np_state", "py_state"]
 
 
@@ -71,7 +73,9 @@ def trainer_state(tr, include_replay=True):
                        "epsilon": float(ag.epsilon), "learn_launches": ag.learn_launches,
                        "env_t": env.t, "env_episode": env.episode, "episode": tr.episode,
                        "step_count": tr.step_count, "total_steps": tr.total_steps,
-                       "ring_total": ag.ring.total}}
+                       "ring_total": ag.ring.total,
+                       "env_steps": [int(x) for x in env.env_steps],
+                       "env_episodes": [int(x) for x in env.env_episodes]}}
     st["agent"] = {k: getattr(ag, k).cpu() for k in _AGENT_TENSORS}
     if ag.target_h is not None:
         st["agent"]["target_h"] = ag.target_h.cpu()
@@ -104,36 +108,48 @@ def load(path, tr):
         raise ValueError("checkpoint was saved without its replay (include_replay=False) but its "
                          "rings hold transitions: a resume would train on empty rings")
 
-    def put(group, obj, k, v):
-        dst = getattr(obj, k)
+    # every tensor is checked before the first copy: a mismatch leaves the
+    # Trainer untouched instead of half-restored
+    copies = []
+
+    def plan(group, dst, v, name):
         if dst is None:
-            raise ValueError(f"checkpoint {group}.{k} has no counterpart in this Trainer")
+            raise ValueError(f"checkpoint {group}.{name} has no counterpart in this Trainer")
         if tuple(dst.shape) != tuple(v.shape) or dst.dtype != v.dtype:
-            raise ValueError(f"checkpoint {group}.{k} {v.dtype}{tuple(v.shape)} != "
+            raise ValueError(f"checkpoint {group}.{name} {v.dtype}{tuple(v.shape)} != "
                              f"{dst.dtype}{tuple(dst.shape)}")
-        dst.copy_(v.to(obj.device))
+        copies.append((dst, v))
 
     for k, v in st["agent"].items():
-        put("agent", ag, k, v)
+        plan("agent", getattr(ag, k), v, k)
     for k, v in st["env"].items():
-        if k == "local":
-            env.local = v.to(env.device)
-            continue
-        put("env", env, k, v)
+        if k != "local":
+            plan("env", getattr(env, k), v, k)
+    if tuple(st["env"]["local"].shape) != tuple(env.local.shape):
+        raise ValueError(f"checkpoint env.local {tuple(st['env']['local'].shape)} != "
+                         f"{tuple(env.local.shape)}")
+    if tuple(st["obs"].shape) != tuple(tr.obs.shape):
+        raise ValueError(f"checkpoint obs {tuple(st['obs'].shape)} != {tuple(tr.obs.shape)}")
     c = st["counters"]
+    if "replay" in st:
+        n = st["replay"]["s"].shape[1]
+        if n != min(int(c["ring_total"]), ag.ring.cap):
+            raise ValueError(f"checkpoint replay holds {n} slots, its counter says "
+                             f"{min(int(c['ring_total']), ag.ring.cap)}")
+        for k, v in st["replay"].items():
+            plan("replay", getattr(ag.ring, k)[:, :n], v, k)
+    for dst, v in copies:
+        dst.copy_(v.to(dst.device))
+    env.local = st["env"]["local"].to(env.device)
     ag.learn_step_counter, ag.global_step_count = c["learn_step_counter"], c["global_step_count"]
     ag.epsilon, ag.learn_launches = c["epsilon"], c["learn_launches"]
     env.t, env.episode = c["env_t"], c["env_episode"]
     tr.episode, tr.step_count, tr.total_steps = c["episode"], c["step_count"], c["total_steps"]
+    env.env_steps[:] = c["env_steps"]
+    env.env_episodes[:] = c["env_episodes"]
     ag.ring.total = c["ring_total"]
     ag._refresh_params_h()  # the 16-bit copies are derived from the f32 nets
     ag._refresh_target_h()
-    if "replay" in st:
-        n = st["replay"]["s"].shape[1]
-        if n != len(ag.ring):
-            raise ValueError(f"checkpoint replay holds {n} slots, its counter says {len(ag.ring)}")
-        for k, v in st["replay"].items():
-            getattr(ag.ring, k)[:, :n].copy_(v.to(ag.device))
     tr.obs = st["obs"].to(env.device)
     # the observation the env hands back is a view of its own buffer
     env.obs = tr.obs

@@ -240,6 +240,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     // online forward on S': layer 3 reads H2 only, so its Q goes to the H1 region
     forward<H>(Wp, X, H1, H2, H1);
     if (tid < B_) {
+#pragma clang fp contract(off)  // y = r + (gamma (1 - d)) q_t, each op rounded as TF's
         const float *qo = H1 + tid * NACT;
         int best = 0;
         for (int k = 1; k < NACT; k++)

@@ -171,8 +171,17 @@ __global__ void __launch_bounds__(256) k_adam(float *W, float *M, float *V, floa
 
 using namespace dmdqn;
 
+namespace dmdqn {
+int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *slab, int n_slabs,
+                     hipStream_t s);  // learn_shared.hip
+}
+
+extern "C" size_t dmdqn_learn_shared_work_bytes(int NA) {
+    return NA > 0 ? (size_t)NA * f16k::B_ * (sizeof(float) + 1) : 0;
+}
+
 extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, int n_slabs,
-                                       float *grad, float scale, void *stream) {
+                                       float *grad, float scale, void *work, void *stream) {
     DMDQN_REQUIRE(a && slab && grad, "dmdqn_learn_shared_grad: null argument");
     DMDQN_REQUIRE(a->NA > 0 && a->cap >= a->batch && a->start >= 0 && a->start < a->cap,
                   "dmdqn_learn_shared_grad: NA=%d cap=%d start=%d", a->NA, a->cap, a->start);
@@ -186,13 +195,22 @@ extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, i
     DMDQN_REQUIRE(n_slabs >= 1, "dmdqn_learn_shared_grad: n_slabs must be >= 1");
     DMDQN_REQUIRE(a->loss_kind == DMDQN_LOSS_MSE || a->loss_kind == DMDQN_LOSS_HUBER,
                   "dmdqn_learn_shared_grad: loss_kind %d", a->loss_kind);
+    DMDQN_REQUIRE(a->target_h, "dmdqn_learn_shared_grad: target_h (the f16 target) required");
     hipStream_t s = as_stream(stream);
-    if (a->qstats)
+    const char *v1 = getenv("DMDQN_SHARED_V1");  // A/B against the one-pass kernel
+    if (work && !(v1 && v1[0] == '1')) {
+        float *y = reinterpret_cast<float *>(work);
+        uint8_t *act = reinterpret_cast<uint8_t *>(y + (size_t)a->NA * f16k::B_);
+        int rc = launch_shared_v2(a, y, act, slab, n_slabs, s);
+        if (rc) return rc;
+    } else if (a->qstats) {
         hipLaunchKernelGGL(f16k::k_learn_shared_f16<true>, dim3(n_slabs), dim3(512), 0, s, *a, slab);
-    else
+        DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
+    } else {
         hipLaunchKernelGGL(f16k::k_learn_shared_f16<false>, dim3(n_slabs), dim3(512), 0, s, *a,
                            slab);
-    DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
+        DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
+    }
     hipLaunchKernelGGL(f16k::k_reduce_slabs, dim3((f16k::L::P / 4 + 255) / 256), dim3(256), 0, s,
                        slab, n_slabs, scale, grad);
     DMDQN_LAUNCH_CHECK("k_reduce_slabs");

@@ -723,6 +723,7 @@ __device__ __forceinline__ void ddqn_target(const dmdqn_learn_args &a, const flo
                                             const Scratch &S) {
     const int tid = threadIdx.x;
     if (tid < B_) {
+#pragma clang fp contract(off)  // y = r + (gamma (1 - d)) q_t, each op rounded as TF's
         const float4 q = *reinterpret_cast<const float4 *>(qo + tid * NACT);
         int best = 0;
         float bq = q.x;

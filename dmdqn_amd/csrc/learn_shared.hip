@@ -1,0 +1,597 @@
+// learn_shared.hip -- the shared-parameter learn of configuration C5 (SURVEY
+// 8e; not in the reference, which trains one network per junction) as two
+// batched passes over every agent's 128-row batch, with the ONE network
+// resident in LDS for the whole launch (f16, the reference's mixed_float16
+// rounding points: learn_h16.hpp).
+//
+//   k_shared_next   per agent: z-score (dqn_agent.py:66-69), X(S') from the
+//                   s' rows, target and online forwards of S', first-max
+//                   argmax, y = r^ + (gamma (1 - d)) Q_t(S')[a*] (:342-347);
+//                   writes y and the batch actions.  Both nets in LDS.
+//   k_shared_grad   per agent: X(S), online forward, MSE / Huber dL/dQ, and
+//                   the backward; the weight gradients of all the agents a
+//                   workgroup walks accumulate in registers and are written
+//                   once per workgroup as a partial slab (k_reduce_slabs,
+//                   RCCL all-reduce and k_adam follow, as before).
+//
+// Each forward runs "wave owns rows": a wave takes a 16-row tile through all
+// three layers in registers.  The transposed GEMMs Z^T = W^T X^T leave each
+// lane with 4 consecutive neurons of one row (MFMA C layout), and two such
+// tiles are exactly the 8 K-values the next layer's B operand needs when the
+// next layer's weights are stored with that K order (kperm below) -- so the
+// activations never go through LDS in the forward, and no barrier is needed.
+// The weight fragments come from LDS (one 16-byte read per lane per MFMA,
+// conflict-free).  Only the weight-gradient reductions over the batch rows
+// need the whole agent's activations: those are staged in LDS images and
+// reduced by "neuron owning" waves (4 barriers per agent).
+#include <math.h>
+
+#include "common.hpp"
+#include "qnet_layout.hpp"
+
+namespace dmdqn {
+namespace shk {
+
+typedef _Float16 h16;
+typedef h16 half8 __attribute__((ext_vector_type(8)));
+typedef h16 half4v __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short v4s __attribute__((vector_size(8)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr int B_ = 128, H = 128, NACT = QN_NA, DP = QN_DP;
+using L = QL<H>;
+
+__device__ __forceinline__ f32x4 mfma(half8 a, half8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float r16(float x) { return (float)(h16)x; }
+__device__ __forceinline__ half8 zero8() {
+    half8 r;
+#pragma unroll
+    for (int e = 0; e < 8; e++) r[e] = (h16)0.0f;
+    return r;
+}
+
+// K order of layers 2 and 3: slot 8g + e of K-step s holds neuron kperm(s, g, e)
+// -- the neurons lane group g of a row holds after the previous layer's two
+// output tiles 2s (e < 4) and 2s + 1 (e >= 4).
+__device__ __forceinline__ int kperm(int s, int g, int e) {
+    return 32 * s + 16 * (e >> 2) + 4 * g + (e & 3);
+}
+
+// ---------------------------------------------------------------- LDS images
+// The blocked, XOR-permuted activation images of learn_h16.hpp (hoff): 8-row x
+// 32-column blocks, conflict-free row-fragment and transposed reads.
+template <int LD = H>
+__device__ __forceinline__ int hoff(int r, int c) {
+    const int ch = c >> 3;
+    return 8 * LD * (r >> 3) + 256 * (ch >> 2) + 32 * (r & 7) +
+           8 * ((ch & 3) ^ (((r >> 1) & 1) | ((r >> 2) & 2))) + (c & 7);
+}
+
+// img[r0 + 8(l>>4) + e][c0 + (l&15)], e = 0..7 (two ds_read_b64_tr_b16).
+template <int LD = H>
+__device__ __forceinline__ half8 frag_tr_h(const h16 *img, int r0, int c0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const h16 *p0 = img + hoff<LD>(r0 + 8 * g + (i >> 2), c0 + 4 * (i & 3));
+    v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)p0);
+    v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(p0 + 128));
+    half8 r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        r[e] = __builtin_bit_cast(h16, (short)t0[e]);
+        r[e + 4] = __builtin_bit_cast(h16, (short)t1[e]);
+    }
+    return r;
+}
+
+// Same, plain row-major [rows][ld] image (the DQ image, ld 16).
+__device__ __forceinline__ half8 frag_tr(const h16 *img, int ld, int r0, int c0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const h16 *p0 = img + (r0 + 8 * g + (i >> 2)) * ld + c0 + 4 * (i & 3);
+    v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)p0);
+    v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(p0 + 4 * ld));
+    half8 r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        r[e] = __builtin_bit_cast(h16, (short)t0[e]);
+        r[e + 4] = __builtin_bit_cast(h16, (short)t1[e]);
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------- the network in LDS
+// A-fragments, [tile][K-step][lane] x 16 B (each wave-instruction reads 1 KB
+// contiguously):  W1: lane (i, g) = W1^T[16t + i][32s + 8g + e];
+// W2: W2^T[16t + i][kperm(s, g, e)];  W3: [s][g][i < 4] = W3^T[i][kperm(s, g, e)]
+// (lanes i >= 4 use zeros);  W2B (backward, dH1 = dZ2 W2^T):
+// W2[j = 16t + i][kperm(s, g, e)] (Keras W2[in][out]);  W3R: W3^T [4][128]
+// plain (dZ2);  biases f16.  All values are the f16 copy Keras computes with
+// (the f32 variables cast to f16: params_h / target_h).
+constexpr int W1_BYTES = 8 * 3 * 64 * 16, W2_BYTES = 8 * 4 * 64 * 16, W3_BYTES = 4 * 4 * 4 * 16;
+constexpr int BIAS_BYTES = (2 * H + 8) * 2;
+constexpr int NET_BYTES = W1_BYTES + W2_BYTES + W3_BYTES + BIAS_BYTES;  // 58896
+
+struct Net {
+    const half8 *w1, *w2, *w3;
+    const h16 *b1, *b2, *b3;
+};
+
+__device__ __forceinline__ Net net_at(char *p) {
+    Net n;
+    n.w1 = reinterpret_cast<const half8 *>(p);
+    n.w2 = reinterpret_cast<const half8 *>(p + W1_BYTES);
+    n.w3 = reinterpret_cast<const half8 *>(p + W1_BYTES + W2_BYTES);
+    n.b1 = reinterpret_cast<const h16 *>(p + W1_BYTES + W2_BYTES + W3_BYTES);
+    n.b2 = n.b1 + H;
+    n.b3 = n.b2 + H;
+    return n;
+}
+
+// Stage one network from its f16 device-layout copy WH (qnet_layout.hpp) into
+// LDS at p.  Every thread of the block takes part; the caller syncs.
+__device__ void stage_net(const h16 *WH, char *p) {
+    const int nt = blockDim.x;
+    half8 *w1 = reinterpret_cast<half8 *>(p);
+    half8 *w2 = reinterpret_cast<half8 *>(p + W1_BYTES);
+    half8 *w3 = reinterpret_cast<half8 *>(p + W1_BYTES + W2_BYTES);
+    h16 *bb = reinterpret_cast<h16 *>(p + W1_BYTES + W2_BYTES + W3_BYTES);
+    for (int ent = threadIdx.x; ent < 8 * 3 * 64; ent += nt) {
+        const int t = ent / 192, s = (ent / 64) % 3, l = ent & 63, i = l & 15, g = l >> 4;
+        half8 v;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int k = 32 * s + 8 * g + e;
+            v[e] = k < QN_D ? WH[L::oW1T + qn_w1<H>(16 * t + i, k)] : (h16)0.0f;
+        }
+        w1[ent] = v;
+    }
+    for (int ent = threadIdx.x; ent < 8 * 4 * 64; ent += nt) {
+        const int t = ent / 256, s = (ent / 64) & 3, l = ent & 63, i = l & 15, g = l >> 4;
+        half8 v;
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = WH[L::oW2T + qn_wt(16 * t + i, kperm(s, g, e), H)];
+        w2[ent] = v;
+    }
+    for (int ent = threadIdx.x; ent < 4 * 4 * 4; ent += nt) {
+        const int s = ent >> 4, g = (ent >> 2) & 3, i = ent & 3;
+        half8 v;
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = WH[L::oW3T + i * H + kperm(s, g, e)];
+        w3[ent] = v;
+    }
+    for (int j = threadIdx.x; j < 2 * H + NACT; j += nt) bb[j] = WH[L::ob1 + j];
+}
+
+// The backward-only pieces of the online net: W2B and W3R.
+constexpr int W2B_BYTES = W2_BYTES, W3R_BYTES = NACT * H * 2;
+
+__device__ void stage_bwd(const h16 *WH, half8 *w2b, h16 *w3r) {
+    const int nt = blockDim.x;
+    for (int ent = threadIdx.x; ent < 8 * 4 * 64; ent += nt) {
+        const int t = ent / 256, s = (ent / 64) & 3, l = ent & 63, i = l & 15, g = l >> 4;
+        half8 v;
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = WH[L::oW2T + qn_wt(kperm(s, g, e), 16 * t + i, H)];
+        w2b[ent] = v;
+    }
+    for (int k = threadIdx.x; k < NACT * H; k += nt) w3r[k] = WH[L::oW3T + k];
+}
+
+// ---------------------------------------------------------------- one 16-row tile
+// X(S) / X(S') B-operands of a 16-row tile: lane (i, g) holds features
+// 32s + 8g .. +7 of row i (int8 replay row -> f16, exact).
+struct XTile {
+    uint2 raw[3];
+};
+
+__device__ __forceinline__ void x_issue(const int8_t *row, XTile &x) {
+    const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int s = 0; s < 3; s++) x.raw[s] = reinterpret_cast<const uint2 *>(row)[4 * s + g];
+}
+
+__device__ __forceinline__ void x_frags(const XTile &x, half8 bx[3]) {
+#pragma unroll
+    for (int s = 0; s < 3; s++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            bx[s][e] = (h16)(float)(int8_t)(x.raw[s].x >> (8 * e));
+            bx[s][e + 4] = (h16)(float)(int8_t)(x.raw[s].y >> (8 * e));
+        }
+}
+
+// relu(h16(h16(acc) + b)) of output tile t into the next layer's operand
+// slot: tile t -> K-step t >> 1, elements 4 (t & 1) .. +3.
+__device__ __forceinline__ void dense_out(f32x4 c, const h16 *bias, int t, half8 *ops) {
+    const int g = (threadIdx.x & 63) >> 4;
+    const half4v b = *reinterpret_cast<const half4v *>(bias + 16 * t + 4 * g);
+    const half4v z = __builtin_convertvector(c, half4v) + b;
+#pragma unroll
+    for (int e = 0; e < 4; e++) ops[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
+}
+
+// Forward of one tile through a net: hb1 / hb2 = the layer-1 / layer-2
+// activations as next-layer operands (permuted K order); returns Q on the
+// lanes g = 0 (Q[row i][0..3]; other lanes hold zeros).
+__device__ __forceinline__ f32x4 fwd_tile(const Net &N, const half8 bx[3], half8 hb1[4],
+                                          half8 hb2[4]) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 3; s++) c = mfma(N.w1[(t * 3 + s) * 64 + l], bx[s], c);
+        dense_out(c, N.b1, t, hb1);
+        __builtin_amdgcn_sched_barrier(0);  // bound the scheduler's LDS-read hoisting
+    }
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; s++) c = mfma(N.w2[(t * 4 + s) * 64 + l], hb1[s], c);
+        dense_out(c, N.b2, t, hb2);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; s++) c = mfma(i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8(), hb2[s], c);
+    f32x4 q;
+#pragma unroll
+    for (int e = 0; e < 4; e++) q[e] = g == 0 ? r16(r16(c[e]) + (float)N.b3[e]) : 0.0f;
+    return q;
+}
+
+// ---------------------------------------------------------------- pass 1: S'
+// LDS: both nets (2 x 58,896 B) + per-wave reward scratch (8 x 1 KB).
+constexpr int NEXT_LDS = 2 * NET_BYTES + 8 * B_ * 8;
+static_assert(NEXT_LDS <= 160 * 1024, "k_shared_next LDS");
+
+// One wave per agent at a time (8 agents in flight per workgroup).
+__global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, float *y_out,
+                                                        uint8_t *act_out) {
+    __shared__ __attribute__((aligned(16))) char smem[NEXT_LDS];
+    stage_net(reinterpret_cast<const h16 *>(a.params_h), smem);
+    stage_net(reinterpret_cast<const h16 *>(a.target_h), smem + NET_BYTES);
+    __syncthreads();
+    const Net on = net_at(smem), tg = net_at(smem + NET_BYTES);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    double *r64 = reinterpret_cast<double *>(smem + 2 * NET_BYTES) + w * B_;
+    for (int agent = blockIdx.x * 8 + w; agent < a.NA; agent += gridDim.x * 8) {
+        const size_t arow = (size_t)agent * a.cap;
+        // rewards of the batch (f64 in the s' rows) -> z-score in numpy's
+        // pairwise order (learn_h16.hpp zscore): 8 partial sums of 16
+        for (int b = l; b < B_; b += 64) {
+            int s = a.start + a.idx[(size_t)agent * B_ + b];
+            if (s >= a.cap) s -= a.cap;
+            const uint2 rb = *reinterpret_cast<const uint2 *>(a.ring_n + (arow + s) * DMDQN_ROW_BYTES +
+                                                              DMDQN_ROW_R);
+            r64[b] = __longlong_as_double((long long)(((unsigned long long)rb.y << 32) | rb.x));
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        double part = 0.0;
+        if (l < 8) {
+            part = r64[l];
+            for (int k = 1; k < 16; k++) part = __dadd_rn(part, r64[8 * k + l]);
+        }
+        double p[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) p[k] = __shfl(part, k);
+        const double mean = __ddiv_rn(__dadd_rn(0.0, __dadd_rn(__dadd_rn(__dadd_rn(p[0], p[1]),
+                                                                         __dadd_rn(p[2], p[3])),
+                                                               __dadd_rn(__dadd_rn(p[4], p[5]),
+                                                                         __dadd_rn(p[6], p[7])))),
+                                      128.0);
+        part = 0.0;
+        if (l < 8) {
+            for (int k = 0; k < 16; k++) {
+                const double d = __dsub_rn(r64[8 * k + l], mean);
+                const double sq = __dmul_rn(d, d);
+                part = k == 0 ? sq : __dadd_rn(part, sq);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) p[k] = __shfl(part, k);
+        const double sd = __dadd_rn(
+            __dsqrt_rn(__ddiv_rn(__dadd_rn(0.0, __dadd_rn(__dadd_rn(__dadd_rn(p[0], p[1]),
+                                                                    __dadd_rn(p[2], p[3])),
+                                                          __dadd_rn(__dadd_rn(p[4], p[5]),
+                                                                    __dadd_rn(p[6], p[7])))),
+                                 128.0)),
+            1e-8);
+#pragma unroll 1
+        for (int rt = 0; rt < B_ / 16; rt++) {
+            const int b = 16 * rt + i;
+            int s = a.start + a.idx[(size_t)agent * B_ + b];
+            if (s >= a.cap) s -= a.cap;
+            const int8_t *row = a.ring_n + (arow + s) * DMDQN_ROW_BYTES;
+            XTile xt;
+            x_issue(row, xt);
+            const uint32_t meta = *reinterpret_cast<const uint32_t *>(row + DMDQN_ROW_A);
+            half8 bx[3], hb1[4], hb2[4];
+            x_frags(xt, bx);
+            const f32x4 qt = fwd_tile(tg, bx, hb1, hb2);
+            const f32x4 qo = fwd_tile(on, bx, hb1, hb2);
+            if (g == 0) {
+                // Double-DQN target (dqn_agent.py:342-347, first max on ties),
+                // each op rounded on its own as TF's
+                int best = 0;
+                float bq = qo[0];
+                if (qo[1] > bq) { best = 1; bq = qo[1]; }
+                if (qo[2] > bq) { best = 2; bq = qo[2]; }
+                if (qo[3] > bq) { best = 3; }
+                const float tq = best == 0 ? qt[0] : best == 1 ? qt[1] : best == 2 ? qt[2] : qt[3];
+                const float rn = (float)__ddiv_rn(__dsub_rn(r64[b], mean), sd);
+                const float dn = ((meta >> 8) & 0xffu) ? 1.0f : 0.0f;
+                const float gd = __fmul_rn(a.gamma, __fsub_rn(1.0f, dn));
+                y_out[(size_t)agent * B_ + b] = __fadd_rn(rn, __fmul_rn(gd, tq));
+                act_out[(size_t)agent * B_ + b] = (uint8_t)(meta & 0xffu);
+                if (a.rn_out) a.rn_out[(size_t)agent * B_ + b] = rn;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- pass 2: gradients
+// LDS: online net (forward, W2B, W3R) + H1 / H2 images (reused for dZ1 / X)
+// + DQ image [128][16] + per-row dq / action + loss partials.
+constexpr int OFF_W2B = NET_BYTES;
+constexpr int OFF_W3R = OFF_W2B + W2B_BYTES;
+constexpr int OFF_I1 = OFF_W3R + W3R_BYTES;      // H1, then dZ1   [128][128] f16
+constexpr int OFF_I2 = OFF_I1 + B_ * H * 2;      // H2 -> dZ2, then X [128][96]
+constexpr int OFF_DQ = OFF_I2 + B_ * H * 2;      // [128][16] f16
+constexpr int OFF_SC = OFF_DQ + B_ * 16 * 2;     // dq f32 [128], act int [128], loss [8]
+constexpr int GRAD_LDS = OFF_SC + B_ * 4 + B_ * 4 + 8 * 4;
+static_assert(GRAD_LDS <= 160 * 1024, "k_shared_grad LDS");
+static_assert(OFF_I1 % 16 == 0 && OFF_DQ % 16 == 0, "aligned images");
+
+// Per-row loss term and dL/dq (common.hpp loss_term), rounded as TF's ops.
+__device__ __forceinline__ void row_loss(int kind, float diff, float &term, float &dq) {
+#pragma clang fp contract(off)
+    if (kind == DMDQN_LOSS_HUBER) {
+        const float ae = fabsf(diff);
+        term = ae <= 1.0f ? 0.5f * diff * diff : ae - 0.5f;
+        dq = (ae <= 1.0f ? diff : copysignf(1.0f, diff)) * (1.0f / (float)B_);
+    } else {
+        term = diff * diff;
+        dq = 2.0f * diff * (1.0f / (float)B_);
+    }
+}
+
+struct Pref {  // one row per lane i: the next agent's inputs, in flight
+    XTile x;
+    float y;
+    uint32_t act;
+};
+
+__device__ __forceinline__ void pref_issue(const dmdqn_learn_args &a, const float *y_in,
+                                           const uint8_t *act_in, int agent, Pref &p) {
+    const int w = threadIdx.x >> 6, i = threadIdx.x & 15;
+    const int b = 16 * w + i;
+    int s = a.start + a.idx[(size_t)agent * B_ + b];
+    if (s >= a.cap) s -= a.cap;
+    x_issue(a.ring_s + ((size_t)agent * a.cap + s) * DMDQN_ROW_BYTES, p.x);
+    p.y = y_in[(size_t)agent * B_ + b];
+    p.act = act_in[(size_t)agent * B_ + b];
+}
+
+template <bool QSTATS>
+__global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, const float *y_in,
+                                                        const uint8_t *act_in, float *slab) {
+    __shared__ __attribute__((aligned(16))) char smem[GRAD_LDS];
+    const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
+    stage_net(WH, smem);
+    stage_bwd(WH, reinterpret_cast<half8 *>(smem + OFF_W2B), reinterpret_cast<h16 *>(smem + OFF_W3R));
+    const Net on = net_at(smem);
+    const half8 *w2b = reinterpret_cast<const half8 *>(smem + OFF_W2B);
+    const h16 *w3r = reinterpret_cast<const h16 *>(smem + OFF_W3R);
+    h16 *I1 = reinterpret_cast<h16 *>(smem + OFF_I1), *I2 = reinterpret_cast<h16 *>(smem + OFF_I2);
+    h16 *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
+    float *sdq = reinterpret_cast<float *>(smem + OFF_SC);
+    int *sact = reinterpret_cast<int *>(smem + OFF_SC + B_ * 4);
+    float *sloss = reinterpret_cast<float *>(smem + OFF_SC + 2 * B_ * 4);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const int row = 16 * w + i;  // this lane's batch row in the row phases
+    half8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
+    // gradient accumulators, across every agent this workgroup walks
+    f32x4 G1[6], G2[8], G3 = {0.f, 0.f, 0.f, 0.f}, GB1 = G3, GB2 = G3, GB3 = G3;
+#pragma unroll
+    for (int t = 0; t < 6; t++) G1[t] = G3;
+#pragma unroll
+    for (int t = 0; t < 8; t++) G2[t] = G3;
+    // DQ image columns 4..15 stay zero
+    for (int k = threadIdx.x; k < B_ * 16; k += 512) DQI[k] = (h16)0.0f;
+    Pref pf;
+    if ((int)blockIdx.x < a.NA) pref_issue(a, y_in, act_in, blockIdx.x, pf);
+    __syncthreads();
+
+    for (int agent = blockIdx.x; agent < a.NA; agent += gridDim.x) {
+        // ---- R: rows 16w..16w+15 -- forward, dL/dQ, dZ2, dH1 -> dZ1 in registers
+        half8 bx[3], hb1[4], hb2[4];
+        x_frags(pf.x, bx);
+        const float yv = pf.y;
+        const int av = (int)pf.act;
+        const f32x4 q = fwd_tile(on, bx, hb1, hb2);
+        float term = 0.0f, dq = 0.0f;
+        if (g == 0) {
+            const float qa = av == 0 ? q[0] : av == 1 ? q[1] : av == 2 ? q[2] : q[3];
+            row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
+            dq = r16(dq);  // dL/dQ in f16 (the gradient of the learn's tf.cast)
+            sdq[row] = dq;
+            sact[row] = av;
+            half4v d;
+#pragma unroll
+            for (int e = 0; e < 4; e++) d[e] = e == av ? (h16)dq : (h16)0.0f;
+            *reinterpret_cast<half4v *>(DQI + row * 16) = d;
+        }
+        dq = __shfl(dq, i);
+        // activations into the images (rows of this wave)
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            half4v v1, v2;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                v1[e] = hb1[t >> 1][4 * (t & 1) + e];
+                v2[e] = hb2[t >> 1][4 * (t & 1) + e];
+            }
+            *reinterpret_cast<half4v *>(I1 + hoff(row, 16 * t + 4 * g)) = v1;
+            *reinterpret_cast<half4v *>(I2 + hoff(row, 16 * t + 4 * g)) = v2;
+        }
+        // dZ2 = h16(dq W3[k][a]) where H2 > 0 (operand order of hb2)
+        half8 dz2[4];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const half4v w3 = *reinterpret_cast<const half4v *>(w3r + av * H + 16 * t + 4 * g);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const h16 hv = hb2[t >> 1][4 * (t & 1) + e];
+                dz2[t >> 1][4 * (t & 1) + e] = hv > (h16)0.0f ? (h16)(dq * (float)w3[e]) : (h16)0.0f;
+            }
+        }
+        // dH1^T = W2 dZ2^T -> dZ1 = h16(dH1) where H1 > 0 (operand order of hb1)
+        half8 dz1[4];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; s++) c = mfma(w2b[(t * 4 + s) * 64 + l], dz2[s], c);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const h16 hv = hb1[t >> 1][4 * (t & 1) + e];
+                dz1[t >> 1][4 * (t & 1) + e] = hv > (h16)0.0f ? (h16)c[e] : (h16)0.0f;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // loss of the batch: per wave over its 16 rows, then 8 partials in order
+        {
+            float ls = term;
+            for (int off = 8; off > 0; off >>= 1) ls += __shfl_xor(ls, off);
+            if (l == 0) sloss[w] = ls;
+        }
+        if (QSTATS) {
+            float s1 = g == 0 ? (q[0] + q[1]) + (q[2] + q[3]) : 0.0f;
+            float s2 = g == 0 ? (q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]) : 0.0f;
+            for (int off = 32; off > 0; off >>= 1) {
+                s1 += __shfl_xor(s1, off);
+                s2 += __shfl_xor(s2, off);
+            }
+            if (l == 0) {
+                float *o = a.qstats + (size_t)agent * 6;
+                atomicAdd(o + 0, s1);
+                atomicAdd(o + 1, s2);
+            }
+            if (l < NACT) {
+                const float cnt = (float)__popcll(__ballot(g == 0 && av == l));
+                atomicAdd(a.qstats + (size_t)agent * 6 + 2 + l, cnt);
+            }
+        }
+        __syncthreads();  // 1: H1, H2, DQ, dq / act of every row
+        if (threadIdx.x == 0 && a.loss) {
+            float ls = 0.0f;
+            for (int k = 0; k < 8; k++) ls += sloss[k];
+            a.loss[agent] = ls / (float)B_;
+        }
+        // next agent's indices and rows in flight behind the reductions
+        const int nxt = agent + gridDim.x;
+        if (nxt < a.NA) pref_issue(a, y_in, act_in, nxt, pf);
+        // ---- W1: wave w owns fan-out neurons 16w..16w+15 of layers 2 and 3
+        // dW3 (k-tile w) and db3 from H2 (before its slice turns into dZ2)
+#pragma unroll
+        for (int b0 = 0; b0 < B_; b0 += 32) {
+            const half8 dqf = frag_tr(DQI, 16, b0, 0);
+            G3 = mfma(frag_tr_h(I2, b0, 16 * w), dqf, G3);
+            GB3 = mfma(ones, dqf, GB3);
+        }
+        // this wave's H2 columns -> dZ2 in place (the values dz2 holds above)
+        for (int c = l; c < B_ * 2; c += 64) {
+            const int b = c >> 1, k0 = 16 * w + 8 * (c & 1);
+            half8 *p = reinterpret_cast<half8 *>(I2 + hoff(b, k0));
+            const half8 hv = *p;
+            const float dqb = sdq[b];
+            const half8 w3 = *reinterpret_cast<const half8 *>(w3r + sact[b] * H + k0);
+            half8 o;
+#pragma unroll
+            for (int e = 0; e < 8; e++) o[e] = hv[e] > (h16)0.0f ? (h16)(dqb * (float)w3[e]) : (h16)0.0f;
+            *p = o;
+        }
+        // dW2 (all fan-in tiles, fan-out slice w) and db2
+        {
+            half8 bq[4];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; q4++) {
+                bq[q4] = frag_tr_h(I2, 32 * q4, 16 * w);
+                GB2 = mfma(ones, bq[q4], GB2);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; q4++) G2[t] = mfma(frag_tr_h(I1, 32 * q4, 16 * t), bq[q4], G2[t]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __syncthreads();  // 2: H1 and dZ2 consumed
+        // ---- R2: dZ1 -> I1, X(S) -> I2 (rows of this wave)
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            half4v v;
+#pragma unroll
+            for (int e = 0; e < 4; e++) v[e] = dz1[t >> 1][4 * (t & 1) + e];
+            *reinterpret_cast<half4v *>(I1 + hoff(row, 16 * t + 4 * g)) = v;
+        }
+#pragma unroll
+        for (int s = 0; s < 3; s++) *reinterpret_cast<half8 *>(I2 + hoff<DP>(row, 32 * s + 8 * g)) = bx[s];
+        __syncthreads();  // 3
+        // ---- W2: wave w owns layer-1 neurons 16w..16w+15: dW1 and db1
+#pragma unroll
+        for (int b0 = 0; b0 < B_; b0 += 32) {
+            const half8 bv = frag_tr_h(I1, b0, 16 * w);
+            GB1 = mfma(ones, bv, GB1);
+#pragma unroll
+            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr_h<DP>(I2, b0, 16 * t), bv, G1[t]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();  // 4: the images are rewritten by the next agent
+    }
+    // partial sums of this workgroup, kernel layout (every index written once)
+    float *G = slab + (size_t)blockIdx.x * L::P;
+    if (i < NACT) {
+        *reinterpret_cast<float4 *>(G + L::oW3T + i * H + 16 * w + 4 * g) =
+            make_float4(G3[0], G3[1], G3[2], G3[3]);
+        if (w == 0 && g == 0) G[L::ob3 + i] = GB3[0];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; t++)  // G2[t]: fan-in j = 16t + 4g + e, fan-out k = 16w + i
+        *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(16 * w + i, 16 * t + 4 * g, H)) =
+            make_float4(G2[t][0], G2[t][1], G2[t][2], G2[t][3]);
+    if (g == 0) G[L::ob2 + 16 * w + i] = GB2[0];
+#pragma unroll
+    for (int t = 0; t < 6; t++)
+        if (t < 5 || g < 2)  // tile 5: features 80..87 (89..95 do not exist)
+            *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(16 * w + i, 16 * t + 4 * g)) =
+                make_float4(G1[t][0], G1[t][1], G1[t][2], G1[t][3]);
+    if (g == 0) G[L::ob1 + 16 * w + i] = GB1[0];
+    if (g == 2) G[L::oW1X + 16 * w + i] = G1[5][0];  // feature 88
+}
+
+}  // namespace shk
+
+// Launch of the two passes (called by dmdqn_learn_shared_grad, learn_f16.hip).
+int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *slab, int n_slabs,
+                     hipStream_t s) {
+    using namespace shk;
+    const int next_blocks = (a->NA + 7) / 8 < n_slabs ? (a->NA + 7) / 8 : n_slabs;
+    hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(512), 0, s, *a, y, act);
+    DMDQN_LAUNCH_CHECK("k_shared_next");
+    if (a->qstats)
+        hipLaunchKernelGGL(k_shared_grad<true>, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
+    else
+        hipLaunchKernelGGL(k_shared_grad<false>, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
+    DMDQN_LAUNCH_CHECK("k_shared_grad");
+    return DMDQN_OK;
+}
+
+}  // namespace dmdqn

@@ -83,16 +83,17 @@ __device__ __forceinline__ double np_double(MTWave &w) {
     return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
 }
 
+// draw_rand 0: no rand() draw, every action is randint (test.py:92 random mode)
 __global__ void __launch_bounds__(64) k_act(uint32_t *np_state, int A, double eps, uint32_t rng,
                                             uint32_t mask, const int32_t *greedy,
-                                            int32_t *actions) {
+                                            int32_t *actions, int draw_rand) {
     __shared__ uint32_t mt[MT_N], tmp[MT_N];
     MTWave w{mt, tmp, 0};
     const int e = blockIdx.x;
     uint32_t *g = np_state + (size_t)e * DMDQN_MT_WORDS;
     w.load(g);
     for (int j = 0; j < A; j++) {
-        double r = np_double(w);
+        const double r = draw_rand ? np_double(w) : 0.0;
         int32_t a;
         if (r < eps) {  // dqn_agent.py:263-265
             uint32_t v;
@@ -344,7 +345,19 @@ extern "C" int dmdqn_act(uint32_t *np_state, int E, int A, double eps, int n_act
     uint32_t rng = (uint32_t)(n_actions - 1), mask = rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
     hipLaunchKernelGGL(k_act, dim3(E), dim3(64), 0, as_stream(stream), np_state, A, eps, rng, mask,
-                       greedy, actions);
+                       greedy, actions, 1);
+    DMDQN_LAUNCH_CHECK("k_act");
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_act_uniform(uint32_t *np_state, int E, int A, int n_actions,
+                                 int32_t *actions, void *stream) {
+    DMDQN_REQUIRE(np_state && actions && E > 0 && A > 0, "dmdqn_act_uniform: bad args");
+    DMDQN_REQUIRE(n_actions >= 1, "dmdqn_act_uniform: n_actions must be >= 1");
+    uint32_t rng = (uint32_t)(n_actions - 1), mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    hipLaunchKernelGGL(k_act, dim3(E), dim3(64), 0, as_stream(stream), np_state, A, 1.0, rng, mask,
+                       nullptr, actions, 0);
     DMDQN_LAUNCH_CHECK("k_act");
     return DMDQN_OK;
 }

@@ -563,10 +563,11 @@ __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
 // !kLDS: the same passes on global memory rings.
 template <bool kLDS, bool kAct>
 __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions,
-                                                  int stride, int t0, int K, int max_time,
+                                                  int stride, int t0_arg, int K, int max_time,
                                                   int32_t *halt, int32_t *phase_out,
                                                   int32_t *tspent, uint8_t *done) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
+    const int t0 = S.t_env ? S.t_env[blockIdx.x] : t0_arg;  // the replica's own clock
     const uint64_t prof_t0 = __builtin_amdgcn_s_memrealtime();
     const IdmK P(Pa);
     // topology tables after the state image (kLDS) or alone (global path)
@@ -708,6 +709,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         G.stats[2] = s_running;
         G.stats[3] = s_pending;
         done[blockIdx.x] = (t >= max_time || (s_running + s_pending) == 0) ? 1 : 0;
+        if (S.t_env) S.t_env[blockIdx.x] = t;
     }
     if constexpr (kLDS) {
         // write back: occupied LDS positions (the rest are in HBM already),
@@ -778,9 +780,10 @@ __device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP]
 
 template <int NT>
 __global__ void __launch_bounds__(NT, NT <= 256 ? 2 : 1)
-k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, int t0, int K,
+k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, int t0_arg, int K,
                int max_time, int32_t *halt, int32_t *phase_out, int32_t *tspent, uint8_t *done) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
+    const int t0 = S.t_env ? S.t_env[blockIdx.x] : t0_arg;  // the replica's own clock
     const IdmK P(Pa);
     EnvView G(S, blockIdx.x);
     const int A = G.A, NL = G.NL, cap = G.cap;
@@ -1135,6 +1138,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         G.stats[2] = s_stats[2];
         G.stats[3] = s_stats[3];
         done[blockIdx.x] = (t >= max_time || (s_stats[2] + s_stats[3]) == 0) ? 1 : 0;
+        if (S.t_env) S.t_env[blockIdx.x] = t;
     }
 }
 
@@ -1143,8 +1147,10 @@ __host__ inline size_t sim_reg_lds_bytes(int R, int C) {
     return (size_t)NL * 9 * 4 + (size_t)A * 8 + (size_t)A * 48 + 16 + topo_bytes(R, C);
 }
 
-__global__ void k_sim_reset(dmdqn_sim S) {
+__global__ void k_sim_reset(dmdqn_sim S, const uint8_t *mask) {
+    if (mask && !mask[blockIdx.x]) return;  // only the replicas whose episode ended
     EnvView V(S, blockIdx.x);
+    if (S.t_env && threadIdx.x == 0) S.t_env[blockIdx.x] = 0;
     for (int l = threadIdx.x; l < V.NL; l += blockDim.x) {
         V.head[l] = 0;
         V.cnt[l] = 0;
@@ -1183,9 +1189,13 @@ static int check_sim(const dmdqn_sim *s) {
 }
 
 extern "C" int dmdqn_sim_reset(const dmdqn_sim *sim, void *stream) {
+    return dmdqn_sim_reset_envs(sim, nullptr, stream);
+}
+
+extern "C" int dmdqn_sim_reset_envs(const dmdqn_sim *sim, const uint8_t *mask, void *stream) {
     int rc = check_sim(sim);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_sim_reset, dim3(sim->E), dim3(256), 0, as_stream(stream), *sim);
+    hipLaunchKernelGGL(k_sim_reset, dim3(sim->E), dim3(256), 0, as_stream(stream), *sim, mask);
     DMDQN_LAUNCH_CHECK("k_sim_reset");
     return DMDQN_OK;
 }

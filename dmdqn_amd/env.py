@@ -113,9 +113,13 @@ class TrafficEnv:
         # train.py:233-236 ends an episode when t >= MAX_SIM_TIME or no vehicle is
         # running or pending (getMinExpectedNumber() == 0).  While departures are
         # still scheduled at or after max_sim_time (the shipped demand: 2499.6 s
-        # > 2400 s) the second condition cannot fire, and the host clock decides
-        # without a device read; otherwise step() reads the kernel's per-replica
-        # flags (one sync per step).
+        # > 2400 s) the second condition cannot fire: every replica ends at the
+        # same step, and the host clock decides without a device read.
+        # Otherwise the replicas end when their own demand has drained, and each
+        # restarts on its own `done` as the reference's one env does
+        # (train.py:188-207: traci.load, a fresh episode, the replay kept):
+        # step() reads the kernel's per-replica flags (one sync per step) and
+        # resets those replicas only; each keeps its own clock (t_env).
         self.drains_early = (nveh - 1) * period < cfg.max_sim_time * 1000
         dev = self.device
         z32 = lambda *s: torch.zeros(s, dtype=torch.int32, device=dev)  # noqa: E731
@@ -136,10 +140,11 @@ class TrafficEnv:
         self.t_exit_ao = torch.from_numpy(g.exit_ao.reshape(-1).copy()).to(dev)
         self.t_stats = z32(E, 4)
         self.t_last_det = z32(E, 12 * g.A)
+        self.t_env = z32(E)  # each replica's episode clock (s)
         # the dmdqn_sim arrays in the order of the sim ops (dmdqn_torch.cpp make_sim)
         self._sim_state = [self.t_x, self.t_v, self.t_dst, self.t_head, self.t_cnt, self.t_req,
                            self.t_gfrom, self.t_fx, self.t_fv, self.t_phase_state, self.t_ts,
-                           self.t_qptr, self.t_stats, self.t_last_det]
+                           self.t_qptr, self.t_stats, self.t_last_det, self.t_env]
         self._sim_tables = [self.t_q_off, self.t_q_ids, self.t_vdst, self.t_exit_id,
                             self.t_exit_ao, self.t_q_dst]
         self._sim_dims = [cfg.rows, cfg.cols, E, cap, period, nveh, int(bool(cfg.actuated))]
@@ -154,6 +159,9 @@ class TrafficEnv:
         self.obs = None
         self.t = 0
         self.episode = 0
+        # per replica (host): steps into the current episode, episodes completed
+        self.env_steps = np.zeros(E, np.int64)
+        self.env_episodes = np.zeros(E, np.int64)
         self.sim_hook = None  # callable(before: bool) around the sim launch (bench timing)
 
     # ------------------------------------------------------------ batched API
@@ -161,11 +169,14 @@ class TrafficEnv:
         """traci.load (train.py:190) for every replica; returns obs [E,A,89]."""
         self._ops.sim_reset(self._sim_state, self._sim_tables, self._sim_dims)
         self.t = 0
+        self.env_steps[:] = 0
         self.halt.zero_()
         self.phase.zero_()
         self.tspent.zero_()
         self.local, self.obs, _ = K.observe(self.R, self.C, self.halt, self.phase, self.tspent,
                                             self.mode)
+        # the state a replica restarts from (identical for every replica)
+        self._local0, self._obs0 = self.local[0].clone(), self.obs[0].clone()
         return self.obs
 
     def advance(self):
@@ -198,19 +209,36 @@ class TrafficEnv:
         prev = self.local
         self.local, self.obs, reward = K.observe(self.R, self.C, self.halt, self.phase,
                                                  self.tspent, self.mode, prev_local=prev)
+        info = {"simulation_time": float(self.t), "done_flags": self.done_u8}
         if self.drains_early:
-            # the reference rule per replica (done_u8, from the last substep);
-            # the transition of replica e carries its own flag, and the episode
-            # (one shared clock) ends once every replica is done -- for E = 1,
-            # train.py's `while not done` exactly
-            flags = self.done_u8.cpu()
-            done_out = self.done_u8.clone()
+            # the reference rule per replica (done_u8, from the last substep):
+            # the transition of replica e carries its own flag, and a replica
+            # whose episode ended restarts now, alone (train.py:188-207);
+            # info["obs_next"] is what the next act sees (the restart state for
+            # those replicas).  `done` is True when every replica ended at this
+            # step -- for E = 1, train.py's `while not done` exactly.
+            flags = self.done_u8.cpu().numpy().astype(bool)
+            info["done"] = self.done_u8.clone()
+            self.env_steps += 1
             done = bool(flags.all())
+            obs_next = self.obs
+            if flags.any():
+                self._ops.sim_reset(self._sim_state, self._sim_tables, self._sim_dims,
+                                    info["done"])
+                m = info["done"].bool().view(self.E, 1, 1)
+                self.local = torch.where(m, self._local0, self.local)
+                obs_next = torch.where(m, self._obs0, self.obs)
+                self.env_episodes[flags] += 1
+                self.env_steps[flags] = 0
+            info["obs_next"] = obs_next
+            info["restarted"] = flags
         else:
             # shared clock and demand horizon: `done` is uniform and known on
             # the host without a device sync
-            done = done_out = self.t >= cfg.max_sim_time
-        info = {"simulation_time": float(self.t), "done_flags": self.done_u8, "done": done_out}
+            done = info["done"] = self.t >= cfg.max_sim_time
+            self.env_steps += 1
+            if done:
+                self.env_episodes += 1
         return self.obs, reward, done, info
 
     def stats(self):

@@ -8,15 +8,14 @@ of a single batched TrafficEnv:
     for the numpy stream (set_seeds(episode_seed), test.py:52);
   * modes: 'dqn' -- greedy online-Q action, with eval_epsilon exploration
     drawn as np.random.rand() < eps then randint (test.py:84-87); 'random' --
-    a uniform action (test.py:92 draws only randint(0, 4); this harness uses
-    the training-path act at eps = 1, rand() then randint, so the two action
-    streams differ while both are uniform); 'fixed' -- the
+    np.random.randint(0, 4) alone per agent (test.py:92-93); 'fixed' -- the
     cycle [(action 0, 30 s), (action 2, 30 s)] advanced by step_duration
     before each choice (test.py:93-107, :214-216);
   * per episode: total_reward = sum over steps and agents of the env reward,
     avg_reward_per_agent = total / A, avg_step_queue_sum = mean over agent-steps
     of sum(obs[:12]) of the observation the action was chosen from
-    (test.py:124-131, :137-139), steps;
+    (test.py:124-131, :137-139), steps -- each replica's own, up to its own
+    `done` (a replica whose demand drains early stops counting there);
   * summary per mode: mean / std of total_reward and avg_step_queue_sum, mean
     steps, episode count (test.py:237-245).
 The reward is the training path's (train.py:254, A-3) -- the reference's
@@ -89,26 +88,41 @@ def run_mode(env_cfg: EnvConfig, mode, episodes=10, eval_seed_start=10000, eval_
     obs = env.reset()
     total = torch.zeros(E, dtype=torch.float64, device=dev)
     qsum = torch.zeros(E, dtype=torch.float64, device=dev)
-    steps = 0
-    done = False
-    while not done:
+    # each replica is one evaluation episode: it counts until its own `done`
+    # (test.py:75, :115-133); a replica whose demand drained restarts in the
+    # env and is masked out from then on
+    ended = torch.zeros(E, dtype=torch.bool, device=dev)
+    ended_host = np.zeros(E, dtype=bool)
+    steps = np.zeros(E, dtype=np.int64)
+    step = 0
+    while True:
         if mode == "dqn":
             actions = agent.act(obs, eps=eval_epsilon)
         elif mode == "random":
-            actions = K.act(np_state, A, eps=1.0)
+            actions = K.act(np_state, A, uniform=True)  # test.py:92-93: randint only
         else:
-            actions = torch.full((E, A), fixed[steps], dtype=torch.int32, device=dev)
-        qsum += obs[..., :12].sum(dim=(1, 2), dtype=torch.float64)
-        obs, reward, done, _ = env.step(actions)
-        total += reward.sum(dim=1)
-        steps += 1
-        if steps >= max_steps:
-            done = True
+            actions = torch.full((E, A), fixed[step], dtype=torch.int32, device=dev)
+        live = (~ended).to(torch.float64)
+        qsum += live * obs[..., :12].sum(dim=(1, 2), dtype=torch.float64)
+        next_obs, reward, done, info = env.step(actions)
+        total += live * reward.sum(dim=1)
+        steps[~ended_host] += 1
+        step += 1
+        if "obs_next" in info:
+            ended |= info["done"].bool()
+            ended_host |= info["restarted"]
+            obs = info["obs_next"]
+        else:
+            obs = next_obs
+            if done:
+                ended_host[:] = True
+        if ended_host.all() or step >= max_steps:  # test.py:133 max_steps_per_episode
+            break
     total = total.cpu().numpy()
     qavg = qsum.cpu().numpy() / (steps * A)
     return [{"mode": mode, "seed": int(env.seeds[e]), "total_reward": float(total[e]),
              "avg_reward_per_agent": float(total[e] / A), "avg_step_queue_sum": float(qavg[e]),
-             "steps": steps} for e in range(E)]
+             "steps": int(steps[e])} for e in range(E)]
 
 
 def evaluate(env_cfg: EnvConfig, modes=("dqn", "random"), episodes=10, eval_seed_start=10000,

@@ -47,14 +47,17 @@ def draw_u32(state, count):
 
 
 # ------------------------------------------------------------------ act
-def act(np_state, A, eps=1.0, n_actions=4, greedy=None, out=None):
+def act(np_state, A, eps=1.0, n_actions=4, greedy=None, out=None, uniform=False):
+    """select_action's draws for E envs x A agents (dqn_agent.py:263-265).
+    uniform=True: np.random.randint(0, n_actions) alone per agent, the draw of
+    the reference evaluation's random mode (src/scripts/test.py:92-93)."""
     E = np_state.shape[0]
     _check(np_state, torch.int32, (E, MT_WORDS), "np_state")
     if out is None:
         out = torch.empty((E, A), dtype=torch.int32, device=np_state.device)
     if greedy is not None:
         _check(greedy, torch.int32, (E, A), "greedy")
-    _ops().act(np_state, A, float(eps), n_actions, greedy, out)
+    _ops().act(np_state, A, float(eps), n_actions, greedy, out, bool(uniform))
     return out
 
 
@@ -94,8 +97,8 @@ class ReplayRing:
         self.d = torch.zeros((NA, cap), dtype=torch.uint8, **z)
         self.err = torch.zeros(1, dtype=torch.int32, **z)
         self.total = 0
-        self._err_host = None  # pinned copy of err in flight (poll)
-        self._err_event = None
+        self._err_slots = None  # POLL_LAG pinned copies of err in flight (poll)
+        self._poll_i = 0
 
     def __len__(self):
         return min(self.total, self.cap)
@@ -123,20 +126,30 @@ class ReplayRing:
 
     def poll(self):
         """Deferred check without stalling the stream: raise if the flag copied
-        at the previous poll was set, then start an asynchronous copy of the
-        current flag into pinned host memory.  A bad store therefore raises at
-        the next poll (the product path polls after every store, so one step
-        later) -- the reference stores float32 rows (dqn_agent.py:39-56), and
-        this build's int8 rows must never silently hold a rounded value."""
-        if self._err_event is not None:
-            self._err_event.synchronize()  # recorded a step ago: long complete
-            if int(self._err_host[0]) != 0:
+        POLL_LAG polls ago was set, then start an asynchronous copy of the
+        current flag into pinned host memory.  The flag is sticky, so a bad
+        store raises at most POLL_LAG polls later (the product path polls after
+        every store) while the host keeps up to POLL_LAG steps of work queued
+        ahead of the GPU; episode ends and checkpoint saves call check(), which
+        waits.  The reference stores float32 rows (dqn_agent.py:39-56), and this
+        build's int8 rows must never silently hold a rounded value."""
+        if self._err_slots is None:
+            self._err_slots = [(torch.zeros(1, dtype=torch.int32, pin_memory=True),
+                                torch.cuda.Event()) for _ in range(POLL_LAG)]
+            self._err_live = [False] * POLL_LAG
+        i = self._poll_i % POLL_LAG
+        host, ev = self._err_slots[i]
+        if self._err_live[i]:
+            ev.synchronize()  # recorded POLL_LAG steps ago: normally long complete
+            if int(host[0]) != 0:
                 raise _lib.DmdqnError(_RANGE_MSG)
-        else:
-            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            self._err_event = torch.cuda.Event()
-        self._err_host.copy_(self.err, non_blocking=True)
-        self._err_event.record()
+        host.copy_(self.err, non_blocking=True)
+        ev.record()
+        self._err_live[i] = True
+        self._poll_i += 1
+
+
+POLL_LAG = 4  # steps the host may run ahead of the replay range check
 
 
 _RANGE_MSG = ("replay_store: an observation value is not an integer in [-128, 127]; the int8 "

@@ -18,9 +18,11 @@ from . import _lib
 # which operator wraps which C entry point (include/dmdqn.h)
 ENTRY_POINTS = {
     "dmdqn_mt_seed_np": "mt_seed", "dmdqn_mt_seed_py": "mt_seed",
-    "dmdqn_mt_draw_u32": "mt_draw_u32", "dmdqn_act": "act", "dmdqn_observe": "observe",
+    "dmdqn_mt_draw_u32": "mt_draw_u32", "dmdqn_act": "act", "dmdqn_act_uniform": "act",
+    "dmdqn_observe": "observe",
     "dmdqn_replay_store": "replay_store", "dmdqn_replay_sample": "replay_sample",
-    "dmdqn_sim_reset": "sim_reset", "dmdqn_sim_step": "sim_step", "dmdqn_learn": "learn_step",
+    "dmdqn_sim_reset": "sim_reset", "dmdqn_sim_reset_envs": "sim_reset",
+    "dmdqn_sim_step": "sim_step", "dmdqn_learn": "learn_step",
     "dmdqn_learn_shared_grad": "learn_shared_grad", "dmdqn_adam": "adam",
     "dmdqn_target_sync": "target_sync", "dmdqn_q_argmax": "q_argmax",
     "dmdqn_q_argmax_shared": "q_argmax",

@@ -43,11 +43,19 @@ P *optr(const OptT &t, at::ScalarType st, const char *name, int64_t numel = -1) 
     return t.has_value() ? dptr<P>(*t, st, name, numel) : nullptr;
 }
 
-// a 16-bit shadow (f16 or bf16) as raw uint16 storage
-uint16_t *h16ptr(const OptT &t, const char *name) {
+// a 16-bit shadow (f16 or bf16) as raw uint16 storage.  precision (1 = f16,
+// 2 = bf16; -1 = either) must match the dtype, so bf16 bits never land in an
+// f16 tensor; min_numel > 0 checks the size (NW * Ph, Ph >= P).
+uint16_t *h16ptr(const OptT &t, const char *name, int64_t precision = -1, int64_t min_numel = 0) {
     if (!t.has_value()) return nullptr;
     TORCH_CHECK(t->scalar_type() == at::kHalf || t->scalar_type() == at::kBFloat16, name,
                 " must be float16 or bfloat16");
+    TORCH_CHECK(precision < 0 || (precision == 1 && t->scalar_type() == at::kHalf) ||
+                    (precision == 2 && t->scalar_type() == at::kBFloat16),
+                name, " dtype ", t->scalar_type(), " does not match precision ", precision,
+                " (1 = float16, 2 = bfloat16)");
+    TORCH_CHECK(t->numel() >= min_numel, name, " holds ", t->numel(), " elements, needs ",
+                min_numel);
     TORCH_CHECK(t->is_cuda() && t->is_contiguous(), name, " must be a contiguous device tensor");
     return reinterpret_cast<uint16_t *>(t->data_ptr());
 }
@@ -81,15 +89,20 @@ void mt_draw_u32(Tensor &state, int64_t count, Tensor &out) {
 }
 
 void act(Tensor &np_state, int64_t A, double eps, int64_t n_actions, const OptT &greedy,
-         Tensor &actions) {
+         Tensor &actions, bool uniform) {
     const int64_t E = np_state.numel() / MT;
     auto s = dptr<uint32_t>(np_state, at::kInt, "np_state", E * MT);
     auto gr = optr<int32_t>(greedy, at::kInt, "greedy", E * A);
     auto out = dptr<int32_t>(actions, at::kInt, "actions", E * A);
     c10::hip::HIPGuardMasqueradingAsCUDA g(np_state.device());
-    check(dmdqn_act(s, (int)E, int32_of(A, "A"), eps, int32_of(n_actions, "n_actions"), gr, out,
-                    stream_of(np_state)),
-          "dmdqn_act");
+    if (uniform)
+        check(dmdqn_act_uniform(s, (int)E, int32_of(A, "A"), int32_of(n_actions, "n_actions"), out,
+                                stream_of(np_state)),
+              "dmdqn_act_uniform");
+    else
+        check(dmdqn_act(s, (int)E, int32_of(A, "A"), eps, int32_of(n_actions, "n_actions"), gr, out,
+                        stream_of(np_state)),
+              "dmdqn_act");
 }
 
 // ---------------------------------------------------------------- observe
@@ -149,11 +162,11 @@ void replay_sample(Tensor &py_state, int64_t A, int64_t n, int64_t k, Tensor &id
 
 // ---------------------------------------------------------------- simulator
 // state (mutable, in order): x, v, dst, head, cnt, req, gfrom, fx, fv, tl_phase,
-// tl_ts, qptr, stats, last_det; tables: q_off, q_ids, vdst, exit_id, exit_ao,
-// q_dst; dims: R, C, E, cap_lane, period_ms, nveh, actuated.
+// tl_ts, qptr, stats, last_det[, t_env]; tables: q_off, q_ids, vdst, exit_id,
+// exit_ao, q_dst; dims: R, C, E, cap_lane, period_ms, nveh, actuated.
 dmdqn_sim make_sim(at::TensorList state, at::TensorList tables, at::IntArrayRef dims) {
-    TORCH_CHECK(state.size() == 14 && tables.size() == 6 && dims.size() == 7,
-                "sim: 14 state tensors, 6 tables, 7 dims");
+    TORCH_CHECK((state.size() == 14 || state.size() == 15) && tables.size() == 6 && dims.size() == 7,
+                "sim: 14 state tensors (+ t_env), 6 tables, 7 dims");
     dmdqn_sim s{};
     s.R = (int)dims[0]; s.C = (int)dims[1]; s.E = (int)dims[2]; s.cap_lane = (int)dims[3];
     s.period_ms = (int)dims[4]; s.nveh = (int)dims[5]; s.actuated = (int)dims[6];
@@ -173,6 +186,7 @@ dmdqn_sim make_sim(at::TensorList state, at::TensorList tables, at::IntArrayRef 
     s.qptr = dptr<int32_t>(state[11], at::kInt, "qptr", E * 4 * A);
     s.stats = dptr<int32_t>(state[12], at::kInt, "stats", E * 4);
     s.last_det = dptr<int32_t>(state[13], at::kInt, "last_det", E * 12 * A);
+    s.t_env = state.size() == 15 ? dptr<int32_t>(state[14], at::kInt, "t_env", E) : nullptr;
     s.q_off = dptr<int32_t>(tables[0], at::kInt, "q_off", E * (4 * A + 1));
     s.q_ids = dptr<uint16_t>(tables[1], at::kShort, "q_ids", E * s.nveh);
     s.vdst = dptr<uint16_t>(tables[2], at::kShort, "vdst", E * s.nveh);
@@ -182,10 +196,12 @@ dmdqn_sim make_sim(at::TensorList state, at::TensorList tables, at::IntArrayRef 
     return s;
 }
 
-void sim_reset(at::TensorList state, at::TensorList tables, at::IntArrayRef dims) {
+void sim_reset(at::TensorList state, at::TensorList tables, at::IntArrayRef dims,
+               const OptT &mask) {
     dmdqn_sim s = make_sim(state, tables, dims);
+    auto m = optr<uint8_t>(mask, at::kByte, "mask", s.E);
     c10::hip::HIPGuardMasqueradingAsCUDA g(state[0].device());
-    check(dmdqn_sim_reset(&s, stream_of(state[0])), "dmdqn_sim_reset");
+    check(dmdqn_sim_reset_envs(&s, m, stream_of(state[0])), "dmdqn_sim_reset_envs");
 }
 
 void sim_step(at::TensorList state, at::TensorList tables, at::IntArrayRef dims,
@@ -235,13 +251,16 @@ dmdqn_learn_args make_learn(const Tensor &ring_s, const Tensor &ring_n, const Te
     a.adam_m = optr<float>(adam_m, at::kFloat, "adam_m", NW * P);
     a.adam_v = optr<float>(adam_v, at::kFloat, "adam_v", NW * P);
     a.target = dptr<float>(target, at::kFloat, "target", NW * P);
-    a.target_h = h16ptr(target_h, "target_h");
+    // the kernels read NW rows of Ph = P rounded up to 8 halves
+    const int64_t Ph = (P + 7) / 8 * 8;
+    if (precision == 0) TORCH_CHECK(!target_h.has_value(), "target_h is for precision 1 / 2");
+    a.target_h = h16ptr(target_h, "target_h", precision == 0 ? -1 : precision, NW * Ph);
     a.loss = optr<float>(loss, at::kFloat, "loss", NA);
     a.gamma = (float)gamma; a.alpha = (float)alpha; a.c1 = (float)c1; a.c2 = (float)c2;
     a.eps = (float)eps;
     a.stamps = optr<uint64_t>(stamps, at::kLong, "stamps", NA * 16);
     a.qstats = optr<float>(qstats, at::kFloat, "qstats", NA * 6);
-    a.params_h = h16ptr(params_h, "params_h");
+    a.params_h = h16ptr(params_h, "params_h", precision == 0 ? -1 : precision, NW * Ph);
     a.loss_kind = (int)loss_kind;
     a.rn_out = optr<float>(rn_out, at::kFloat, "rn_out", NA * B);
     return a;
@@ -267,7 +286,7 @@ void learn_shared_grad(const Tensor &ring_s, const Tensor &ring_n, const Tensor 
                        const Tensor &params, const Tensor &target, const Tensor &target_h,
                        const Tensor &params_h, Tensor &loss, int64_t start, double gamma,
                        int64_t loss_kind, const OptT &qstats, const OptT &rn_out, Tensor &slab,
-                       Tensor &grad, double scale) {
+                       Tensor &grad, double scale, const OptT &work) {
     const int64_t NA = loss.numel();
     Tensor p = params, t = target;  // read-only here: the Adam step is a separate op
     dmdqn_learn_args a = make_learn(ring_s, ring_n, ring_a, ring_d, ring_r, idx, p, std::nullopt,
@@ -278,8 +297,10 @@ void learn_shared_grad(const Tensor &ring_s, const Tensor &ring_n, const Tensor 
     const int n_slabs = (int)(slab.numel() / a.P);
     auto sl = dptr<float>(slab, at::kFloat, "slab");
     auto gr = dptr<float>(grad, at::kFloat, "grad", a.P);
+    auto wk = optr<uint8_t>(work, at::kByte, "work",
+                            (int64_t)dmdqn_learn_shared_work_bytes((int)NA));
     c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
-    check(dmdqn_learn_shared_grad(&a, sl, n_slabs, gr, (float)scale, stream_of(params)),
+    check(dmdqn_learn_shared_grad(&a, sl, n_slabs, gr, (float)scale, wk, stream_of(params)),
           "dmdqn_learn_shared_grad");
 }
 
@@ -293,7 +314,8 @@ void adam(Tensor &params, Tensor &adam_m, Tensor &adam_v, Tensor &target, const 
     auto t = dptr<float>(target, at::kFloat, "target", n);
     auto gr = dptr<float>(grad, at::kFloat, "grad", n);
     c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
-    check(dmdqn_adam(w, m, v, t, h16ptr(target_h, "target_h"), h16ptr(params_h, "params_h"), gr,
+    // k_adam writes f16 shadows (the shared net is fp16-only)
+    check(dmdqn_adam(w, m, v, t, h16ptr(target_h, "target_h", 1, n), h16ptr(params_h, "params_h", 1, n), gr,
                      int32_of(n, "n"), (float)gscale, (float)alpha, (float)c1, (float)c2,
                      (float)eps, sync ? 1 : 0, stream_of(params)),
           "dmdqn_adam");
@@ -305,8 +327,10 @@ void target_sync(const Tensor &params, Tensor &target, const OptT &target_h, int
     auto p = dptr<float>(params, at::kFloat, "params");
     auto t = dptr<float>(target, at::kFloat, "target", NW * P);
     const int64_t Ph = target_h.has_value() ? target_h->numel() / NW : P;
+    TORCH_CHECK(!target_h.has_value() || (target_h->numel() % NW == 0 && Ph >= P),
+                "target_h must be [NW, Ph] with Ph >= P");
     c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
-    check(dmdqn_target_sync(p, t, h16ptr(target_h, "target_h"), (int)NW, (int)P, (int)Ph,
+    check(dmdqn_target_sync(p, t, h16ptr(target_h, "target_h", precision), (int)NW, (int)P, (int)Ph,
                             (int)precision, stream_of(params)),
           "dmdqn_target_sync");
 }
@@ -331,13 +355,13 @@ void q_argmax(const Tensor &params, int64_t hidden, int64_t precision, const Ten
 // shape function beyond "nothing is returned".
 void mt_seed_meta(Tensor &, const Tensor &, const std::string &) {}
 void mt_draw_u32_meta(Tensor &, int64_t, Tensor &) {}
-void act_meta(Tensor &, int64_t, double, int64_t, const OptT &, Tensor &) {}
+void act_meta(Tensor &, int64_t, double, int64_t, const OptT &, Tensor &, bool) {}
 void observe_meta(int64_t, int64_t, const Tensor &, const Tensor &, const Tensor &, int64_t,
                   const OptT &, const OptT &, const OptT &, const OptT &) {}
 void replay_store_meta(int64_t, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                        const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &) {}
 void replay_sample_meta(Tensor &, int64_t, int64_t, int64_t, Tensor &) {}
-void sim_reset_meta(at::TensorList, at::TensorList, at::IntArrayRef) {}
+void sim_reset_meta(at::TensorList, at::TensorList, at::IntArrayRef, const OptT &) {}
 void sim_step_meta(at::TensorList, at::TensorList, at::IntArrayRef, at::ArrayRef<double>,
                    const OptT &, int64_t, int64_t, int64_t, int64_t, Tensor &, Tensor &, Tensor &,
                    Tensor &) {}
@@ -348,7 +372,8 @@ void learn_step_meta(const Tensor &, const Tensor &, const Tensor &, const Tenso
 void learn_shared_grad_meta(const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, Tensor &, int64_t, double, int64_t,
-                            const OptT &, const OptT &, Tensor &, Tensor &, double) {}
+                            const OptT &, const OptT &, Tensor &, Tensor &, double,
+                            const OptT &) {}
 void adam_meta(Tensor &, Tensor &, Tensor &, Tensor &, const OptT &, const OptT &, const Tensor &,
                double, double, double, double, double, bool) {}
 void target_sync_meta(const Tensor &, Tensor &, const OptT &, int64_t) {}
@@ -363,8 +388,9 @@ TORCH_LIBRARY(dmdqn, m) {
     m.def("mt_seed(Tensor(a!) state, Tensor seeds, str kind) -> ()");
     m.def("mt_draw_u32(Tensor(a!) state, int count, Tensor(b!) out) -> ()");
     // DQNAgent.select_action (dqn_agent.py:246-274)
+    // (uniform: test.py:92-93's randint-only draw)
     m.def("act(Tensor(a!) np_state, int A, float eps, int n_actions, Tensor? greedy, "
-          "Tensor(b!) actions) -> ()");
+          "Tensor(b!) actions, bool uniform=False) -> ()");
     // get_own_state / build_state_vector / rewards (order_lanes.py:430-555, train.py:159-165,254)
     m.def("observe(int R, int C, Tensor halt, Tensor phase, Tensor tspent, int mode, "
           "Tensor(a!)? local, Tensor(b!)? obs, Tensor? prev_local, Tensor(c!)? reward) -> ()");
@@ -375,7 +401,7 @@ TORCH_LIBRARY(dmdqn, m) {
     // random.sample(self.buffer, k) (dqn_agent.py:63)
     m.def("replay_sample(Tensor(a!) py_state, int A, int n, int k, Tensor(b!) idx) -> ()");
     // traci.load (train.py:190); setPhase x A + simulationStep x K (train.py:225-236)
-    m.def("sim_reset(Tensor(a!)[] state, Tensor[] tables, int[] dims) -> ()");
+    m.def("sim_reset(Tensor(a!)[] state, Tensor[] tables, int[] dims, Tensor? mask=None) -> ()");
     m.def("sim_step(Tensor(a!)[] state, Tensor[] tables, int[] dims, float[] idm, Tensor? actions, "
           "int stride, int t0, int K, int max_time, Tensor(b!) halt, Tensor(c!) phase, "
           "Tensor(d!) tspent, Tensor(e!) done) -> ()");
@@ -390,7 +416,7 @@ TORCH_LIBRARY(dmdqn, m) {
           "Tensor ring_r, Tensor idx, Tensor params, Tensor target, Tensor target_h, "
           "Tensor params_h, Tensor(a!) loss, int start, float gamma, int loss_kind, "
           "Tensor(b!)? qstats, Tensor(c!)? rn_out, Tensor(d!) slab, Tensor(e!) grad, "
-          "float scale) -> ()");
+          "float scale, Tensor(f!)? work=None) -> ()");
     // Keras-3 Adam (dqn_agent.py:357, A-11) on a flat gradient
     m.def("adam(Tensor(a!) params, Tensor(b!) adam_m, Tensor(c!) adam_v, Tensor(d!) target, "
           "Tensor(e!)? target_h, Tensor(f!)? params_h, Tensor grad, float gscale, float alpha, "

@@ -99,15 +99,7 @@ class Trainer:
         agent.remember(self.obs, actions, reward, next_obs, info["done"])  # train.py:274-282
         loss = agent.learn(collect_stats=collect_stats)
         self.last_loss, self.last_reward = loss, reward
-        self.step_count += 1
-        self.total_steps += 1
-        if done:                                               # train.py:188-190
-            agent.ring.check()  # episode boundary: every store so far was exact
-            self.episode += 1
-            self.step_count = 0
-            self.obs = env.reset()
-        else:
-            self.obs = next_obs
+        self.obs = self._after_step(done, next_obs, info)
         return StepStats(loss is not None, done)
 
     def _step_side_sample(self, collect_stats):
@@ -132,15 +124,7 @@ class Trainer:
         self._ev_learn = torch.cuda.Event()
         self._ev_learn.record(main)
         self.last_loss, self.last_reward = loss, reward
-        self.step_count += 1
-        self.total_steps += 1
-        if done:                                               # train.py:188-190
-            agent.ring.check()  # episode boundary: every store so far was exact
-            self.episode += 1
-            self.step_count = 0
-            self.obs = env.reset()
-        else:
-            self.obs = next_obs
+        self.obs = self._after_step(done, next_obs, info)
         return StepStats(loss is not None, done)
 
     def _step_overlap(self, collect_stats):
@@ -169,20 +153,36 @@ class Trainer:
         self._ev_learn = torch.cuda.Event()
         self._ev_learn.record(main)
         self.last_loss, self.last_reward = loss, reward
+        self.obs = self._after_step(done, next_obs, info, side=side, main=main)
+        return StepStats(loss is not None, done)
+
+    def _after_step(self, done, next_obs, info, side=None, main=None):
+        """Counters and the observation the next act sees (train.py:188-209).
+        Replicas that restart on their own `done` (env.drains_early) were reset
+        by env.step itself: info["obs_next"] already holds their restart state.
+        Otherwise every replica ends together, and the whole batch reloads."""
+        env, agent = self.env, self.agent
         self.step_count += 1
         self.total_steps += 1
-        if done:                                               # train.py:188-190
-            agent.ring.check()  # episode boundary: every store so far was exact
-            self.episode += 1
-            self.step_count = 0
-            with torch.cuda.stream(side):
-                self.obs = env.reset()
-            main.wait_stream(side)
-            self.obs.record_stream(main)
-            env.local.record_stream(main)
-        else:
-            self.obs = next_obs
-        return StepStats(loss is not None, done)
+        if "obs_next" in info:
+            if info["restarted"].any():
+                agent.ring.check()  # episode boundary: every store so far was exact
+                self.episode = int(env.env_episodes.min())
+                self.step_count = int(env.env_steps.min())
+            return info["obs_next"]
+        if not done:
+            return next_obs
+        agent.ring.check()  # episode boundary: every store so far was exact
+        self.episode += 1                                      # train.py:188-190
+        self.step_count = 0
+        if side is None:
+            return env.reset()
+        with torch.cuda.stream(side):
+            obs = env.reset()
+        main.wait_stream(side)
+        obs.record_stream(main)
+        env.local.record_stream(main)
+        return obs
 
     def join_streams(self):
         """Call after changing trainer state on the caller's stream between

@@ -87,6 +87,12 @@ int dmdqn_mt_draw_u32(uint32_t *state, int E, int count, uint32_t *out, void *st
 int dmdqn_act(uint32_t *np_state, int E, int A, double eps, int n_actions,
               const int32_t *greedy, int32_t *actions, void *stream);
 
+/* A uniform action per agent drawn as np.random.randint(0, n_actions) alone
+ * (no rand() first): the 'random' mode of the reference's evaluation script
+ * (src/scripts/test.py:92-93).  Per env, agents in junction order. */
+int dmdqn_act_uniform(uint32_t *np_state, int E, int A, int n_actions, int32_t *actions,
+                      void *stream);
+
 /* ------------------------------------------------------------------ observe
  * Replaces order_lanes.get_own_state (:430-499), build_state_vector (:502-555)
  * and the reward lines of train.py (:159-165, :254).
@@ -160,6 +166,12 @@ typedef struct dmdqn_sim {
     int32_t *last_det;           /* [E][12A] substep of the last detection on each
                                     observed lane's detector (actuated mode; the
                                     reset writes -1000)                        */
+    int32_t *t_env;              /* [E] each replica's episode clock (s), or NULL:
+                                    every replica runs at the step's t0.  With it
+                                    a replica restarts on its own `done`
+                                    (dmdqn_sim_reset_envs) as the reference's one
+                                    env does (train.py:188-207, 233-236); the
+                                    step reads t0 from it and advances it by K */
 } dmdqn_sim;
 
 /* Car-following / geometry constants (SUMO passenger defaults + grid_3x3
@@ -176,9 +188,14 @@ typedef struct dmdqn_idm {
  * origin queues rewound (replaces traci.load, train.py:190). */
 int dmdqn_sim_reset(const dmdqn_sim *sim, void *stream);
 
+/* dmdqn_sim_reset for the envs e with mask[e] != 0 only (uint8 [E], device):
+ * the replicas whose episode ended restart while the others run on. */
+int dmdqn_sim_reset_envs(const dmdqn_sim *sim, const uint8_t *mask, void *stream);
+
 /* One RL step for every env (train.py:225-236): if actions != NULL set
  * phase = action_stride*action (ACTION_MAP {0:0,1:3,2:6,3:9}) with the phase
- * timer restarted at t0, then run K one-second substeps from time t0.
+ * timer restarted at t0, then run K one-second substeps from time t0 (with
+ * sim->t_env: t0 = t_env[e] per replica, and t_env[e] += K).
  * With sim->actuated, phase 0 is SUMO's actuated phase (grid_3x3.net.xml:894):
  * it ends once it has run minDur = 5 s and no vehicle has been over a detector
  * of its green lanes for more than max_gap, or at maxDur = 50 s; the other
@@ -279,9 +296,14 @@ int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, int pr
  * args: params / target / target_h point at ONE network ([P], [Ph]); adam_m /
  * adam_v are not used here; loss [NA] receives each agent's loss.
  * slab: f32 [n_slabs][P] scratch, one partial sum per persistent workgroup
- * (one workgroup per CU: n_slabs = 256 on MI355X).  precision must be 1. */
+ * (one workgroup per CU: n_slabs = 256 on MI355X).  precision must be 1.
+ * work: device scratch of dmdqn_learn_shared_work_bytes(NA) bytes (each batch
+ * row's TD target and action between the kernel's two passes: the S' pass
+ * with both nets resident in LDS, then the gradient pass); NULL runs the
+ * older one-pass kernel (one agent at a time per workgroup). */
 int dmdqn_learn_shared_grad(const dmdqn_learn_args *args, float *slab, int n_slabs, float *grad,
-                            float scale, void *stream);
+                            float scale, void *work, void *stream);
+size_t dmdqn_learn_shared_work_bytes(int NA);
 
 /* Keras-3 Adam (dqn_agent.py:357, A-11) on n flat parameters with gradient
  * gscale * grad[i]; params_h (when not NULL) receives the f16 copy of every

@@ -42,11 +42,11 @@ def test_python_bindings_cover_header(lib):
     ctypes signature (the C-ABI tests' path)."""
     from dmdqn_amd import _lib, agent, env, ops  # noqa: F401  (agent registers its signatures)
     declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version", "dmdqn_debug_status",
-                                   "dmdqn_debug_build"}
+                                   "dmdqn_debug_build", "dmdqn_learn_shared_work_bytes"}
     host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy"}
     assert declared - host_only <= set(ops.ENTRY_POINTS), sorted(declared - host_only -
                                                                  set(ops.ENTRY_POINTS))
-    ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_step"}
+    ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_reset_envs", "dmdqn_sim_step"}
     assert ctypes_only <= set(_lib.SIGNATURES), sorted(ctypes_only - set(_lib.SIGNATURES))
 
 
@@ -64,6 +64,9 @@ def test_torch_ops_registered_without_gpu(lib):
 
 def test_version_and_error_string(lib):
     assert lib.dmdqn_version() >= 1
+    import ctypes
+    lib.dmdqn_learn_shared_work_bytes.restype = ctypes.c_size_t
+    assert lib.dmdqn_learn_shared_work_bytes(16384) == 16384 * 128 * 5
     assert isinstance(lib.dmdqn_last_error(), bytes)
 
 

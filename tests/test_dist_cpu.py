@@ -72,7 +72,7 @@ def _shared_worker(rank, ws, port, q):
     P = 8
     seen = {}
 
-    def learn_shared_grad(*args):
+    def learn_shared_grad(*args, **kw):
         fake.grad.copy_(torch.arange(P, dtype=torch.float32) * (rank + 1))
         seen["scale"] = args[-1]
 
@@ -86,7 +86,7 @@ def _shared_worker(rank, ws, port, q):
                            cfg=AG.AgentConfig(), loss=None, rn_out=None,
                            slab=torch.zeros((2, P)), grad=torch.zeros(P),
                            params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
-                           target=torch.zeros(P), target_h=None, params_h=None,
+                           target=torch.zeros(P), target_h=None, params_h=None, shared_work=None,
                            _ops=SimpleNamespace(learn_shared_grad=learn_shared_grad, adam=adam))
     AG.BatchedDQN._learn_shared(fake, 1e-3, 0.1, 1e-3, 1e-7, True, None)
     q.put((rank, seen))

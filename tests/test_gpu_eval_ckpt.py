@@ -63,7 +63,8 @@ def test_export_loads_into_dqnagent(tmp_path):
 
 
 def test_random_mode_reproduces_oracle():
-    """Random-mode evaluation episodes == the oracle loop with the same seeds."""
+    """Random-mode evaluation episodes == the oracle with the same seeds; the
+    action stream is test.py:92-93's: np.random.randint(0, 4) alone per agent."""
     rows = EV.run_mode(EnvConfig(rows=2, cols=2), "random", episodes=3, eval_seed_start=77,
                        max_steps=40)
     for r in rows:
@@ -73,7 +74,7 @@ def test_random_mode_reproduces_oracle():
         tot, q, t = 0.0, 0.0, 0
         for _ in range(40):
             q += float(L[:, :12].sum())
-            acts = O.act(nps, 4, 1.0)
+            acts = np.array([O.np_randint(nps, 4) for _ in range(4)], np.int32)
             halt, ph, ts, _ = env.step(acts, 3, t, 10, 2400)
             t += 10
             tot += float(np.sum(O.reward(L)))
@@ -81,6 +82,49 @@ def test_random_mode_reproduces_oracle():
         assert r["steps"] == 40
         assert np.isclose(r["total_reward"], tot, rtol=1e-12)
         assert np.isclose(r["avg_step_queue_sum"], q / (40 * 4), rtol=1e-12)
+
+
+def test_uniform_act_is_numpy_randint():
+    """dmdqn_act_uniform: per env, agents in order, np.random.randint(0, n)
+    alone (the numpy stream), for n = 4 and a non-power-of-two n = 3."""
+    from dmdqn_amd import kernels as K
+    seeds = [5, 6, 7]
+    for n in (4, 3):
+        st = K.seed_streams(seeds, "np")
+        a = K.act(st, 9, n_actions=n, uniform=True)
+        b = K.act(st, 9, n_actions=n, uniform=True)
+        for e, s in enumerate(seeds):
+            rs = np.random.RandomState(s)
+            ref = [rs.randint(0, n) for _ in range(18)]
+            np.testing.assert_array_equal(np.concatenate([a[e].cpu().numpy(), b[e].cpu().numpy()]),
+                                          ref)
+
+
+def test_evaluation_steps_per_replica_when_demand_drains():
+    """Replicas whose demand drains at different times each end their own
+    evaluation episode at their own `done` (test.py:75, :115-133): steps,
+    total reward and queue average per replica vs the oracle run of that seed."""
+    cfg = EnvConfig(rows=2, cols=2, end_ms=40_000)
+    rows = EV.run_mode(cfg, "random", episodes=3, eval_seed_start=21, max_steps=200)
+    lengths = set()
+    for r in rows:
+        s = r["seed"]
+        env, nps = O.OracleEnv(2, 2, s, end_ms=40_000), O.np_stream(s)
+        L = O.local_state(np.zeros((4, 12)), np.zeros(4), np.zeros(4), 0)
+        tot, q, t, n, done = 0.0, 0.0, 0, 0, False
+        while not done:
+            q += float(L[:, :12].sum())
+            acts = np.array([O.np_randint(nps, 4) for _ in range(4)], np.int32)
+            halt, ph, ts, done = env.step(acts, 3, t, 10, 2400)
+            t += 10
+            n += 1
+            tot += float(np.sum(O.reward(L)))
+            L = O.local_state(halt, ph, ts, 0)
+        assert r["steps"] == n < 200, (r, n)
+        assert np.isclose(r["total_reward"], tot, rtol=1e-12)
+        assert np.isclose(r["avg_step_queue_sum"], q / (n * 4), rtol=1e-12)
+        lengths.add(n)
+    assert len(lengths) > 1, "the seeds should drain at different steps"
 
 
 def test_fixed_and_dqn_modes_and_cli(tmp_path):
@@ -138,3 +182,23 @@ def test_resume_refuses_a_different_configuration(tmp_path):
     CK.load(path, tr3)
     assert torch.equal(tr3.agent.target_h[:, :tr3.agent.P],
                        tr3.agent.target.to(tr3.agent.target_h.dtype))
+
+
+def test_resume_mismatch_leaves_trainer_untouched(tmp_path):
+    """A checkpoint whose LAST tensor does not fit is refused before anything is
+    copied: the Trainer keeps its own weights, rings and env."""
+    tr = _trainer("fp16")
+    _run(tr, 130)
+    st = CK.trainer_state(tr)
+    st["replay"]["d"] = st["replay"]["d"][:1]  # the last tensor checked
+    path = os.path.join(str(tmp_path), "bad.pt")
+    torch.save(st, path)
+    tr2 = _trainer("fp16")
+    _run(tr2, 3)
+    before = [t.clone() for t in (tr2.agent.params, tr2.agent.adam_m, tr2.env.t_x,
+                                  tr2.agent.ring.s, tr2.agent.np_state)]
+    with pytest.raises(ValueError, match="replay.d"):
+        CK.load(path, tr2)
+    after = (tr2.agent.params, tr2.agent.adam_m, tr2.env.t_x, tr2.agent.ring.s,
+             tr2.agent.np_state)
+    assert all(torch.equal(a, b) for a, b in zip(before, after))

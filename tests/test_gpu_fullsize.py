@@ -6,16 +6,20 @@ oracle on sampled replicas and agents (BASELINE.json configs).
   C3  4x4 grid x 1024 replicas, fp16 (mixed_float16), replay 10000: 16,384
       learn workgroups, 21 GB per ring array (byte offsets past 2^31), 1100
       steps so the sampler runs CPython's set branch (n > 1045)
-  C5  8x8 grid x 256 replicas, one shared network (the 8x8 sim runs from
-      global memory), replay 10000
+  C3' the same past 10,000 steps: wrapped rings, the steady state bench.py
+      times
+  C5  8x8 grid x 256 replicas, one shared network (the 8x8 sim takes the
+      register path), replay 10000
 
 Per step, for sampled replicas (first, middle, last): actions, rewards and
 observations bit-exact vs oracle.OracleLoop (same seeds); once the replay is
 active, every sampled agent's 128 replay indices bit-exact vs CPython's
 random.sample.  At the checked learns, for 8 agents across those replicas: the
-device z-scored rewards bit-exact, the loss vs the 16-bit rounding emulation
-(test_gpu_learn TOL16) and vs the fp32 oracle (rtol 2e-2), and the
-gradient >= 99 % within the emulation's tolerance; every agent's loss finite.
+device z-scored rewards bit-exact, the loss vs oracle.learn_mixed (Keras 3's
+mixed-precision learn, pinned to the reference's own DQNAgent in
+tests/test_learn_mixed_golden_cpu.py; test_gpu_learn TOL16) and vs the fp32
+oracle (rtol 2e-2), and the gradient >= 99 % within the checker's
+tolerance; every agent's loss finite.
 C4 (8 GPUs, env-sharded) is the C3 shard per GPU (tests/test_gpu_multiproc.py
 covers the sharding with real kernels)."""
 import json
@@ -71,7 +75,9 @@ def _check_learn(tr, agents, pre, precision, shared):
         assert np.isfinite(p_now).all() and not np.array_equal(p_now, pre[0][0])
 
 
-def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False):
+def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, sparse_until=0):
+    """sparse_until: before this step, compare with the oracle only every 97th
+    step (the oracle loops still run every step)."""
     cfg = AgentConfig(precision=precision, seed=0, shared_params=shared)
     tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=0), cfg)
     A, ag = tr.env.A, tr.agent
@@ -91,6 +97,8 @@ def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False):
                    for k in ["params", "target", "adam_m", "adam_v"]]
         tr.step()
         outs = [lp.step() for lp in loops]
+        if step < sparse_until and step % 97 and pre is None:
+            continue
         acts, obs, rew = (_rows(x, sampled) for x in (ag.actions, tr.obs, tr.last_reward))
         for i, out in enumerate(outs):
             np.testing.assert_array_equal(acts[i], out["actions"], err_msg=f"step {step} env {i}")
@@ -111,6 +119,24 @@ def test_c3_4x4x1024_fp16_full_size():
     tr = _run_config(4, 4, 1024, "fp16", 1100, {128, 1100})
     assert len(tr.agent.ring) == 1100 and tr.agent.ring.s.numel() > 2 ** 31
     assert tr.episode == 4  # episode boundaries at 240, 480, 720, 960
+    del tr
+    torch.cuda.empty_cache()
+
+
+def test_c3_steady_state_wrapped_rings():
+    """The regime bench.py times: C3 (4x4 x 1024, fp16, replay
+    10,000) driven past 10,000 steps, so every ring is full and wrapped (deque
+    position 0 = the oldest transition at ring slot start != 0,
+    dqn_agent.py:29, 59-85) and the sampler runs CPython's set branch at
+    n = 10,000.  Sampled replicas {0, 511, 1023} vs OracleLoop every 97th step
+    and at every step after the wrap: actions, rewards, observations and replay
+    indices bit-exact; at learns 3 and 5 steps after the wrap, for 8 agents,
+    the device z-score bit-exact and the loss vs the Keras mixed-precision
+    checker (pinned to the reference's own learn) and the fp32 oracle."""
+    cap = 10000
+    tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap)
+    ring = tr.agent.ring
+    assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
     del tr
     torch.cuda.empty_cache()
 

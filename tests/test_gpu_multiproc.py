@@ -32,13 +32,14 @@ def _free_port():
     return p
 
 
-def _run(rank, ws, shared):
+def _run(rank, ws, shared, overlap="none"):
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.env import EnvConfig
     from dmdqn_amd.trainer import Trainer
     E = E_RANK if ws > 1 else E_RANK * 2
     cfg = AgentConfig(precision="fp16", seed=7, shared_params=shared, replay_buffer_size=500)
-    tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=E, seed=100, env_offset=rank * E), cfg)
+    tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=E, seed=100, env_offset=rank * E), cfg,
+                 overlap=overlap)
     idx = []
     for _ in range(STEPS):
         tr.step()
@@ -49,7 +50,7 @@ def _run(rank, ws, shared):
             "idx": np.stack(idx[-3:]), "seeds": tr.env.seeds.copy()}
 
 
-def _worker(rank, ws, port, shared, q):
+def _worker(rank, ws, port, shared, q, overlap="none"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -57,18 +58,18 @@ def _worker(rank, ws, port, shared, q):
     D.init(backend="gloo")
     torch.cuda.set_device(0)
     try:
-        q.put((rank, _run(rank, ws, shared)))
+        q.put((rank, _run(rank, ws, shared, overlap)))
     finally:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def _two_ranks(shared):
+def _two_ranks(shared, overlap="none"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, shared, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, shared, q, overlap)) for r in range(2)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(2))
@@ -107,3 +108,52 @@ def test_c5_shared_allreduce_equals_union_batch():
     d = np.abs(res[0]["params"] - one["params"]).max()
     print(f"C5 2-rank vs union: max |dw| {d:.3g}")
     np.testing.assert_allclose(res[0]["params"], one["params"], rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_bench_two_rank_launch(shared):
+    """The launch the driver's multi-GPU bench uses (torch.distributed.run,
+    one rank per GPU, max-over-ranks timing), rehearsed with 2 ranks on this
+    one GPU (DMDQN_DEVICE_OVERRIDE=0, gloo: RCCL needs a device per rank):
+    rank 0 prints one JSON line with n_gpus 2, the whole-job value over both
+    ranks' replicas, "weak" scaling; the shared run goes through the C5
+    gradient all-reduce every learn."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    E = 64
+    args = ["--rows", "8", "--cols", "8", "--shared"] if shared else ["--rows", "2", "--cols", "2"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--envs", str(E), "--steps", "5",
+           "--warmup", "2", "--prefill-steps", "130", "--no-cpu-baseline",
+           "--dist-backend", "gloo"] + args
+    env = dict(os.environ, DMDQN_DEVICE_OVERRIDE="0", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    A = 64 if shared else 4
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert out["config"]["global_envs"] == 2 * E
+    assert out["steps"] == 5 and out["value"] > 0
+    # value = agent-env steps of both ranks / max-over-ranks wall time
+    np.testing.assert_allclose(out["value"], 5 * 2 * E * A / (out["ms_per_step"] * 5 / 1e3),
+                               rtol=2e-3)
+    if shared:
+        assert "all-reduce" in out["config"]["parallelism"]
+
+
+def test_c5_allreduce_beside_next_step_bit_identical():
+    """C5 with the "full" schedule at 2 ranks: the next step's act / sim /
+    observe / sample run on the side stream while this step's shared learn,
+    its gradient all-reduce and Adam run on the main stream -- the
+    all-reduce overlaps the next step's env work.  Weights, losses, replay
+    indices and observations are bit-identical to the sequential order."""
+    seq = _two_ranks(shared=True)
+    ovl = _two_ranks(shared=True, overlap="full")
+    for r in range(2):
+        for k in ("params", "target", "loss", "idx", "obs"):
+            np.testing.assert_array_equal(ovl[r][k], seq[r][k], err_msg=f"rank {r} {k}")

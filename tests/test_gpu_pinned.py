@@ -370,6 +370,9 @@ def test_dropin_replaybuffer_sample_zscore_bit_exact():
 # ---------------------------------------------------------------------------
 # replay range errors on the product path
 def test_remember_non_integer_observation_raises():
+    """A non-int8 observation raises POLL_LAG stores later (the host is not
+    held back by the check), and check() raises at once."""
+    from dmdqn_amd.kernels import POLL_LAG
     ag = BatchedDQN(1, 2, AgentConfig(replay_buffer_size=50))
     good = torch.zeros((1, 2, 89), dtype=torch.float32, device=DEV)
     bad = good.clone()
@@ -377,9 +380,13 @@ def test_remember_non_integer_observation_raises():
     a = torch.zeros((1, 2), dtype=torch.int32, device=DEV)
     r = torch.zeros((1, 2), dtype=torch.float64, device=DEV)
     ag.remember(good, a, r, good, False)
-    ag.remember(bad, a, r, good, False)  # deferred: the next poll raises
+    ag.remember(bad, a, r, good, False)  # deferred
+    for _ in range(POLL_LAG - 1):
+        ag.remember(good, a, r, good, False)
     with pytest.raises(_lib.DmdqnError, match="not an integer"):
         ag.remember(good, a, r, good, False)
+    with pytest.raises(_lib.DmdqnError, match="not an integer"):
+        ag.ring.check()
 
 
 def test_dropin_remember_raises_immediately():
@@ -394,12 +401,14 @@ def test_dropin_remember_raises_immediately():
 
 
 def test_trainer_raises_on_non_integer_observation():
+    """... within POLL_LAG + 1 steps of the bad store."""
+    from dmdqn_amd.kernels import POLL_LAG
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=2, seed=1), AgentConfig(replay_buffer_size=50))
     tr.step()
     tr.obs = tr.obs + 0.25  # a caller feeding its own features
     with pytest.raises(_lib.DmdqnError):
-        tr.step()
-        tr.step()
+        for _ in range(POLL_LAG + 1):
+            tr.step()
 
 
 # ---------------------------------------------------------------------------
@@ -435,3 +444,41 @@ def test_done_when_demand_drains_before_max_time():
         assert n < 240
     d = tr.agent.ring.d[:, :n].cpu().numpy()
     assert (d[:, -1] == 1).all() and (d[:, :-1] == 0).all()
+
+
+def test_replicas_restart_on_their_own_done():
+    """Three replicas whose demand drains at different steps (end_ms 60 s),
+    each vs its own OracleLoop (train.py:188-207 for one env: traci.load when
+    THAT env is done, replay kept): every step's actions, rewards, the
+    observation the next act sees (the restart state after a done), the
+    per-replica done flags stored with the transitions and the replay indices
+    are bit-exact; each replica runs several episodes of its own length."""
+    E, steps = 3, 70
+    tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=E, seed=9, end_ms=60_000),
+                 AgentConfig(replay_buffer_size=500))
+    assert tr.env.drains_early
+    A = tr.env.A
+    loops = [O.OracleLoop(2, 2, int(s), learn=False,
+                          env=O.OracleEnv(2, 2, int(s), end_ms=60_000)) for s in tr.env.seeds]
+    ends = [[] for _ in range(E)]
+    for t in range(steps):
+        tr.step()
+        outs = [lp.step() for lp in loops]
+        acts, rew = tr.agent.actions.cpu().numpy(), tr.last_reward.cpu().numpy()
+        obs = tr.obs.cpu().numpy()
+        d = tr.agent.ring.d[:, t].cpu().numpy().reshape(E, A)
+        for e, out in enumerate(outs):
+            np.testing.assert_array_equal(acts[e], out["actions"], err_msg=f"step {t} env {e}")
+            np.testing.assert_array_equal(rew[e], out["reward"], err_msg=f"step {t} env {e}")
+            np.testing.assert_array_equal(obs[e], loops[e].obs, err_msg=f"step {t} env {e}")
+            assert (d[e] == int(out["done"])).all(), f"step {t} env {e}"
+            if out["done"]:
+                ends[e].append(t)
+            if out["idx"] is not None:
+                np.testing.assert_array_equal(tr.agent.idx[e * A:(e + 1) * A].cpu().numpy(),
+                                              out["idx"], err_msg=f"step {t} env {e}")
+    lens = [np.diff([-1] + x) for x in ends]
+    print("episode lengths per replica:", [list(x) for x in lens])
+    assert all(len(x) >= 2 for x in ends)
+    assert len({tuple(x[:2]) for x in lens}) > 1, "replicas should drain at different steps"
+    assert tr.episode == min(len(x) for x in ends)

@@ -111,5 +111,5 @@ def test_shared_many_agents_across_slabs():
     g_one = torch.empty(ag.P, dtype=torch.float32, device=DEV)
     a = ag.c_learn_args()  # the C ABI directly (the product path uses torch.ops.dmdqn)
     call("dmdqn_learn_shared_grad", C.byref(a), ptr(slab1), 1, ptr(g_one), C.c_float(1.0 / ag.NA),
-         stream_of())
+         ptr(ag.shared_work), stream_of())
     torch.testing.assert_close(g_one, g1, rtol=1e-4, atol=1e-6 * float(g1.abs().max()))

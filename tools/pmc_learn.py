@@ -3,7 +3,8 @@ the learn kernel, with the gfx950 corrections of MI355X_MICROARCH.md (HBM):
   * FETCH_SIZE (KB) reports 1/2 of the bytes of a wide coalesced stream -> x2
   * WRITE_SIZE (KB) is exact for 16-byte stores
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (TCC slots).
-Usage: python tools/pmc_learn.py <fetch_csv> <write_csv> <workload_key> [kernel_substr]
+Usage: python tools/pmc_learn.py <fetch_csv> <write_csv> <workload_key> [kernel_substr] [source]
+(source: where the passes were run, e.g. "profiles/r03/c3 @ <commit>").
 Writes/updates profiles/learn_pmc.json."""
 import csv
 import json
@@ -23,6 +24,7 @@ def per_kernel(path, counter, substr):
 def main():
     fetch_csv, write_csv, key = sys.argv[1:4]
     substr = sys.argv[4] if len(sys.argv) > 4 else "k_learn"
+    source = sys.argv[5] if len(sys.argv) > 5 else None
     fv = per_kernel(fetch_csv, "FETCH_SIZE", substr)
     wv = per_kernel(write_csv, "WRITE_SIZE", substr)
     if not fv or not wv:
@@ -39,6 +41,8 @@ def main():
               "FETCH_SIZE_KB_raw": fetch_kb, "WRITE_SIZE_KB_raw": write_kb,
               "hbm_bytes_per_launch": int(round((2.0 * fetch_kb + write_kb) * 1024)),
               "correction": "fetch x2 (gfx950 FETCH_SIZE reads 1/2 of wide streams), write x1"}
+    if source:
+        d[key]["source"] = source
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d[key]))

@@ -1,16 +1,51 @@
 #!/bin/bash
-# rocprofv3 --kernel-trace --stats of the C2 and C5 bench configurations (run via
-# gpurun from the repo root); summaries land in gpurun_out/cfgprof/<name>.csv.
+# rocprofv3 evidence for the one-GPU BASELINE configurations (run via gpurun
+# from the repo root).  Per configuration:
+#   1. --kernel-trace --stats of the default bench (steady state, n = 10000)
+#   2. --pmc FETCH_SIZE and 3. --pmc WRITE_SIZE (separate passes, TCC slots),
+#      reduced by tools/pmc_learn.py into profiles/learn_pmc.json for the learn
+#      kernel and k_sim_step (gfx950 corrections: FETCH x2, WRITE x1)
+#   4. --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES (own pass)
+# Summaries are copied to gpurun_out/<tag>/<cfg>/ for committing under
+# profiles/<round>/.  Every GPU step has its own time limit; `set -e` stops the
+# chain at the first failure.
+# usage: bash tools/profile_configs.sh <tag> c2|c3|c5 ...
 set -e
+TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/cfgprof
-mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o run \
-    -- python3 $R/bench.py --rows 2 --cols 2 --envs 256 --precision bf16 --steps 20 --warmup 5 \
-    --no-cpu-baseline > $O/c2.json 2> $O/c2.err
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o run \
-    -- python3 $R/bench.py --shared --rows 8 --cols 8 --envs 256 --steps 20 --warmup 5 \
-    --no-cpu-baseline > $O/c5.json 2> $O/c5.err
-cp "$(find $O/c2 -name '*kernel_stats.csv' | head -n 1)" $O/c2_kernel_stats.csv
-cp "$(find $O/c5 -name '*kernel_stats.csv' | head -n 1)" $O/c5_kernel_stats.csv
+for CFG in "$@"; do
+    case $CFG in
+        c2) ARGS="--rows 2 --cols 2 --envs 256 --precision bf16"; KEY=2x2x256_bf16; LK=k_learn_bf16 ;;
+        c3) ARGS="--rows 4 --cols 4 --envs 1024 --precision fp16"; KEY=4x4x1024_fp16; LK=k_learn_f16 ;;
+        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK=k_learn_shared ;;
+        *) echo "unknown config $CFG"; exit 2 ;;
+    esac
+    O=$R/gpurun_out/$TAG/$CFG
+    mkdir -p $O
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run \
+        -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline $ARGS > $O/bench_prof.json 2> $O/bench_prof.err
+    echo "$CFG stats done"
+    timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcF -o run \
+        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline $ARGS > $O/pmcF.log 2>&1
+    echo "$CFG fetch done"
+    timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcW -o run \
+        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline $ARGS > $O/pmcW.log 2>&1
+    echo "$CFG write done"
+    timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES \
+        --output-format csv -d $O/pmcM -o run \
+        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline $ARGS > $O/pmcM.log 2>&1
+    echo "$CFG mfma done"
+    F=$(find $O/pmcF -name '*counter_collection.csv' | head -n 1)
+    W=$(find $O/pmcW -name '*counter_collection.csv' | head -n 1)
+    M=$(find $O/pmcM -name '*counter_collection.csv' | head -n 1)
+    (cd $R && python3 tools/pmc_learn.py "$F" "$W" "$KEY" "$LK" "profiles/$TAG/$CFG" &&
+         python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_sim" k_sim_step "profiles/$TAG/$CFG" &&
+         python3 tools/pmc_mfma.py "$M" "$LK" > $O/mfma_busy.json)
+    cp "$(find $O/stats -name '*kernel_stats.csv' | head -n 1)" $O/kernel_stats.csv
+    gzip -c "$F" > $O/fetch_size_counter_collection.csv.gz
+    gzip -c "$W" > $O/write_size_counter_collection.csv.gz
+    gzip -c "$M" > $O/mfma_counter_collection.csv.gz
+    cp $R/profiles/learn_pmc.json $O/
+    rm -rf $O/stats $O/pmcF $O/pmcW $O/pmcM
+done
