@@ -126,18 +126,37 @@ __global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a,
     if (lg == 2) G[L::oW1X + 16 * w + lr] = G1[5][0];  // feature 88
 }
 
-// grad[i] = scale * sum_w slab[w][i]  (fixed order over workgroups)
-__global__ void __launch_bounds__(256) k_reduce_slabs(const float *slab, int nw, float scale,
+// grad[i] = scale * sum_w slab[w][i] in a fixed order: wave v of a block sums
+// slabs v, v + 8, v + 16, ... for 64 float4 columns, then the 8 partials are
+// added in wave order.  (One thread per column walking all 256 slabs kept
+// only 28 CUs busy on a chain of dependent loads: 72 us.)
+__global__ void __launch_bounds__(512) k_reduce_slabs(const float *slab, int nw, float scale,
                                                       float *grad) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= L::P / 4) return;
-    float4 acc = reinterpret_cast<const float4 *>(slab)[i];
-    for (int k = 1; k < nw; k++) {
-        const float4 v = reinterpret_cast<const float4 *>(slab + (size_t)k * L::P)[i];
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    __shared__ float4 part[8][64];
+    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int c = blockIdx.x * 64 + l;  // float4 column
+    constexpr int NC = L::P / 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < NC) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(slab);
+#pragma unroll 4
+        for (int k = wv; k < nw; k += 8) {
+            const float4 v = s4[(size_t)k * NC + c];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
     }
-    acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
-    reinterpret_cast<float4 *>(grad)[i] = acc;
+    part[wv][l] = acc;
+    __syncthreads();
+    if (wv == 0 && c < NC) {
+        float4 t = part[0][l];
+#pragma unroll
+        for (int q = 1; q < 8; q++) {
+            const float4 v = part[q][l];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        t.x *= scale; t.y *= scale; t.z *= scale; t.w *= scale;
+        reinterpret_cast<float4 *>(grad)[c] = t;
+    }
 }
 
 }  // namespace f16k
@@ -211,7 +230,7 @@ extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, i
                            slab);
         DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
     }
-    hipLaunchKernelGGL(f16k::k_reduce_slabs, dim3((f16k::L::P / 4 + 255) / 256), dim3(256), 0, s,
+    hipLaunchKernelGGL(f16k::k_reduce_slabs, dim3((f16k::L::P / 4 + 63) / 64), dim3(512), 0, s,
                        slab, n_slabs, scale, grad);
     DMDQN_LAUNCH_CHECK("k_reduce_slabs");
     return DMDQN_OK;

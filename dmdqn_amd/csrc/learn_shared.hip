@@ -214,41 +214,93 @@ __device__ __forceinline__ void dense_out(f32x4 c, const h16 *bias, int t, half8
 
 // Forward of one tile through a net: hb1 / hb2 = the layer-1 / layer-2
 // activations as next-layer operands (permuted K order); returns Q on the
-// lanes g = 0 (Q[row i][0..3]; other lanes hold zeros).
+// lanes g = 0 (Q[row i][0..3]; other lanes hold zeros).  DB: each output
+// tile's weight fragments are read from LDS one tile ahead (double-buffered,
+// order pinned by scheduling barriers: the LDS latency hides behind the
+// previous tile's MFMAs without the scheduler hoisting every read at once);
+// !DB reads them with the tile (28 fewer VGPRs: the gradient pass, whose
+// accumulators live across the whole launch, would spill).
+template <bool DB>
 __device__ __forceinline__ f32x4 fwd_tile(const Net &N, const half8 bx[3], half8 hb1[4],
                                           half8 hb2[4]) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    {
+        half8 cur[3], nxt[3];
+        if (DB)
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
+            for (int s = 0; s < 3; s++) cur[s] = N.w1[s * 64 + l];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (!DB)
+#pragma unroll
+                for (int s = 0; s < 3; s++) cur[s] = N.w1[(t * 3 + s) * 64 + l];
+            if (DB && t < 7)
+#pragma unroll
+                for (int s = 0; s < 3; s++) nxt[s] = N.w1[((t + 1) * 3 + s) * 64 + l];
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 3; s++) c = mfma(cur[s], bx[s], c);
+            dense_out(c, N.b1, t, hb1);
+            if (DB)
+#pragma unroll
+                for (int s = 0; s < 3; s++) cur[s] = nxt[s];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    {
+        half8 cur[4], nxt[4];
+        if (DB)
+#pragma unroll
+            for (int s = 0; s < 4; s++) cur[s] = N.w2[s * 64 + l];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (!DB)
+#pragma unroll
+                for (int s = 0; s < 4; s++) cur[s] = N.w2[(t * 4 + s) * 64 + l];
+            if (DB && t < 7)
+#pragma unroll
+                for (int s = 0; s < 4; s++) nxt[s] = N.w2[((t + 1) * 4 + s) * 64 + l];
+            else if (DB)
+#pragma unroll
+                for (int s = 0; s < 4; s++) nxt[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; s++) c = mfma(cur[s], hb1[s], c);
+            dense_out(c, N.b2, t, hb2);
+            if (DB)
+#pragma unroll
+                for (int s = 0; s < 4; s++) cur[s] = nxt[s];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (!DB)
+#pragma unroll
+            for (int s = 0; s < 4; s++) cur[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
         f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 3; s++) c = mfma(N.w1[(t * 3 + s) * 64 + l], bx[s], c);
-        dense_out(c, N.b1, t, hb1);
-        __builtin_amdgcn_sched_barrier(0);  // bound the scheduler's LDS-read hoisting
+        for (int s = 0; s < 4; s++) c = mfma(cur[s], hb2[s], c);  // layer 3 (cur = W3 fragments)
+        f32x4 q;
+#pragma unroll
+        for (int e = 0; e < 4; e++) q[e] = g == 0 ? r16(r16(c[e]) + (float)N.b3[e]) : 0.0f;
+        return q;
     }
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; s++) c = mfma(N.w2[(t * 4 + s) * 64 + l], hb1[s], c);
-        dense_out(c, N.b2, t, hb2);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; s++) c = mfma(i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8(), hb2[s], c);
-    f32x4 q;
-#pragma unroll
-    for (int e = 0; e < 4; e++) q[e] = g == 0 ? r16(r16(c[e]) + (float)N.b3[e]) : 0.0f;
-    return q;
 }
 
 // ---------------------------------------------------------------- pass 1: S'
-// LDS: both nets (2 x 58,896 B) + per-wave reward scratch (8 x 1 KB).
-constexpr int NEXT_LDS = 2 * NET_BYTES + 8 * B_ * 8;
+// LDS: both nets (2 x 58,896 B) + per wave: rewards f64 [128], ring slots
+// [128], transition word (a | done << 8) [128].
+constexpr int NEXT_WAVE_BYTES = B_ * 8 + B_ * 4 + B_ * 4;
+constexpr int NEXT_LDS = 2 * NET_BYTES + 8 * NEXT_WAVE_BYTES;
 static_assert(NEXT_LDS <= 160 * 1024, "k_shared_next LDS");
 
-// One wave per agent at a time (8 agents in flight per workgroup).
+__device__ __forceinline__ int ring_slot(const dmdqn_learn_args &a, int pos) {
+    int s = a.start + pos;
+    return s >= a.cap ? s - a.cap : s;
+}
+
+// One wave per agent at a time (8 agents in flight per workgroup).  HBM
+// reads run ahead: the next agent's deque positions while this agent runs,
+// this agent's row metadata (a, done, r) in one burst at its start, and each
+// tile's X(S') one tile ahead.
 __global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, float *y_out,
                                                         uint8_t *act_out) {
     __shared__ __attribute__((aligned(16))) char smem[NEXT_LDS];
@@ -257,20 +309,42 @@ __global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, floa
     __syncthreads();
     const Net on = net_at(smem), tg = net_at(smem + NET_BYTES);
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    double *r64 = reinterpret_cast<double *>(smem + 2 * NET_BYTES) + w * B_;
-    for (int agent = blockIdx.x * 8 + w; agent < a.NA; agent += gridDim.x * 8) {
-        const size_t arow = (size_t)agent * a.cap;
-        // rewards of the batch (f64 in the s' rows) -> z-score in numpy's
-        // pairwise order (learn_h16.hpp zscore): 8 partial sums of 16
-        for (int b = l; b < B_; b += 64) {
-            int s = a.start + a.idx[(size_t)agent * B_ + b];
-            if (s >= a.cap) s -= a.cap;
-            const uint2 rb = *reinterpret_cast<const uint2 *>(a.ring_n + (arow + s) * DMDQN_ROW_BYTES +
-                                                              DMDQN_ROW_R);
-            r64[b] = __longlong_as_double((long long)(((unsigned long long)rb.y << 32) | rb.x));
+    char *wsc = smem + 2 * NET_BYTES + w * NEXT_WAVE_BYTES;
+    double *r64 = reinterpret_cast<double *>(wsc);
+    int *slots = reinterpret_cast<int *>(wsc + B_ * 8);
+    uint32_t *tw = reinterpret_cast<uint32_t *>(wsc + B_ * 12);
+    const int stride = gridDim.x * 8;
+    int agent = blockIdx.x * 8 + w;
+    // deque positions of rows l and l + 64 (metadata) and i (tile 0's X)
+    int p0 = 0, p1 = 0, pt = 0;
+    if (agent < a.NA) {
+        p0 = a.idx[(size_t)agent * B_ + l];
+        p1 = a.idx[(size_t)agent * B_ + l + 64];
+        pt = a.idx[(size_t)agent * B_ + i];
+    }
+    for (; agent < a.NA; agent += stride) {
+        const int8_t *base = a.ring_n + (size_t)agent * a.cap * DMDQN_ROW_BYTES;
+        const int s0 = ring_slot(a, p0), s1 = ring_slot(a, p1), st = ring_slot(a, pt);
+        const uint4 m0 = *reinterpret_cast<const uint4 *>(base + (size_t)s0 * DMDQN_ROW_BYTES + DMDQN_ROW_A);
+        const uint4 m1 = *reinterpret_cast<const uint4 *>(base + (size_t)s1 * DMDQN_ROW_BYTES + DMDQN_ROW_A);
+        XTile xt;
+        x_issue(base + (size_t)st * DMDQN_ROW_BYTES, xt);
+        const int nxt = agent + stride;
+        if (nxt < a.NA) {
+            p0 = a.idx[(size_t)nxt * B_ + l];
+            p1 = a.idx[(size_t)nxt * B_ + l + 64];
+            pt = a.idx[(size_t)nxt * B_ + i];
         }
-        __builtin_amdgcn_s_waitcnt(0);
+        slots[l] = s0;
+        slots[l + 64] = s1;
+        tw[l] = m0.x;
+        tw[l + 64] = m1.x;
+        r64[l] = __longlong_as_double((long long)(((unsigned long long)m0.w << 32) | m0.z));
+        r64[l + 64] = __longlong_as_double((long long)(((unsigned long long)m1.w << 32) | m1.z));
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
+        // z-score of the batch rewards in numpy's pairwise order (learn_h16.hpp
+        // zscore): 8 partial sums of 16
         double part = 0.0;
         if (l < 8) {
             part = r64[l];
@@ -304,16 +378,12 @@ __global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, floa
 #pragma unroll 1
         for (int rt = 0; rt < B_ / 16; rt++) {
             const int b = 16 * rt + i;
-            int s = a.start + a.idx[(size_t)agent * B_ + b];
-            if (s >= a.cap) s -= a.cap;
-            const int8_t *row = a.ring_n + (arow + s) * DMDQN_ROW_BYTES;
-            XTile xt;
-            x_issue(row, xt);
-            const uint32_t meta = *reinterpret_cast<const uint32_t *>(row + DMDQN_ROW_A);
             half8 bx[3], hb1[4], hb2[4];
             x_frags(xt, bx);
-            const f32x4 qt = fwd_tile(tg, bx, hb1, hb2);
-            const f32x4 qo = fwd_tile(on, bx, hb1, hb2);
+            if (rt + 1 < B_ / 16)  // the next tile's rows, in flight behind this tile
+                x_issue(base + (size_t)slots[b + 16] * DMDQN_ROW_BYTES, xt);
+            const f32x4 qt = fwd_tile<true>(tg, bx, hb1, hb2);
+            const f32x4 qo = fwd_tile<true>(on, bx, hb1, hb2);
             if (g == 0) {
                 // Double-DQN target (dqn_agent.py:342-347, first max on ties),
                 // each op rounded on its own as TF's
@@ -323,14 +393,16 @@ __global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, floa
                 if (qo[2] > bq) { best = 2; bq = qo[2]; }
                 if (qo[3] > bq) { best = 3; }
                 const float tq = best == 0 ? qt[0] : best == 1 ? qt[1] : best == 2 ? qt[2] : qt[3];
+                const uint32_t m = tw[b];
                 const float rn = (float)__ddiv_rn(__dsub_rn(r64[b], mean), sd);
-                const float dn = ((meta >> 8) & 0xffu) ? 1.0f : 0.0f;
+                const float dn = ((m >> 8) & 0xffu) ? 1.0f : 0.0f;
                 const float gd = __fmul_rn(a.gamma, __fsub_rn(1.0f, dn));
                 y_out[(size_t)agent * B_ + b] = __fadd_rn(rn, __fmul_rn(gd, tq));
-                act_out[(size_t)agent * B_ + b] = (uint8_t)(meta & 0xffu);
+                act_out[(size_t)agent * B_ + b] = (uint8_t)(m & 0xffu);
                 if (a.rn_out) a.rn_out[(size_t)agent * B_ + b] = rn;
             }
         }
+        __builtin_amdgcn_wave_barrier();  // every lane is done with this agent's scratch
     }
 }
 
@@ -366,15 +438,22 @@ struct Pref {  // one row per lane i: the next agent's inputs, in flight
     uint32_t act;
 };
 
+// The row this lane feeds in the row phases (16w + i) of `agent`, whose deque
+// position pos was loaded one agent earlier.
 __device__ __forceinline__ void pref_issue(const dmdqn_learn_args &a, const float *y_in,
-                                           const uint8_t *act_in, int agent, Pref &p) {
+                                           const uint8_t *act_in, int agent, int pos, Pref &p) {
     const int w = threadIdx.x >> 6, i = threadIdx.x & 15;
     const int b = 16 * w + i;
-    int s = a.start + a.idx[(size_t)agent * B_ + b];
+    int s = a.start + pos;
     if (s >= a.cap) s -= a.cap;
     x_issue(a.ring_s + ((size_t)agent * a.cap + s) * DMDQN_ROW_BYTES, p.x);
     p.y = y_in[(size_t)agent * B_ + b];
     p.act = act_in[(size_t)agent * B_ + b];
+}
+
+__device__ __forceinline__ int pos_of(const dmdqn_learn_args &a, int agent) {
+    return agent < a.NA ? a.idx[(size_t)agent * B_ + 16 * (threadIdx.x >> 6) + (threadIdx.x & 15)]
+                        : 0;
 }
 
 template <bool QSTATS>
@@ -406,7 +485,8 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
     // DQ image columns 4..15 stay zero
     for (int k = threadIdx.x; k < B_ * 16; k += 512) DQI[k] = (h16)0.0f;
     Pref pf;
-    if ((int)blockIdx.x < a.NA) pref_issue(a, y_in, act_in, blockIdx.x, pf);
+    if ((int)blockIdx.x < a.NA) pref_issue(a, y_in, act_in, blockIdx.x, pos_of(a, blockIdx.x), pf);
+    int npos = pos_of(a, blockIdx.x + gridDim.x);  // the next agent's deque position, in flight
     __syncthreads();
 
     for (int agent = blockIdx.x; agent < a.NA; agent += gridDim.x) {
@@ -415,7 +495,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
         x_frags(pf.x, bx);
         const float yv = pf.y;
         const int av = (int)pf.act;
-        const f32x4 q = fwd_tile(on, bx, hb1, hb2);
+        const f32x4 q = fwd_tile<false>(on, bx, hb1, hb2);
         float term = 0.0f, dq = 0.0f;
         if (g == 0) {
             const float qa = av == 0 ? q[0] : av == 1 ? q[1] : av == 2 ? q[2] : q[3];
@@ -497,7 +577,8 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
         }
         // next agent's indices and rows in flight behind the reductions
         const int nxt = agent + gridDim.x;
-        if (nxt < a.NA) pref_issue(a, y_in, act_in, nxt, pf);
+        if (nxt < a.NA) pref_issue(a, y_in, act_in, nxt, npos, pf);
+        npos = pos_of(a, nxt + gridDim.x);
         // ---- W1: wave w owns fan-out neurons 16w..16w+15 of layers 2 and 3
         // dW3 (k-tile w) and db3 from H2 (before its slice turns into dZ2)
 #pragma unroll

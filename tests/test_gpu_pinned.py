@@ -167,9 +167,10 @@ def test_dropin_h16_matches_reference_mixed_per_learn(tag):
     wrapped) and 333; huber_f16 / mse_bf16 learns 1-16 and 203.
     Stated tolerances:
       * actions bit-exact (numpy stream);
-      * loss rtol 2e-3; 1e-2 where the batch holds a Double-DQN near-tie (two
+      * loss rtol 2e-4; 2e-3 where the batch holds a Double-DQN near-tie (two
         16-bit online Q(S') of a row within one ulp: the argmax may then take
-        the other action under another f32 summation order);
+        the other action under another f32 summation order) -- measured
+        3.0e-5 / 3.4e-4 (mse_f16), 6.4e-6 (huber_f16), 1.2e-7 (mse_bf16);
       * the gradient Adam received (from m'): >= 99 % of the entries within one
         16-bit ulp + 1e-3 of the largest entry of the reference's;
       * Adam bit-exact given the same gradient: >= 50 % of m' and w' entries
@@ -186,7 +187,7 @@ def test_dropin_h16_matches_reference_mixed_per_learn(tag):
           f"{min(r['m_eq'] for r in recs):.4f}, w' equal min {min(r['w_eq'] for r in recs):.4f}, "
           f"|dw| max {max(r['dw'] for r in recs):.3g}")
     for r, e in zip(recs, rel):
-        assert e <= (1e-2 if r["fragile"] else 2e-3), (r["k"], e)
+        assert e <= (2e-3 if r["fragile"] else 2e-4), (r["k"], e)
         assert r["g_near"] >= 0.99, r
         assert r["m_eq"] >= 0.5 and r["w_eq"] >= 0.5 and r["dw"] <= 5e-3, r
 
@@ -453,7 +454,7 @@ def test_replicas_restart_on_their_own_done():
     observation the next act sees (the restart state after a done), the
     per-replica done flags stored with the transitions and the replay indices
     are bit-exact; each replica runs several episodes of its own length."""
-    E, steps = 3, 70
+    E, steps = 3, 130
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=E, seed=9, end_ms=60_000),
                  AgentConfig(replay_buffer_size=500))
     assert tr.env.drains_early
