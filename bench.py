@@ -375,7 +375,7 @@ def main():
                              "full": "act/sim/observe/sample of step t+1 beside learn t"}[args.overlap],
             },
             "roofline": {
-                "kernel": ("k_learn_shared_f16 + k_reduce_slabs + k_adam" if args.shared else
+                "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared else
                            "k_learn (fused gather + 3x fwd + bwd + Adam, MFMA)"),
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -398,7 +398,7 @@ def main():
                                           sim_traffic, sim_src,
                                           sim_state_fits_lds(args.rows, args.cols)),
             "mfma": {
-                "kernel": ("k_learn_shared_f16" if args.shared else LEARN_KERNELS[args.precision]) +
+                "kernel": ("k_shared_next + k_shared_grad" if args.shared else LEARN_KERNELS[args.precision]) +
                           f" (Q-net forward/backward, {MFMA_OPS[args.precision]})",
                 "flop_per_launch": NA * LEARN_FLOP_PER_AGENT,
                 "achieved": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12, 2),

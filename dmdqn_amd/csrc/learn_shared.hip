@@ -70,11 +70,25 @@ __device__ __forceinline__ int hoff(int r, int c) {
            8 * ((ch & 3) ^ (((r >> 1) & 1) | ((r >> 2) & 2))) + (c & 7);
 }
 
-// img[r0 + 8(l>>4) + e][c0 + (l&15)], e = 0..7 (two ds_read_b64_tr_b16).
+// hoff(r, c) = hoff(r & 15, c & 31) + 16 LD (r >> 4) + 256 (c >> 5) (the XOR
+// takes row bits 1 and 3): the callers pass that split (rlo = r & 15, clo =
+// c & 31, rblk = r >> 4, cblk = c >> 5) so each lane keeps one base per
+// distinct (rlo, clo) and every block offset that is a compile-time constant
+// folds into the LDS instruction's immediate (computing hoff whole left dozens
+// of loop-invariant addresses in VGPRs).  tests/test_layout_cpu.py checks the
+// identity for every call site's index pattern.
+template <int LD = H>
+__device__ __forceinline__ int hsplit(int rlo, int clo, int rblk, int cblk) {
+    return hoff<LD>(rlo, clo) + 16 * LD * rblk + 256 * cblk;
+}
+
+// img[r0 + 8(l>>4) + e][c0 + (l&15)], e = 0..7 (two ds_read_b64_tr_b16);
+// r0 % 32 == 0, c0 % 16 == 0.
 template <int LD = H>
 __device__ __forceinline__ half8 frag_tr_h(const h16 *img, int r0, int c0) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    const h16 *p0 = img + hoff<LD>(r0 + 8 * g + (i >> 2), c0 + 4 * (i & 3));
+    const h16 *p0 = img + hsplit<LD>(8 * (g & 1) + (i >> 2), (c0 & 16) + 4 * (i & 3), g >> 1, 0) +
+                    (16 * LD * (r0 >> 4) + 256 * (c0 >> 5));
     v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)p0);
     v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(p0 + 128));
     half8 r;
@@ -179,6 +193,15 @@ __device__ void stage_bwd(const h16 *WH, half8 *w2b, h16 *w3r) {
     for (int k = threadIdx.x; k < NACT * H; k += nt) w3r[k] = WH[L::oW3T + k];
 }
 
+// Diagnostics (tools/stamp_shared.py): when a stamps buffer is passed, lane 0
+// of the wave (next) / thread 0 of the workgroup (grad) writes the phase ends
+// of each agent it handles, s_memrealtime (100 MHz), into stamps[agent][k].
+#define SH_STAMP(agent, k, who)                                                       \
+    do {                                                                              \
+        if (a.stamps && (who) == 0)                                                   \
+            a.stamps[(size_t)(agent) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
 // ---------------------------------------------------------------- one 16-row tile
 // X(S) / X(S') B-operands of a 16-row tile: lane (i, g) holds features
 // 32s + 8g .. +7 of row i (int8 replay row -> f16, exact).
@@ -212,7 +235,93 @@ __device__ __forceinline__ void dense_out(f32x4 c, const h16 *bias, int t, half8
     for (int e = 0; e < 4; e++) ops[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
 }
 
-// Forward of one tile through a net: hb1 / hb2 = the layer-1 / layer-2
+// Forward of NT 16-row tiles through a net, every weight fragment read once
+// from LDS and used for the NT tiles: hb1 / hb2 = the layer-1 / layer-2
+// activations as next-layer operands (permuted K order); q = Q on the lanes
+// g = 0 (Q[row i][0..3]; other lanes hold zeros).  DB: each output tile's
+// weight fragments are read from LDS one tile ahead (double-buffered, order
+// pinned by scheduling barriers: the LDS latency hides behind the previous
+// tile's MFMAs without the scheduler hoisting every read at once); !DB reads
+// them with the tile (28 fewer VGPRs: the gradient pass, whose accumulators
+// live across the whole launch, would spill).
+template <int NT, bool DB>
+__device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3], half8 (&hb1)[NT][4],
+                                          half8 (&hb2)[NT][4], f32x4 (&q)[NT]) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    {
+        half8 cur[3], nxt[3];
+        if (DB)
+#pragma unroll
+            for (int s = 0; s < 3; s++) cur[s] = N.w1[s * 64 + l];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (!DB)
+#pragma unroll
+                for (int s = 0; s < 3; s++) cur[s] = N.w1[(t * 3 + s) * 64 + l];
+            if (DB && t < 7)
+#pragma unroll
+                for (int s = 0; s < 3; s++) nxt[s] = N.w1[((t + 1) * 3 + s) * 64 + l];
+            f32x4 c[NT];
+#pragma unroll
+            for (int n = 0; n < NT; n++) c[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 3; s++)
+#pragma unroll
+                for (int n = 0; n < NT; n++) c[n] = mfma(cur[s], bx[n][s], c[n]);
+#pragma unroll
+            for (int n = 0; n < NT; n++) dense_out(c[n], N.b1, t, hb1[n]);
+            if (DB)
+#pragma unroll
+                for (int s = 0; s < 3; s++) cur[s] = nxt[s];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    half8 cur[4], nxt[4];
+    if (DB)
+#pragma unroll
+        for (int s = 0; s < 4; s++) cur[s] = N.w2[s * 64 + l];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        if (!DB)
+#pragma unroll
+            for (int s = 0; s < 4; s++) cur[s] = N.w2[(t * 4 + s) * 64 + l];
+        if (DB && t < 7)
+#pragma unroll
+            for (int s = 0; s < 4; s++) nxt[s] = N.w2[((t + 1) * 4 + s) * 64 + l];
+        else if (DB)
+#pragma unroll
+            for (int s = 0; s < 4; s++) nxt[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
+        f32x4 c[NT];
+#pragma unroll
+        for (int n = 0; n < NT; n++) c[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int n = 0; n < NT; n++) c[n] = mfma(cur[s], hb1[n][s], c[n]);
+#pragma unroll
+        for (int n = 0; n < NT; n++) dense_out(c[n], N.b2, t, hb2[n]);
+        if (DB)
+#pragma unroll
+            for (int s = 0; s < 4; s++) cur[s] = nxt[s];
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!DB)
+#pragma unroll
+        for (int s = 0; s < 4; s++) cur[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
+    f32x4 c[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) c[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; s++)  // layer 3 (cur = W3 fragments)
+#pragma unroll
+        for (int n = 0; n < NT; n++) c[n] = mfma(cur[s], hb2[n][s], c[n]);
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) q[n][e] = g == 0 ? r16(r16(c[n][e]) + (float)N.b3[e]) : 0.0f;
+}
+
+// One tile, fragments read with (!DB) or one tile ahead of (DB) the tile: hb1 / hb2 = the layer-1 / layer-2
 // activations as next-layer operands (permuted K order); returns Q on the
 // lanes g = 0 (Q[row i][0..3]; other lanes hold zeros).  DB: each output
 // tile's weight fragments are read from LDS one tile ahead (double-buffered,
@@ -285,9 +394,77 @@ __device__ __forceinline__ f32x4 fwd_tile(const Net &N, const half8 bx[3], half8
     }
 }
 
+// One tile, software-pipelined without a second fragment buffer (the
+// gradient pass: its accumulators live across the whole launch): an output
+// tile's MFMAs issue, then the NEXT tile's weight fragments and bias are read
+// into the registers the MFMAs just consumed, then this tile's bias + relu --
+// the LDS latency hides behind the MFMA drain and the VALU epilogue.  The
+// scheduling barriers pin that order.  Same result as fwd_tiles<1, *>.
+__device__ __forceinline__ f32x4 fwd_tile_pipe(const Net &N, const half8 bx[3], half8 hb1[4],
+                                               half8 hb2[4]) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    half8 w[4];
+    half4v bias = *reinterpret_cast<const half4v *>(N.b1 + 4 * g);
+#pragma unroll
+    for (int s = 0; s < 3; s++) w[s] = N.w1[s * 64 + l];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 3; s++) c = mfma(w[s], bx[s], c);
+        __builtin_amdgcn_sched_barrier(0);
+        const half4v bt = bias;
+        if (t < 7) {
+#pragma unroll
+            for (int s = 0; s < 3; s++) w[s] = N.w1[((t + 1) * 3 + s) * 64 + l];
+            bias = *reinterpret_cast<const half4v *>(N.b1 + 16 * (t + 1) + 4 * g);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; s++) w[s] = N.w2[s * 64 + l];
+            bias = *reinterpret_cast<const half4v *>(N.b2 + 4 * g);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const half4v z = __builtin_convertvector(c, half4v) + bt;
+#pragma unroll
+        for (int e = 0; e < 4; e++) hb1[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; s++) c = mfma(w[s], hb1[s], c);
+        __builtin_amdgcn_sched_barrier(0);
+        const half4v bt = bias;
+        if (t < 7) {
+#pragma unroll
+            for (int s = 0; s < 4; s++) w[s] = N.w2[((t + 1) * 4 + s) * 64 + l];
+            bias = *reinterpret_cast<const half4v *>(N.b2 + 16 * (t + 1) + 4 * g);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; s++) w[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const half4v z = __builtin_convertvector(c, half4v) + bt;
+#pragma unroll
+        for (int e = 0; e < 4; e++) hb2[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; s++) c = mfma(w[s], hb2[s], c);  // layer 3 (w = W3 fragments)
+    f32x4 q;
+#pragma unroll
+    for (int e = 0; e < 4; e++) q[e] = g == 0 ? r16(r16(c[e]) + (float)N.b3[e]) : 0.0f;
+    return q;
+}
+
 // ---------------------------------------------------------------- pass 1: S'
 // LDS: both nets (2 x 58,896 B) + per wave: rewards f64 [128], ring slots
 // [128], transition word (a | done << 8) [128].
+#ifndef NEXT_NT
+#define NEXT_NT 2  // 16-row tiles per weight read in k_shared_next
+#endif
 constexpr int NEXT_WAVE_BYTES = B_ * 8 + B_ * 4 + B_ * 4;
 constexpr int NEXT_LDS = 2 * NET_BYTES + 8 * NEXT_WAVE_BYTES;
 static_assert(NEXT_LDS <= 160 * 1024, "k_shared_next LDS");
@@ -315,25 +492,34 @@ __global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, floa
     uint32_t *tw = reinterpret_cast<uint32_t *>(wsc + B_ * 12);
     const int stride = gridDim.x * 8;
     int agent = blockIdx.x * 8 + w;
-    // deque positions of rows l and l + 64 (metadata) and i (tile 0's X)
-    int p0 = 0, p1 = 0, pt = 0;
+    constexpr int RT = 16 * NEXT_NT;
+    // deque positions of rows l and l + 64 (metadata) and 16n + i (the first
+    // tiles' X)
+    int p0 = 0, p1 = 0, pt[NEXT_NT];
+#pragma unroll
+    for (int n = 0; n < NEXT_NT; n++) pt[n] = 0;
     if (agent < a.NA) {
         p0 = a.idx[(size_t)agent * B_ + l];
         p1 = a.idx[(size_t)agent * B_ + l + 64];
-        pt = a.idx[(size_t)agent * B_ + i];
+#pragma unroll
+        for (int n = 0; n < NEXT_NT; n++) pt[n] = a.idx[(size_t)agent * B_ + 16 * n + i];
     }
     for (; agent < a.NA; agent += stride) {
+        SH_STAMP(agent, 10, l);
         const int8_t *base = a.ring_n + (size_t)agent * a.cap * DMDQN_ROW_BYTES;
-        const int s0 = ring_slot(a, p0), s1 = ring_slot(a, p1), st = ring_slot(a, pt);
+        const int s0 = ring_slot(a, p0), s1 = ring_slot(a, p1);
         const uint4 m0 = *reinterpret_cast<const uint4 *>(base + (size_t)s0 * DMDQN_ROW_BYTES + DMDQN_ROW_A);
         const uint4 m1 = *reinterpret_cast<const uint4 *>(base + (size_t)s1 * DMDQN_ROW_BYTES + DMDQN_ROW_A);
-        XTile xt;
-        x_issue(base + (size_t)st * DMDQN_ROW_BYTES, xt);
+        XTile xt[NEXT_NT];
+#pragma unroll
+        for (int n = 0; n < NEXT_NT; n++)
+            x_issue(base + (size_t)ring_slot(a, pt[n]) * DMDQN_ROW_BYTES, xt[n]);
         const int nxt = agent + stride;
         if (nxt < a.NA) {
             p0 = a.idx[(size_t)nxt * B_ + l];
             p1 = a.idx[(size_t)nxt * B_ + l + 64];
-            pt = a.idx[(size_t)nxt * B_ + i];
+#pragma unroll
+            for (int n = 0; n < NEXT_NT; n++) pt[n] = a.idx[(size_t)nxt * B_ + 16 * n + i];
         }
         slots[l] = s0;
         slots[l + 64] = s1;
@@ -375,34 +561,43 @@ __global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, floa
                                                                     __dadd_rn(p[6], p[7])))),
                                  128.0)),
             1e-8);
+        SH_STAMP(agent, 11, l);
 #pragma unroll 1
-        for (int rt = 0; rt < B_ / 16; rt++) {
-            const int b = 16 * rt + i;
-            half8 bx[3], hb1[4], hb2[4];
-            x_frags(xt, bx);
-            if (rt + 1 < B_ / 16)  // the next tile's rows, in flight behind this tile
-                x_issue(base + (size_t)slots[b + 16] * DMDQN_ROW_BYTES, xt);
-            const f32x4 qt = fwd_tile<true>(tg, bx, hb1, hb2);
-            const f32x4 qo = fwd_tile<true>(on, bx, hb1, hb2);
+        for (int rp = 0; rp < B_ / RT; rp++) {  // RT rows: NEXT_NT tiles share every weight read
+            half8 bx[NEXT_NT][3], hb1[NEXT_NT][4], hb2[NEXT_NT][4];
+#pragma unroll
+            for (int n = 0; n < NEXT_NT; n++) x_frags(xt[n], bx[n]);
+            if (rp + 1 < B_ / RT)  // the next rows, in flight behind these tiles
+#pragma unroll
+                for (int n = 0; n < NEXT_NT; n++)
+                    x_issue(base + (size_t)slots[RT * (rp + 1) + 16 * n + i] * DMDQN_ROW_BYTES, xt[n]);
+            f32x4 qt[NEXT_NT], qo[NEXT_NT];
+            fwd_tiles<NEXT_NT, true>(tg, bx, hb1, hb2, qt);
+            fwd_tiles<NEXT_NT, true>(on, bx, hb1, hb2, qo);
             if (g == 0) {
-                // Double-DQN target (dqn_agent.py:342-347, first max on ties),
-                // each op rounded on its own as TF's
-                int best = 0;
-                float bq = qo[0];
-                if (qo[1] > bq) { best = 1; bq = qo[1]; }
-                if (qo[2] > bq) { best = 2; bq = qo[2]; }
-                if (qo[3] > bq) { best = 3; }
-                const float tq = best == 0 ? qt[0] : best == 1 ? qt[1] : best == 2 ? qt[2] : qt[3];
-                const uint32_t m = tw[b];
-                const float rn = (float)__ddiv_rn(__dsub_rn(r64[b], mean), sd);
-                const float dn = ((m >> 8) & 0xffu) ? 1.0f : 0.0f;
-                const float gd = __fmul_rn(a.gamma, __fsub_rn(1.0f, dn));
-                y_out[(size_t)agent * B_ + b] = __fadd_rn(rn, __fmul_rn(gd, tq));
-                act_out[(size_t)agent * B_ + b] = (uint8_t)(m & 0xffu);
-                if (a.rn_out) a.rn_out[(size_t)agent * B_ + b] = rn;
+#pragma unroll
+                for (int n = 0; n < NEXT_NT; n++) {
+                    const int b = RT * rp + 16 * n + i;
+                    // Double-DQN target (dqn_agent.py:342-347, first max on
+                    // ties), each op rounded on its own as TF's
+                    int best = 0;
+                    float bq = qo[n][0];
+                    if (qo[n][1] > bq) { best = 1; bq = qo[n][1]; }
+                    if (qo[n][2] > bq) { best = 2; bq = qo[n][2]; }
+                    if (qo[n][3] > bq) { best = 3; }
+                    const float tq = best == 0 ? qt[n][0] : best == 1 ? qt[n][1] : best == 2 ? qt[n][2] : qt[n][3];
+                    const uint32_t m = tw[b];
+                    const float rn = (float)__ddiv_rn(__dsub_rn(r64[b], mean), sd);
+                    const float dn = ((m >> 8) & 0xffu) ? 1.0f : 0.0f;
+                    const float gd = __fmul_rn(a.gamma, __fsub_rn(1.0f, dn));
+                    y_out[(size_t)agent * B_ + b] = __fadd_rn(rn, __fmul_rn(gd, tq));
+                    act_out[(size_t)agent * B_ + b] = (uint8_t)(m & 0xffu);
+                    if (a.rn_out) a.rn_out[(size_t)agent * B_ + b] = rn;
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();  // every lane is done with this agent's scratch
+        SH_STAMP(agent, 12, l);
     }
 }
 
@@ -456,6 +651,18 @@ __device__ __forceinline__ int pos_of(const dmdqn_learn_args &a, int agent) {
                         : 0;
 }
 
+// Tuning switches (tools/build_exp.py + tools/stamp_shared.py, same box, all
+// bit-identical): SH_PIPE_FWD = the forward of fwd_tile_pipe (R.fwd 2.5 ->
+// 2.0 us per agent, but 9 more spilled VGPRs slow W1 by more); SH_PIPE_BWD =
+// the dH1 / dW2 / dW1 fragment reads one step ahead and the dZ2 conversion's
+// reads batched (10.4 -> 9.8 us per agent).
+#ifndef SH_PIPE_FWD
+#define SH_PIPE_FWD 0
+#endif
+#ifndef SH_PIPE_BWD
+#define SH_PIPE_BWD 1
+#endif
+
 template <bool QSTATS>
 __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, const float *y_in,
                                                         const uint8_t *act_in, float *slab) {
@@ -490,12 +697,18 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
     __syncthreads();
 
     for (int agent = blockIdx.x; agent < a.NA; agent += gridDim.x) {
+        SH_STAMP(agent, 0, threadIdx.x);
         // ---- R: rows 16w..16w+15 -- forward, dL/dQ, dZ2, dH1 -> dZ1 in registers
         half8 bx[3], hb1[4], hb2[4];
         x_frags(pf.x, bx);
         const float yv = pf.y;
         const int av = (int)pf.act;
+#if SH_PIPE_FWD
+        const f32x4 q = fwd_tile_pipe(on, bx, hb1, hb2);
+#else
         const f32x4 q = fwd_tile<false>(on, bx, hb1, hb2);
+#endif
+        SH_STAMP(agent, 13, threadIdx.x);
         float term = 0.0f, dq = 0.0f;
         if (g == 0) {
             const float qa = av == 0 ? q[0] : av == 1 ? q[1] : av == 2 ? q[2] : q[3];
@@ -518,11 +731,17 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
                 v1[e] = hb1[t >> 1][4 * (t & 1) + e];
                 v2[e] = hb2[t >> 1][4 * (t & 1) + e];
             }
-            *reinterpret_cast<half4v *>(I1 + hoff(row, 16 * t + 4 * g)) = v1;
-            *reinterpret_cast<half4v *>(I2 + hoff(row, 16 * t + 4 * g)) = v2;
+            const int o = hsplit(i, 16 * (t & 1) + 4 * g, w, 0) + 256 * (t >> 1);
+            *reinterpret_cast<half4v *>(I1 + o) = v1;  // [row][16t + 4g]
+            *reinterpret_cast<half4v *>(I2 + o) = v2;
         }
         // dZ2 = h16(dq W3[k][a]) where H2 > 0 (operand order of hb2)
         half8 dz2[4];
+#if SH_PIPE_BWD
+        half8 wb[4];  // dH1's first W2B tile, in flight behind the dZ2 epilogue
+#pragma unroll
+        for (int s = 0; s < 4; s++) wb[s] = w2b[s * 64 + l];
+#endif
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const half4v w3 = *reinterpret_cast<const half4v *>(w3r + av * H + 16 * t + 4 * g);
@@ -532,13 +751,26 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
                 dz2[t >> 1][4 * (t & 1) + e] = hv > (h16)0.0f ? (h16)(dq * (float)w3[e]) : (h16)0.0f;
             }
         }
+        SH_STAMP(agent, 14, threadIdx.x);
         // dH1^T = W2 dZ2^T -> dZ1 = h16(dH1) where H1 > 0 (operand order of hb1)
         half8 dz1[4];
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#if SH_PIPE_BWD
+            // MFMAs of tile t, then tile t + 1's fragments into the registers
+            // they consumed, then tile t's mask (fwd_tile_pipe's order)
+#pragma unroll
+            for (int s = 0; s < 4; s++) c = mfma(wb[s], dz2[s], c);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t < 7)
+#pragma unroll
+                for (int s = 0; s < 4; s++) wb[s] = w2b[((t + 1) * 4 + s) * 64 + l];
+            __builtin_amdgcn_sched_barrier(0);
+#else
 #pragma unroll
             for (int s = 0; s < 4; s++) c = mfma(w2b[(t * 4 + s) * 64 + l], dz2[s], c);
+#endif
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const h16 hv = hb1[t >> 1][4 * (t & 1) + e];
@@ -546,6 +778,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        SH_STAMP(agent, 15, threadIdx.x);
         // loss of the batch: per wave over its 16 rows, then 8 partials in order
         {
             float ls = term;
@@ -569,7 +802,9 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
                 atomicAdd(a.qstats + (size_t)agent * 6 + 2 + l, cnt);
             }
         }
+        SH_STAMP(agent, 1, threadIdx.x);
         __syncthreads();  // 1: H1, H2, DQ, dq / act of every row
+        SH_STAMP(agent, 2, threadIdx.x);
         if (threadIdx.x == 0 && a.loss) {
             float ls = 0.0f;
             for (int k = 0; k < 8; k++) ls += sloss[k];
@@ -588,6 +823,33 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
             GB3 = mfma(ones, dqf, GB3);
         }
         // this wave's H2 columns -> dZ2 in place (the values dz2 holds above)
+#if SH_PIPE_BWD
+        {  // every read of the four chunks first, then the stores (one LDS round trip)
+            half8 hv[4], w3[4];
+            float dqb[4];
+            int ab[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int b = (l >> 1) + 32 * j;  // [b][16w + 8(l & 1)]
+                hv[j] = *reinterpret_cast<const half8 *>(
+                    I2 + hsplit((l >> 1) & 15, 16 * (w & 1) + 8 * (l & 1), l >> 5, w >> 1) + 16 * H * 2 * j);
+                dqb[j] = sdq[b];
+                ab[j] = sact[b];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                w3[j] = *reinterpret_cast<const half8 *>(w3r + ab[j] * H + 16 * w + 8 * (l & 1));
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                half8 o;
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                    o[e] = hv[j][e] > (h16)0.0f ? (h16)(dqb[j] * (float)w3[j][e]) : (h16)0.0f;
+                *reinterpret_cast<half8 *>(
+                    I2 + hsplit((l >> 1) & 15, 16 * (w & 1) + 8 * (l & 1), l >> 5, w >> 1) + 16 * H * 2 * j) = o;
+            }
+        }
+#else
         for (int c = l; c < B_ * 2; c += 64) {
             const int b = c >> 1, k0 = 16 * w + 8 * (c & 1);
             half8 *p = reinterpret_cast<half8 *>(I2 + hoff(b, k0));
@@ -599,6 +861,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
             for (int e = 0; e < 8; e++) o[e] = hv[e] > (h16)0.0f ? (h16)(dqb * (float)w3[e]) : (h16)0.0f;
             *p = o;
         }
+#endif
         // dW2 (all fan-in tiles, fan-out slice w) and db2
         {
             half8 bq[4];
@@ -607,26 +870,76 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
                 bq[q4] = frag_tr_h(I2, 32 * q4, 16 * w);
                 GB2 = mfma(ones, bq[q4], GB2);
             }
+#if SH_PIPE_BWD
+            half8 af[4];  // fan-in tile t's H1 fragments, one tile ahead
+#pragma unroll
+            for (int q4 = 0; q4 < 4; q4++) af[q4] = frag_tr_h(I1, 32 * q4, 0);
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                half8 an[4];
+                if (t < 7)
+#pragma unroll
+                    for (int q4 = 0; q4 < 4; q4++) an[q4] = frag_tr_h(I1, 32 * q4, 16 * (t + 1));
+#pragma unroll
+                for (int q4 = 0; q4 < 4; q4++) G2[t] = mfma(af[q4], bq[q4], G2[t]);
+                if (t < 7)
+#pragma unroll
+                    for (int q4 = 0; q4 < 4; q4++) af[q4] = an[q4];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#else
 #pragma unroll
             for (int t = 0; t < 8; t++) {
 #pragma unroll
                 for (int q4 = 0; q4 < 4; q4++) G2[t] = mfma(frag_tr_h(I1, 32 * q4, 16 * t), bq[q4], G2[t]);
                 __builtin_amdgcn_sched_barrier(0);
             }
+#endif
         }
+        SH_STAMP(agent, 3, threadIdx.x);
         __syncthreads();  // 2: H1 and dZ2 consumed
+        SH_STAMP(agent, 4, threadIdx.x);
         // ---- R2: dZ1 -> I1, X(S) -> I2 (rows of this wave)
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             half4v v;
 #pragma unroll
             for (int e = 0; e < 4; e++) v[e] = dz1[t >> 1][4 * (t & 1) + e];
-            *reinterpret_cast<half4v *>(I1 + hoff(row, 16 * t + 4 * g)) = v;
+            *reinterpret_cast<half4v *>(
+                I1 + hsplit(i, 16 * (t & 1) + 4 * g, w, 0) + 256 * (t >> 1)) = v;
         }
 #pragma unroll
-        for (int s = 0; s < 3; s++) *reinterpret_cast<half8 *>(I2 + hoff<DP>(row, 32 * s + 8 * g)) = bx[s];
+        for (int s = 0; s < 3; s++)  // [row][32s + 8g]
+            *reinterpret_cast<half8 *>(I2 + hsplit<DP>(i, 8 * g, w, 0) + 256 * s) = bx[s];
+        SH_STAMP(agent, 5, threadIdx.x);
         __syncthreads();  // 3
+        SH_STAMP(agent, 6, threadIdx.x);
         // ---- W2: wave w owns layer-1 neurons 16w..16w+15: dW1 and db1
+#if SH_PIPE_BWD
+        {
+            half8 bv = frag_tr_h(I1, 0, 16 * w), xa[6];  // batch rows 0..31, then one step ahead
+#pragma unroll
+            for (int t = 0; t < 6; t++) xa[t] = frag_tr_h<DP>(I2, 0, 16 * t);
+#pragma unroll
+            for (int b0 = 0; b0 < B_; b0 += 32) {
+                half8 bn, xn[6];
+                if (b0 + 32 < B_) {
+                    bn = frag_tr_h(I1, b0 + 32, 16 * w);
+#pragma unroll
+                    for (int t = 0; t < 6; t++) xn[t] = frag_tr_h<DP>(I2, b0 + 32, 16 * t);
+                }
+                GB1 = mfma(ones, bv, GB1);
+#pragma unroll
+                for (int t = 0; t < 6; t++) G1[t] = mfma(xa[t], bv, G1[t]);
+                if (b0 + 32 < B_) {
+                    bv = bn;
+#pragma unroll
+                    for (int t = 0; t < 6; t++) xa[t] = xn[t];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#else
 #pragma unroll
         for (int b0 = 0; b0 < B_; b0 += 32) {
             const half8 bv = frag_tr_h(I1, b0, 16 * w);
@@ -635,7 +948,10 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, cons
             for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr_h<DP>(I2, b0, 16 * t), bv, G1[t]);
             __builtin_amdgcn_sched_barrier(0);
         }
+#endif
+        SH_STAMP(agent, 7, threadIdx.x);
         __syncthreads();  // 4: the images are rewritten by the next agent
+        SH_STAMP(agent, 8, threadIdx.x);
     }
     // partial sums of this workgroup, kernel layout (every index written once)
     float *G = slab + (size_t)blockIdx.x * L::P;

@@ -45,11 +45,13 @@ def _rows(t, idx):
     return t[torch.as_tensor(idx, device=t.device)].cpu().numpy()
 
 
-def _check_learn(tr, agents, pre, precision, shared):
-    """One learn of tr's last step for `agents`, from the pre-step state `pre`."""
+def _check_learn(tr, agents, pre, precision, shared, t32=None):
+    """One learn of tr's last step for `agents`, from the pre-step state `pre`.
+    t32: the loss tolerance vs the fp32 oracle (default TOL16's)."""
     ag = tr.agent
     rnd = ROUND[precision]
-    tl, ta, tr_, _, t32 = TOL16[precision]
+    tl, ta, tr_, _, t32_ = TOL16[precision]
+    t32 = t32_ if t32 is None else t32
     loss = ag.loss.cpu().numpy()
     assert np.isfinite(loss).all(), "every agent's loss is finite"
     idx = ag.idx.cpu().numpy()
@@ -75,9 +77,10 @@ def _check_learn(tr, agents, pre, precision, shared):
         assert np.isfinite(p_now).all() and not np.array_equal(p_now, pre[0][0])
 
 
-def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, sparse_until=0):
+def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, sparse_until=0,
+                t32=None):
     """sparse_until: before this step, compare with the oracle only every 97th
-    step (the oracle loops still run every step)."""
+    step (the oracle loops still run every step).  t32: _check_learn's."""
     cfg = AgentConfig(precision=precision, seed=0, shared_params=shared)
     tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=0), cfg)
     A, ag = tr.env.A, tr.agent
@@ -109,7 +112,7 @@ def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, 
             for i, out in enumerate(outs):
                 np.testing.assert_array_equal(idx[i], out["idx"], err_msg=f"step {step} env {i}")
         if pre is not None:
-            _check_learn(tr, pick, pre, precision, shared)
+            _check_learn(tr, pick, pre, precision, shared, t32)
             checked += 1
     assert checked == len(learn_checks)
     return tr
@@ -132,9 +135,13 @@ def test_c3_steady_state_wrapped_rings():
     and at every step after the wrap: actions, rewards, observations and replay
     indices bit-exact; at learns 3 and 5 steps after the wrap, for 8 agents,
     the device z-score bit-exact and the loss vs the Keras mixed-precision
-    checker (pinned to the reference's own learn) and the fp32 oracle."""
+    checker (pinned to the reference's own learn; rtol 2e-3, as at step 128)
+    and, as a sanity bound, the fp32 oracle at rtol 5e-2: after 10,000 learns
+    the f16 rounding of Q and y (which Keras's mixed_float16 learn does too)
+    moved one agent's loss 2.4 % from the fp32 learn's (measured, round 3)
+    while it matched the mixed checker to 2e-3."""
     cap = 10000
-    tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap)
+    tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap, t32=5e-2)
     ring = tr.agent.ring
     assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
     del tr

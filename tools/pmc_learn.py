@@ -4,7 +4,9 @@ the learn kernel, with the gfx950 corrections of MI355X_MICROARCH.md (HBM):
   * WRITE_SIZE (KB) is exact for 16-byte stores
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (TCC slots).
 Usage: python tools/pmc_learn.py <fetch_csv> <write_csv> <workload_key> [kernel_substr] [source]
-(source: where the passes were run, e.g. "profiles/r03/c3 @ <commit>").
+(kernel_substr: one name, or a comma list of the kernels one learn launches --
+their per-dispatch means are summed; source: where the passes were run, e.g.
+"profiles/r03/c3 @ <commit>").
 Writes/updates profiles/learn_pmc.json."""
 import csv
 import json
@@ -25,19 +27,23 @@ def main():
     fetch_csv, write_csv, key = sys.argv[1:4]
     substr = sys.argv[4] if len(sys.argv) > 4 else "k_learn"
     source = sys.argv[5] if len(sys.argv) > 5 else None
-    fv = per_kernel(fetch_csv, "FETCH_SIZE", substr)
-    wv = per_kernel(write_csv, "WRITE_SIZE", substr)
-    if not fv or not wv:
-        raise SystemExit(f"no {substr} rows: fetch {len(fv)} write {len(wv)}")
-    fetch_kb = sum(fv) / len(fv)
-    write_kb = sum(wv) / len(wv)
+    fetch_kb = write_kb = 0.0
+    counts = []
+    for name in substr.split(","):
+        fv = per_kernel(fetch_csv, "FETCH_SIZE", name)
+        wv = per_kernel(write_csv, "WRITE_SIZE", name)
+        if not fv or not wv:
+            raise SystemExit(f"no {name} rows: fetch {len(fv)} write {len(wv)}")
+        fetch_kb += sum(fv) / len(fv)
+        write_kb += sum(wv) / len(wv)
+        counts += [len(fv), len(wv)]
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                        "learn_pmc.json")
     d = {}
     if os.path.exists(out):
         with open(out) as f:
             d = json.load(f)
-    d[key] = {"kernel": substr, "dispatches": [len(fv), len(wv)],
+    d[key] = {"kernel": substr, "dispatches": counts,
               "FETCH_SIZE_KB_raw": fetch_kb, "WRITE_SIZE_KB_raw": write_kb,
               "hbm_bytes_per_launch": int(round((2.0 * fetch_kb + write_kb) * 1024)),
               "correction": "fetch x2 (gfx950 FETCH_SIZE reads 1/2 of wide streams), write x1"}

@@ -5,7 +5,8 @@
 #   2. --pmc FETCH_SIZE and 3. --pmc WRITE_SIZE (separate passes, TCC slots),
 #      reduced by tools/pmc_learn.py into profiles/learn_pmc.json for the learn
 #      kernel and k_sim_step (gfx950 corrections: FETCH x2, WRITE x1)
-#   4. --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES (own pass)
+#   4. --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES (own pass),
+#      per learn kernel (C5 launches four: next, grad, slab reduction, Adam)
 # Summaries are copied to gpurun_out/<tag>/<cfg>/ for committing under
 # profiles/<round>/.  Every GPU step has its own time limit; `set -e` stops the
 # chain at the first failure.
@@ -18,7 +19,7 @@ for CFG in "$@"; do
     case $CFG in
         c2) ARGS="--rows 2 --cols 2 --envs 256 --precision bf16"; KEY=2x2x256_bf16; LK=k_learn_bf16 ;;
         c3) ARGS="--rows 4 --cols 4 --envs 1024 --precision fp16"; KEY=4x4x1024_fp16; LK=k_learn_f16 ;;
-        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK=k_learn_shared ;;
+        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK=k_shared_next,k_shared_grad,k_reduce_slabs,k_adam ;;
         *) echo "unknown config $CFG"; exit 2 ;;
     esac
     O=$R/gpurun_out/$TAG/$CFG
@@ -41,7 +42,7 @@ for CFG in "$@"; do
     M=$(find $O/pmcM -name '*counter_collection.csv' | head -n 1)
     (cd $R && python3 tools/pmc_learn.py "$F" "$W" "$KEY" "$LK" "profiles/$TAG/$CFG" &&
          python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_sim" k_sim_step "profiles/$TAG/$CFG" &&
-         python3 tools/pmc_mfma.py "$M" "$LK" > $O/mfma_busy.json)
+         for K1 in ${LK//,/ }; do python3 tools/pmc_mfma.py "$M" "$K1" > $O/mfma_busy_$K1.json; done)
     cp "$(find $O/stats -name '*kernel_stats.csv' | head -n 1)" $O/kernel_stats.csv
     gzip -c "$F" > $O/fetch_size_counter_collection.csv.gz
     gzip -c "$W" > $O/write_size_counter_collection.csv.gz
