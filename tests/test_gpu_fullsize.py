@@ -47,11 +47,20 @@ def _rows(t, idx):
 
 def _check_learn(tr, agents, pre, precision, shared, t32=None):
     """One learn of tr's last step for `agents`, from the pre-step state `pre`.
-    t32: the loss tolerance vs the fp32 oracle (default TOL16's)."""
+    t32: the loss tolerance vs the fp32 oracle: an rtol, or "q-scaled"
+    (default): TOL16's rtol or, where larger, the change in the mean squared
+    TD error that an error of delta = 4 16-bit ulps of max|Q| in q - y can
+    make, 2 sqrt(L) delta + delta^2 -- Keras's mixed learn rounds Q and y to
+    f16 / bf16 (the device matches that learn to TOL16 above), so once |Q| is
+    a few times |q - y| a fixed rtol on L measures the 16-bit format, not the
+    kernel (round 3: C2 bf16 5.2 % in its first 13 learns, C3 fp16 5.8 % after
+    10,000 steps)."""
     ag = tr.agent
     rnd = ROUND[precision]
     tl, ta, tr_, _, t32_ = TOL16[precision]
-    t32 = t32_ if t32 is None else t32
+    t32 = "q-scaled" if t32 is None else t32
+    q_scaled = t32 == "q-scaled"
+    ulp = 2.0 ** -11 if precision == "fp16" else 2.0 ** -8
     loss = ag.loss.cpu().numpy()
     assert np.isfinite(loss).all(), "every agent's loss is finite"
     idx = ag.idx.cpu().numpy()
@@ -66,7 +75,14 @@ def _check_learn(tr, agents, pre, precision, shared, t32=None):
         np.testing.assert_allclose(loss[j], l_e, rtol=tl, err_msg=f"agent {j} vs emulation")
         p1, m1, v1 = p0.copy(), m0.copy(), v0.copy()
         l32 = O.learn(p1, t0, m1, v1, S, Aa, Rn, S2, D, t)
-        np.testing.assert_allclose(loss[j], l32, rtol=t32, err_msg=f"agent {j} vs fp32 oracle")
+        if q_scaled:
+            qmax = float(np.abs(O.qnet_forward(p0, S)).max())
+            delta = 4 * ulp * qmax
+            bound = max(t32_ * l32, 2 * np.sqrt(l32) * delta + delta * delta)
+            assert abs(loss[j] - l32) <= bound, (
+                f"agent {j}: loss {loss[j]} vs fp32 {l32}, max|Q| {qmax}, bound {bound}")
+        else:
+            np.testing.assert_allclose(loss[j], l32, rtol=t32, err_msg=f"agent {j} vs fp32 oracle")
         if not shared:
             m_g = kernel_to_keras(ag.adam_m[j:j + 1].cpu().numpy(), 128)[0]
             g_g = m0 + (m_g - m0) / np.float32(0.1)  # m1 = m0 + (g - m0) c1
@@ -136,12 +152,9 @@ def test_c3_steady_state_wrapped_rings():
     indices bit-exact; at learns 3 and 5 steps after the wrap, for 8 agents,
     the device z-score bit-exact and the loss vs the Keras mixed-precision
     checker (pinned to the reference's own learn; rtol 2e-3, as at step 128)
-    and, as a sanity bound, the fp32 oracle at rtol 5e-2: after 10,000 learns
-    the f16 rounding of Q and y (which Keras's mixed_float16 learn does too)
-    moved one agent's loss 2.4 % from the fp32 learn's (measured, round 3)
-    while it matched the mixed checker to 2e-3."""
+    and, as a sanity bound, the fp32 oracle "q-scaled" (_check_learn)."""
     cap = 10000
-    tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap, t32=5e-2)
+    tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap)
     ring = tr.agent.ring
     assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
     del tr
