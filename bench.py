@@ -210,6 +210,9 @@ def main():
                     help="stream schedule (dmdqn_amd/trainer.py; all bit-identical): none = one "
                          "stream; sample = replay draws on a side stream beside act/sim/observe/"
                          "store; full = step t+1's act/sim/observe/sample beside learn t")
+    ap.add_argument("--split-learn", action="store_true",
+                    help="independent learn as two launches (gradient, Adam; bit-identical; "
+                         "trainer.py split_learn)")
     ap.add_argument("--cu-split", type=int, default=0,
                     help="with --overlap full/sample: run the side stream on this many CUs "
                          "and the learn stream on the rest (CU-masked HIP streams)")
@@ -252,7 +255,8 @@ def main():
     # independent nets are seeded per rank; the shared net must start identical on every rank
     agent_cfg = AgentConfig(precision=args.precision, seed=1000 if args.shared else 1000 + rank,
                             shared_params=args.shared)
-    tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side)
+    tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side,
+                 split_learn=args.split_learn)
     E, A = tr.env.E, tr.env.A
     NA = E * A
     prefill = agent_cfg.replay_buffer_size if args.prefill_steps is None else args.prefill_steps
@@ -281,10 +285,13 @@ def main():
     D.barrier()
     torch.cuda.synchronize(dev)
     tr.agent.learn_hook = hook
+    from dmdqn_amd import kernels as KM
+    wait0 = KM.POLL_WAIT_S[0]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.step()
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
+    t_wait = KM.POLL_WAIT_S[0] - wait0  # ... of which blocked on the lagged replay check
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     D.barrier()
@@ -350,6 +357,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el_max / args.steps * 1e3, 4),
             "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 4),
+            # the host's own cost: issue time less the waits on the check POLL_LAG
+            # steps back (waits = the host is ahead of the GPU, not behind it)
+            "host_busy_ms_per_step": round((t_issue - t_wait) / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

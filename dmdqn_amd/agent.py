@@ -45,6 +45,8 @@ class CLearn(C.Structure):
 # directly (c_learn_args); the product path goes through torch.ops.dmdqn
 _lib.register({
     "dmdqn_learn": [C.POINTER(CLearn), C.c_void_p],
+    "dmdqn_learn_grad": [C.POINTER(CLearn), C.c_void_p, C.c_void_p],
+    "dmdqn_adam_agents": [C.POINTER(CLearn), C.c_void_p, C.c_void_p],
     "dmdqn_q_argmax": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                        C.c_void_p, C.c_void_p],
     "dmdqn_q_argmax_shared": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
@@ -326,6 +328,27 @@ class BatchedDQN:
         self.learn_hook = None  # optional callable(before: bool), e.g. HIP event timing
         self.stamps = None      # optional int64 [NA, 16] device tensor: phase timestamps
         self.rn_out = None      # optional f32 [NA, batch] device tensor: the z-scored rewards
+        self._split_grad = None  # [NA, P] f32 scratch of the split learn (set_split_learn)
+
+    def set_split_learn(self, on=True):
+        """Run each independent-agent learn as two launches (dmdqn_learn_grad,
+        dmdqn_adam_agents): bit-identical to the fused kernel, 4 more bytes of
+        HBM traffic per parameter each way, but its bandwidth-bound Adam half
+        can share the chip with the next step's act / sim / observe (trainer
+        overlap "full"), which the fused kernel's LDS-heavy workgroups leave no
+        room for.  fp16 / bf16, independent networks only."""
+        if on:
+            if self.shared or self.cfg.precision not in H16_DTYPES:
+                raise ValueError("the split learn is for independent fp16 / bf16 networks")
+            if self._split_grad is None:
+                self._split_grad = torch.empty((self.NA, self.P), dtype=torch.float32,
+                                               device=self.device)
+        else:
+            self._split_grad = None
+
+    @property
+    def split_learn(self):
+        return self._split_grad is not None
 
     # -------------------------------------------------------------- act
     def current_epsilon(self):
@@ -403,7 +426,7 @@ class BatchedDQN:
                                  self.adam_m, self.adam_v, self.target, self.target_h, self.loss,
                                  ring.start, self.H, PRECISIONS[cfg.precision], sync, cfg.gamma,
                                  alpha, c1, c2, eps, LOSSES[cfg.loss], qstats, self.rn_out,
-                                 self.stamps)
+                                 self.stamps, grad=self._split_grad)
         if self.learn_hook:
             self.learn_hook(False)
         self.learn_launches += 1

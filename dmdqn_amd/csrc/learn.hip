@@ -455,6 +455,10 @@ __global__ void __launch_bounds__(256) k_q_argmax(const float *params, size_t ps
 
 int launch_learn_f16(const dmdqn_learn_args *a, hipStream_t s);   // learn_f16.hip
 int launch_learn_bf16(const dmdqn_learn_args *a, hipStream_t s);  // learn_bf16.hip
+int launch_learn_grad_f16(const dmdqn_learn_args *a, float *grad, hipStream_t s);
+int launch_learn_grad_bf16(const dmdqn_learn_args *a, float *grad, hipStream_t s);
+int launch_adam_agents_f16(const dmdqn_learn_args *a, const float *grad, hipStream_t s);
+int launch_adam_agents_bf16(const dmdqn_learn_args *a, const float *grad, hipStream_t s);
 
 DMDQN_DBG_READER(dbg_flags_learn)
 
@@ -462,7 +466,7 @@ DMDQN_DBG_READER(dbg_flags_learn)
 
 using namespace dmdqn;
 
-extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
+static int check_learn_args(const dmdqn_learn_args *a) {
     DMDQN_REQUIRE(a, "dmdqn_learn: null args");
     DMDQN_REQUIRE(a->NA > 0 && a->cap >= a->batch && a->start >= 0 && a->start < a->cap,
                   "dmdqn_learn: NA=%d cap=%d start=%d", a->NA, a->cap, a->start);
@@ -474,6 +478,11 @@ extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
                   a->precision);
     DMDQN_REQUIRE(a->loss_kind == DMDQN_LOSS_MSE || a->loss_kind == DMDQN_LOSS_HUBER,
                   "dmdqn_learn: loss_kind %d", a->loss_kind);
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
+    if (int rc = check_learn_args(a)) return rc;
     if (a->precision == 1) return launch_learn_f16(a, as_stream(stream));
     if (a->precision == 2) return launch_learn_bf16(a, as_stream(stream));
     if (a->hidden == 128) {
@@ -487,6 +496,25 @@ extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
     }
     DMDQN_LAUNCH_CHECK("k_learn");
     return DMDQN_OK;
+}
+
+extern "C" int dmdqn_learn_grad(const dmdqn_learn_args *a, float *grad, void *stream) {
+    if (int rc = check_learn_args(a)) return rc;
+    DMDQN_REQUIRE(grad, "dmdqn_learn_grad: null grad");
+    DMDQN_REQUIRE(a->precision == 1 || a->precision == 2,
+                  "dmdqn_learn_grad: precision %d (the split learn is fp16 / bf16 only)",
+                  a->precision);
+    return a->precision == 1 ? launch_learn_grad_f16(a, grad, as_stream(stream))
+                             : launch_learn_grad_bf16(a, grad, as_stream(stream));
+}
+
+extern "C" int dmdqn_adam_agents(const dmdqn_learn_args *a, const float *grad, void *stream) {
+    DMDQN_REQUIRE(a && grad && a->NA > 0 && a->params && a->adam_m && a->adam_v && a->target,
+                  "dmdqn_adam_agents: null argument");
+    DMDQN_REQUIRE(a->precision == 1 || a->precision == 2,
+                  "dmdqn_adam_agents: precision %d (fp16 / bf16 only)", a->precision);
+    return a->precision == 1 ? launch_adam_agents_f16(a, grad, as_stream(stream))
+                             : launch_adam_agents_bf16(a, grad, as_stream(stream));
 }
 
 template <int H>

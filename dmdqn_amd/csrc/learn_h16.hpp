@@ -48,6 +48,9 @@
 #define H16_MFMA __builtin_amdgcn_mfma_f32_16x16x32_bf16
 #define H16_LEARN_KERNEL k_learn_bf16
 #define H16_LAUNCH launch_learn_bf16
+#define H16_LAUNCH_GRAD launch_learn_grad_bf16
+#define H16_LAUNCH_ADAM launch_adam_agents_bf16
+#define H16_ADAM_KERNEL k_adam_agents_bf16
 #define H16_NAME "bf16"
 #else
 #define H16K f16k
@@ -55,6 +58,9 @@
 #define H16_MFMA __builtin_amdgcn_mfma_f32_16x16x32_f16
 #define H16_LEARN_KERNEL k_learn_f16
 #define H16_LAUNCH launch_learn_f16
+#define H16_LAUNCH_GRAD launch_learn_grad_f16
+#define H16_LAUNCH_ADAM launch_adam_agents_f16
+#define H16_ADAM_KERNEL k_adam_agents_f16
 #define H16_NAME "fp16"
 #endif
 
@@ -422,7 +428,9 @@ __device__ __forceinline__ void adam_el(float &w, float &m, float &v, float g, f
 struct AdamC {
     float alpha, c1, c2, eps;
     bool sync;
-    h16 *TH;  // f16 target copy written on syncs (or null)
+    h16 *TH;    // f16 target copy written on syncs (or null)
+    bool gout;  // compile-time: write the 16-bit gradient to G instead of the
+    float *G;   // Adam step (split learn: dmdqn_learn_grad + dmdqn_adam_agents)
 };
 
 // Keras-3 Adam on NT groups of 4 consecutive parameters (one 16-byte lane
@@ -431,6 +439,13 @@ struct AdamC {
 template <int NT>
 __device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, const size_t *idx,
                                        const f32x4 *g, const AdamC &k) {
+    if (k.gout) {
+#pragma unroll
+        for (int q = 0; q < NT; q++)
+            *reinterpret_cast<float4 *>(k.G + idx[q]) =
+                make_float4(gval(g[q], 0), gval(g[q], 1), gval(g[q], 2), gval(g[q], 3));
+        return;
+    }
     float4 w[NT], m[NT], v[NT];
 #pragma unroll
     for (int q = 0; q < NT; q++) {
@@ -502,6 +517,15 @@ template <int NB, int NT, bool EARLY, typename Index, typename GT, typename Grad
 __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T, Index ix,
                                           const GT *g, const AdamC &k, Grad grad,
                                           Valid valid = {}) {
+    if (k.gout) {  // the same index map, the gradient stored instead
+        grad();
+#pragma unroll
+        for (int t = 0; t < NB * NT; t++)
+            if (valid(t))
+                *reinterpret_cast<float4 *>(k.G + ix(t)) =
+                    make_float4(gval(g[t], 0), gval(g[t], 1), gval(g[t], 2), gval(g[t], 3));
+        return;
+    }
     float4 w[2][NT], m[2][NT], v[2][NT];
     if constexpr (!EARLY) grad();
 #pragma unroll
@@ -570,6 +594,10 @@ __device__ __forceinline__ void adam4(float *W, float *M, float *V, float *T, si
 
 __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, size_t i, float g,
                                       const AdamC &k) {
+    if (k.gout) {
+        k.G[i] = r16(g);
+        return;
+    }
     float m = M[i], v = V[i], w = W[i];
     adam_el(w, m, v, r16(g), k.alpha, k.c1, k.c2, k.eps);  // the 16-bit gradient
     M[i] = m;
@@ -882,9 +910,12 @@ __device__ __forceinline__ void bwd_dz1(h16 *R1, const uint32_t *mask, const f32
 // QSTATS: also emit the learn metrics (a.qstats != NULL).  SYNC: this learn
 // ends with the hard target copy (a.sync_target): a compile-time constant, so
 // the Adam streams of the other 499 of 500 learns carry no branch (a branch
-// there makes the vmcnt waits conservative).
-template <bool QSTATS, bool SYNC>
-__global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
+// there makes the vmcnt waits conservative).  GOUT: the split learn -- every
+// gradient entry goes to gout[agent][P] (the 16-bit value Adam would receive)
+// and dmdqn_adam_agents applies the identical Adam step in a second launch,
+// which can share the chip with the next step's side-stream work.
+template <bool QSTATS, bool SYNC, bool GOUT>
+__global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, float *gout) {
     LEARN_SMEM_SETUP;
     const int agent = blockIdx.x;
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
@@ -893,7 +924,8 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
     float *Tp = a.target + agent * Pz;
     const size_t Ph = (Pz + 7) / 8 * 8;
     h16 *TH = a.target_h ? reinterpret_cast<h16 *>(a.target_h) + agent * Ph : nullptr;
-    const AdamC AK{a.alpha, a.c1, a.c2, a.eps, SYNC, TH};
+    const AdamC AK{a.alpha, a.c1, a.c2, a.eps, SYNC && !GOUT, TH, GOUT,
+                   GOUT ? gout + agent * Pz : nullptr};
     STAMP(0);
     Frags fr;
     if (TH) load_frags(TH, fr);  // in flight during the z-score + gather
@@ -932,6 +964,7 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
     STAMP(7);
     const half8 ones = ones8();
 #if DMDQN_EARLY_W3
+    static_assert(!GOUT, "the early-W3 variant has no split form");
     // ---- dW3[k][a] = H2^T . DQ (wave w: k-tile w) ; db3 (wave 0).  W3's
     // Adam loads (lanes lr < 4: rows k = 16w + 4lg + e, column a -> W3T[a][k..k+3])
     // are issued before the loss, so their latency hides behind it.
@@ -1077,6 +1110,40 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a) {
     }
 }
 
+// The split learn's second launch: Keras-3 Adam (adam_el, the fused kernel's
+// arithmetic) on every agent's P parameters from grad[NA][P]; on a sync also
+// the f32 target and its 16-bit shadow (agent stride Ph).  One lane per 4
+// consecutive parameters, blockIdx.y = agent.
+template <bool SYNC>
+__global__ void __launch_bounds__(256) H16_ADAM_KERNEL(float *W, float *M, float *V, float *T,
+                                                       h16 *TH, const float *G, float alpha,
+                                                       float c1, float c2, float eps) {
+    constexpr int P4 = L::P / 4;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= P4) return;
+    const size_t Ph = ((size_t)L::P + 7) / 8 * 8;
+    const size_t i = (size_t)blockIdx.y * L::P + 4 * (size_t)q;
+    float4 w = *reinterpret_cast<const float4 *>(W + i), m = *reinterpret_cast<const float4 *>(M + i);
+    float4 v = *reinterpret_cast<const float4 *>(V + i);
+    const float4 g = *reinterpret_cast<const float4 *>(G + i);
+    float *pw = &w.x, *pm = &m.x, *pv = &v.x;
+    const float *pg = &g.x;
+#pragma unroll
+    for (int e = 0; e < 4; e++) adam_el(pw[e], pm[e], pv[e], pg[e], alpha, c1, c2, eps);
+    *reinterpret_cast<float4 *>(W + i) = w;
+    *reinterpret_cast<float4 *>(M + i) = m;
+    *reinterpret_cast<float4 *>(V + i) = v;
+    if (SYNC) {
+        *reinterpret_cast<float4 *>(T + i) = w;
+        if (TH) {
+            half4v hv;
+            hv[0] = (h16)w.x; hv[1] = (h16)w.y;
+            hv[2] = (h16)w.z; hv[3] = (h16)w.w;
+            *reinterpret_cast<half4v *>(TH + (size_t)blockIdx.y * Ph + 4 * (size_t)q) = hv;
+        }
+    }
+}
+
 DMDQN_DBG_READER(dbg_flags)
 
 }  // namespace H16K
@@ -1086,10 +1153,40 @@ int H16_LAUNCH(const dmdqn_learn_args *a, hipStream_t s) {
                   "dmdqn_learn: precision %d (" H16_NAME ") needs hidden=128 (P=%d)", a->precision,
                   H16K::L::P);
     using namespace H16K;
-    auto kern = a->qstats ? (a->sync_target ? H16_LEARN_KERNEL<true, true> : H16_LEARN_KERNEL<true, false>)
-                          : (a->sync_target ? H16_LEARN_KERNEL<false, true> : H16_LEARN_KERNEL<false, false>);
-    hipLaunchKernelGGL(kern, dim3(a->NA), dim3(512), 0, s, *a);
+    auto kern = a->qstats ? (a->sync_target ? H16_LEARN_KERNEL<true, true, false>
+                                            : H16_LEARN_KERNEL<true, false, false>)
+                          : (a->sync_target ? H16_LEARN_KERNEL<false, true, false>
+                                            : H16_LEARN_KERNEL<false, false, false>);
+    hipLaunchKernelGGL(kern, dim3(a->NA), dim3(512), 0, s, *a, (float *)nullptr);
     DMDQN_LAUNCH_CHECK("k_learn_" H16_NAME);
+    return DMDQN_OK;
+}
+
+// The split learn's first launch: forward/backward, gradient -> grad[NA][P].
+int H16_LAUNCH_GRAD(const dmdqn_learn_args *a, float *grad, hipStream_t s) {
+    DMDQN_REQUIRE(a->hidden == 128 && a->P == H16K::L::P,
+                  "dmdqn_learn_grad: precision %d (" H16_NAME ") needs hidden=128 (P=%d)",
+                  a->precision, H16K::L::P);
+    using namespace H16K;
+    auto kern = a->qstats ? H16_LEARN_KERNEL<true, false, true> : H16_LEARN_KERNEL<false, false, true>;
+    hipLaunchKernelGGL(kern, dim3(a->NA), dim3(512), 0, s, *a, grad);
+    DMDQN_LAUNCH_CHECK("k_learn_" H16_NAME " (gradient)");
+    return DMDQN_OK;
+}
+
+// The split learn's second launch (a's Adam constants and sync_target).
+int H16_LAUNCH_ADAM(const dmdqn_learn_args *a, const float *grad, hipStream_t s) {
+    using namespace H16K;
+    DMDQN_REQUIRE(a->P == L::P, "dmdqn_adam_agents: P=%d != %d", a->P, L::P);
+    const dim3 grid((L::P / 4 + 255) / 256, a->NA);
+    h16 *TH = reinterpret_cast<h16 *>(a->target_h);
+    if (a->sync_target)
+        hipLaunchKernelGGL(H16_ADAM_KERNEL<true>, grid, dim3(256), 0, s, a->params, a->adam_m,
+                           a->adam_v, a->target, TH, grad, a->alpha, a->c1, a->c2, a->eps);
+    else
+        hipLaunchKernelGGL(H16_ADAM_KERNEL<false>, grid, dim3(256), 0, s, a->params, a->adam_m,
+                           a->adam_v, a->target, TH, grad, a->alpha, a->c1, a->c2, a->eps);
+    DMDQN_LAUNCH_CHECK("k_adam_agents_" H16_NAME);
     return DMDQN_OK;
 }
 

@@ -6,6 +6,8 @@ below is one (or a few) launches of a hand-written gfx950 kernel in
 libdmdqn_hip.so, through the TORCH_LIBRARY(dmdqn) registration (ops.py), on
 torch's current stream.
 """
+import time
+
 import torch
 
 from . import _lib
@@ -140,7 +142,9 @@ class ReplayRing:
         i = self._poll_i % POLL_LAG
         host, ev = self._err_slots[i]
         if self._err_live[i]:
-            ev.synchronize()  # recorded POLL_LAG steps ago: normally long complete
+            t0 = time.perf_counter()
+            ev.synchronize()  # recorded POLL_LAG steps ago: complete unless the host is ahead
+            POLL_WAIT_S[0] += time.perf_counter() - t0
             if int(host[0]) != 0:
                 raise _lib.DmdqnError(_RANGE_MSG)
         host.copy_(self.err, non_blocking=True)
@@ -150,6 +154,9 @@ class ReplayRing:
 
 
 POLL_LAG = 4  # steps the host may run ahead of the replay range check
+# host seconds spent blocked in poll() (bench.py: the host's own issue cost is
+# the issue time minus this -- a host POLL_LAG steps ahead of the GPU waits here)
+POLL_WAIT_S = [0.0]
 
 
 _RANGE_MSG = ("replay_store: an observation value is not an integer in [-128, 127]; the int8 "

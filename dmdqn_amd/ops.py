@@ -23,6 +23,7 @@ ENTRY_POINTS = {
     "dmdqn_replay_store": "replay_store", "dmdqn_replay_sample": "replay_sample",
     "dmdqn_sim_reset": "sim_reset", "dmdqn_sim_reset_envs": "sim_reset",
     "dmdqn_sim_step": "sim_step", "dmdqn_learn": "learn_step",
+    "dmdqn_learn_grad": "learn_step", "dmdqn_adam_agents": "learn_step",
     "dmdqn_learn_shared_grad": "learn_shared_grad", "dmdqn_adam": "adam",
     "dmdqn_target_sync": "target_sync", "dmdqn_q_argmax": "q_argmax",
     "dmdqn_q_argmax_shared": "q_argmax",

@@ -271,13 +271,19 @@ void learn_step(const Tensor &ring_s, const Tensor &ring_n, const Tensor &ring_a
                 Tensor &adam_m, Tensor &adam_v, Tensor &target, const OptT &target_h, Tensor &loss,
                 int64_t start, int64_t hidden, int64_t precision, bool sync, double gamma,
                 double alpha, double c1, double c2, double eps, int64_t loss_kind,
-                const OptT &qstats, const OptT &rn_out, const OptT &stamps) {
+                const OptT &qstats, const OptT &rn_out, const OptT &stamps, const OptT &grad) {
     const int64_t NA = loss.numel();
     dmdqn_learn_args a = make_learn(ring_s, ring_n, ring_a, ring_d, ring_r, idx, params, adam_m,
                                     adam_v, target, target_h, loss, start, hidden, precision, sync,
                                     gamma, alpha, c1, c2, eps, loss_kind, qstats, rn_out,
                                     std::nullopt, stamps, NA, NA);
     c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
+    if (grad.has_value()) {  // the split learn: gradient launch, then the Adam launch
+        auto gr = dptr<float>(*grad, at::kFloat, "grad", NA * (int64_t)a.P);
+        check(dmdqn_learn_grad(&a, gr, stream_of(params)), "dmdqn_learn_grad");
+        check(dmdqn_adam_agents(&a, gr, stream_of(params)), "dmdqn_adam_agents");
+        return;
+    }
     check(dmdqn_learn(&a, stream_of(params)), "dmdqn_learn");
 }
 
@@ -368,7 +374,7 @@ void sim_step_meta(at::TensorList, at::TensorList, at::IntArrayRef, at::ArrayRef
 void learn_step_meta(const Tensor &, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                      const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, const OptT &, Tensor &,
                      int64_t, int64_t, int64_t, bool, double, double, double, double, double,
-                     int64_t, const OptT &, const OptT &, const OptT &) {}
+                     int64_t, const OptT &, const OptT &, const OptT &, const OptT &) {}
 void learn_shared_grad_meta(const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, Tensor &, int64_t, double, int64_t,
@@ -410,7 +416,7 @@ TORCH_LIBRARY(dmdqn, m) {
           "Tensor idx, Tensor(a!) params, Tensor(b!) adam_m, Tensor(c!) adam_v, Tensor(d!) target, "
           "Tensor(e!)? target_h, Tensor(f!) loss, int start, int hidden, int precision, bool sync, "
           "float gamma, float alpha, float c1, float c2, float eps, int loss_kind, "
-          "Tensor(g!)? qstats, Tensor(h!)? rn_out, Tensor(i!)? stamps) -> ()");
+          "Tensor(g!)? qstats, Tensor(h!)? rn_out, Tensor(i!)? stamps, Tensor(j!)? grad=None) -> ()");
     // C5: per-agent gradients of one shared net, summed
     m.def("learn_shared_grad(Tensor ring_s, Tensor ring_n, Tensor ring_a, Tensor ring_d, "
           "Tensor ring_r, Tensor idx, Tensor params, Tensor target, Tensor target_h, "

@@ -26,6 +26,9 @@ sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
             shares the GPU with the sim, so its own duration grows.
               side:  [wait store t-1] act_t sim_t observe_t sample_t (ev_obs)
               main:                  [wait ev_obs] store_t (ev_store) learn_t
+            The fused learn's workgroups fill every CU until they end, so the
+            side work queued beside it mostly waits; split_learn=True makes the
+            learn two launches whose Adam half leaves room beside it.
 
 What a step returns or exposes per step (obs, reward, loss, agent.actions,
 agent.idx) is fresh or double-buffered, so the caller may read it on its own
@@ -53,7 +56,7 @@ class StepStats:
 
 class Trainer:
     def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
-                 overlap="none", side_stream=None):
+                 overlap="none", side_stream=None, split_learn=False):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
         if overlap is True or overlap is False:
             overlap = "full" if overlap else "none"
@@ -69,6 +72,13 @@ class Trainer:
         self._join = True  # the side stream's first work waits for everything before it
         self.agent = BatchedDQN(self.env.E, self.env.A, agent_cfg or AgentConfig(), device=device,
                                 env_seeds=self.env.seeds)
+        # split_learn (agent.set_split_learn): the learn as two launches so its
+        # Adam half can share the chip with the next step's side-stream work
+        # (overlap "full").  Off by default: measured at C2 (round 3), the
+        # overlapped sim / act ran 2x / 6x slower beside the bandwidth-bound
+        # Adam and the step lost 3 % (3.01 vs 3.09 M steps/s).
+        if split_learn:
+            self.agent.set_split_learn(True)
         self.obs = self.env.reset()
         self.episode = 0
         self.step_count = 0

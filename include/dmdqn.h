@@ -265,6 +265,18 @@ typedef struct dmdqn_learn_args {
 
 int dmdqn_learn(const dmdqn_learn_args *args, void *stream);
 
+/* dmdqn_learn split in two launches (precision 1 / 2 only; same arithmetic,
+ * bit-identical results -- the same DQNAgent.replay, dqn_agent.py:328-380):
+ * dmdqn_learn_grad runs the forward/backward and writes each agent's 16-bit
+ * gradient (the values Keras's Adam receives, as f32) to grad [NA][P] (device
+ * layout); dmdqn_adam_agents then applies the Keras-3 Adam step of the same
+ * args (alpha, c1, c2, eps, sync_target) to params / adam_m / adam_v (and
+ * target / target_h on a sync).  The second launch is bandwidth-bound and
+ * small-footprint, so the next env step's work can share the chip with it
+ * (trainer.py, overlap "full").  grad is scratch owned by the caller. */
+int dmdqn_learn_grad(const dmdqn_learn_args *args, float *grad, void *stream);
+int dmdqn_adam_agents(const dmdqn_learn_args *args, const float *grad, void *stream);
+
 /* Hard target sync outside a learn (DQNAgent.update_target_network,
  * dqn_agent.py:382-387): target[NW][P] <- params[NW][P]; when target_h is not
  * NULL (precision 1 = f16, 2 = bf16) also its 16-bit shadow [NW][Ph], RNE. */
