@@ -19,7 +19,9 @@ namespace dmdqn {
 __device__ __forceinline__ int8_t to_i8(float v, int32_t *err) {
     float r = rintf(v);
     if (!(r == v) || r < -128.0f || r > 127.0f) {
-        atomicExch(err, DMDQN_ERANGE);
+        // every writer stores the same code: a plain store (err may be pinned
+        // host memory, where device atomics are not available)
+        *reinterpret_cast<volatile int32_t *>(err) = DMDQN_ERANGE;
         return 0;
     }
     return (int8_t)(int)r;

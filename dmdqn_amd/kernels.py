@@ -97,9 +97,15 @@ class ReplayRing:
         self.a = torch.zeros((NA, cap), dtype=torch.uint8, **z)
         self.r = torch.zeros((NA, cap), dtype=torch.float64, **z)
         self.d = torch.zeros((NA, cap), dtype=torch.uint8, **z)
-        self.err = torch.zeros(1, dtype=torch.int32, **z)
+        # the range flag lives in pinned host memory, written by the store kernel
+        # itself (zero-copy; only on an error): polling it needs no copy launch
+        if torch.device(device).type == "cuda":
+            self.err = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        else:
+            self.err = torch.zeros(1, dtype=torch.int32, **z)
+        self.device = torch.device(device)
         self.total = 0
-        self._err_slots = None  # POLL_LAG pinned copies of err in flight (poll)
+        self._err_events = None  # the event recorded behind a store every POLL_LAG polls
         self._poll_i = 0
 
     def __len__(self):
@@ -122,35 +128,43 @@ class ReplayRing:
         self.total += 1
 
     def check(self):
-        """Raise if a stored value was not exactly representable (syncs)."""
-        if int(self.err.item()) != 0:
+        """Raise if a stored value was not exactly representable (syncs the
+        current stream, behind every store issued on it)."""
+        if self.err.is_pinned():
+            torch.cuda.current_stream(self.device).synchronize()
+        if int(self.err[0]) != 0:
             raise _lib.DmdqnError(_RANGE_MSG)
 
     def poll(self):
-        """Deferred check without stalling the stream: raise if the flag copied
-        POLL_LAG polls ago was set, then start an asynchronous copy of the
-        current flag into pinned host memory.  The flag is sticky, so a bad
-        store raises at most POLL_LAG polls later (the product path polls after
-        every store) while the host keeps up to POLL_LAG steps of work queued
-        ahead of the GPU; episode ends and checkpoint saves call check(), which
-        waits.  The reference stores float32 rows (dqn_agent.py:39-56), and this
-        build's int8 rows must never silently hold a rounded value."""
-        if self._err_slots is None:
-            self._err_slots = [(torch.zeros(1, dtype=torch.int32, pin_memory=True),
-                                torch.cuda.Event()) for _ in range(POLL_LAG)]
-            self._err_live = [False] * POLL_LAG
-        i = self._poll_i % POLL_LAG
-        host, ev = self._err_slots[i]
-        if self._err_live[i]:
-            t0 = time.perf_counter()
-            ev.synchronize()  # recorded POLL_LAG steps ago: complete unless the host is ahead
-            POLL_WAIT_S[0] += time.perf_counter() - t0
-            if int(host[0]) != 0:
-                raise _lib.DmdqnError(_RANGE_MSG)
-        host.copy_(self.err, non_blocking=True)
-        ev.record()
-        self._err_live[i] = True
+        """Deferred check without stalling the stream.  The store kernels write
+        the (sticky) flag straight into pinned host memory.  Every POLL_LAG-th
+        poll waits for the event recorded POLL_LAG polls earlier (behind that
+        poll's store), reads the flag, raises if it is set, and records a new
+        event: a bad store raises at most 2 POLL_LAG - 1 polls later (the
+        product path polls after every store), the host keeps up to ~POLL_LAG
+        steps of work queued ahead of the GPU, and the queue carries one event
+        marker per POLL_LAG steps (each costs the GPU a few microseconds).
+        Episode ends and checkpoint saves call check(), which waits.  The
+        reference stores float32 rows (dqn_agent.py:39-56), and this build's
+        int8 rows must never silently hold a rounded value."""
+        if not self.err.is_pinned():  # a CPU-device ring: nothing in flight
+            self.check()
+            return
         self._poll_i += 1
+        if self._poll_i % POLL_LAG:
+            return
+        if self._err_events is None:
+            self._err_events = torch.cuda.Event()
+            self._err_live = False
+        ev = self._err_events
+        if self._err_live:
+            t0 = time.perf_counter()
+            ev.synchronize()  # recorded POLL_LAG polls ago: complete unless the host is ahead
+            POLL_WAIT_S[0] += time.perf_counter() - t0
+            if int(self.err[0]) != 0:
+                raise _lib.DmdqnError(_RANGE_MSG)
+        ev.record()
+        self._err_live = True
 
 
 POLL_LAG = 4  # steps the host may run ahead of the replay range check

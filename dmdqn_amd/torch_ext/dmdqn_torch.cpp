@@ -143,7 +143,10 @@ void replay_store(int64_t slot, const Tensor &obs_s, const Tensor &obs_n, const 
     auto ra = dptr<uint8_t>(ring_a, at::kByte, "ring_a", NA * cap);
     auto rr = dptr<double>(ring_r, at::kDouble, "ring_r", NA * cap);
     auto rd = dptr<uint8_t>(ring_d, at::kByte, "ring_d", NA * cap);
-    auto e = dptr<int32_t>(err, at::kInt, "err", 1);
+    // err: a device tensor, or pinned host memory the kernel writes directly
+    TORCH_CHECK(err.is_cuda() || err.is_pinned(), "err must be a device tensor or pinned host memory");
+    TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() == 1, "err must be one int32");
+    auto e = reinterpret_cast<int32_t *>(err.data_ptr());
     c10::hip::HIPGuardMasqueradingAsCUDA g(obs_s.device());
     check(dmdqn_replay_store((int)NA, int32_of(cap, "cap"), int32_of(slot, "slot"), s, n, a, r, d,
                              rs, rn, ra, rr, rd, e, stream_of(obs_s)),

@@ -112,7 +112,9 @@ int dmdqn_observe(int R, int C, int E, const int32_t *halt, const int32_t *phase
  * Replaces ReplayBuffer.add (src/agents/dqn_agent.py:31-57): one transition
  * per agent into ring slot `slot` (capacity `cap`).  Observations are stored
  * as int8 rows of DMDQN_ROW_BYTES (exact for this env's integer features; a
- * non-representable value sets *err to DMDQN_ERANGE).  done: uint8 [NA].
+ * non-representable value sets *err to DMDQN_ERANGE with a plain store, so
+ * err may be device memory or pinned host memory the host polls without a
+ * copy).  done: uint8 [NA].
  * ring_s / ring_n int8 [NA][cap][DMDQN_ROW_BYTES] (ring_n rows also receive
  * a, done and r at DMDQN_ROW_A / _D / _R); ring_a uint8 [NA][cap];
  * ring_r f64 [NA][cap]; ring_d uint8 [NA][cap] (the same values, per slot, for

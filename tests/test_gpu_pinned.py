@@ -371,8 +371,9 @@ def test_dropin_replaybuffer_sample_zscore_bit_exact():
 # ---------------------------------------------------------------------------
 # replay range errors on the product path
 def test_remember_non_integer_observation_raises():
-    """A non-int8 observation raises POLL_LAG stores later (the host is not
-    held back by the check), and check() raises at once."""
+    """A non-int8 observation raises within 2 POLL_LAG - 1 stores after it
+    (kernels.ReplayRing.poll: one event per POLL_LAG polls; it can raise
+    sooner when the GPU is ahead, never later), and check() raises at once."""
     from dmdqn_amd.kernels import POLL_LAG
     ag = BatchedDQN(1, 2, AgentConfig(replay_buffer_size=50))
     good = torch.zeros((1, 2, 89), dtype=torch.float32, device=DEV)
@@ -380,12 +381,13 @@ def test_remember_non_integer_observation_raises():
     bad[0, 1, 5] = 0.5
     a = torch.zeros((1, 2), dtype=torch.int32, device=DEV)
     r = torch.zeros((1, 2), dtype=torch.float64, device=DEV)
-    ag.remember(good, a, r, good, False)
-    ag.remember(bad, a, r, good, False)  # deferred
-    for _ in range(POLL_LAG - 1):
+    for _ in range(POLL_LAG + 2):  # a clean ring never raises
         ag.remember(good, a, r, good, False)
+    ag.ring.check()
+    ag.remember(bad, a, r, good, False)
     with pytest.raises(_lib.DmdqnError, match="not an integer"):
-        ag.remember(good, a, r, good, False)
+        for _ in range(2 * POLL_LAG - 1):
+            ag.remember(good, a, r, good, False)
     with pytest.raises(_lib.DmdqnError, match="not an integer"):
         ag.ring.check()
 
@@ -402,13 +404,13 @@ def test_dropin_remember_raises_immediately():
 
 
 def test_trainer_raises_on_non_integer_observation():
-    """... within POLL_LAG + 1 steps of the bad store."""
+    """... within 2 POLL_LAG steps of the bad store (kernels.ReplayRing.poll)."""
     from dmdqn_amd.kernels import POLL_LAG
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=2, seed=1), AgentConfig(replay_buffer_size=50))
     tr.step()
     tr.obs = tr.obs + 0.25  # a caller feeding its own features
     with pytest.raises(_lib.DmdqnError):
-        for _ in range(POLL_LAG + 1):
+        for _ in range(2 * POLL_LAG):
             tr.step()
 
 
