@@ -20,7 +20,7 @@
  * restatement is the stricter oracle, tolerances are stated in the tests).
  * TF/Keras are absent.  The restatement is pinned by tests/golden/learn.npz:
  * the reference's own DQNAgent.learn control flow run over a torch-backed TF
- * shim (tests/golden/make_learn_golden.py, tf_shim.py), 633 MSE and 233 Huber
+ * shim (tests/golden/make_learn_golden.py, tf_shim.py), 393 MSE and 233 Huber
  * learns (tests/test_learn_golden_cpu.py); and cross-checked against torch
  * autograd in tests/test_learn_oracle_cpu.py.
  *

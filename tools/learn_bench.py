@@ -1,7 +1,8 @@
 """Diagnostic: the fp16 (or --bf16) learn kernel alone at C3 size (16 agents x 1024 envs)
 on random replay contents, timed with HIP events on one stream.  Prints the
 median and min of N launches (ms) -- a tighter A/B signal than bench.py.
-usage: python tools/learn_bench.py [N] [--shared] [--bf16]"""
+usage: python tools/learn_bench.py [N] [--shared] [--bf16] [--envs E] [--agents A]
+(default E = 1024, A = 16: C3; C2 is --envs 256 --agents 4 --bf16)"""
 import json
 import sys
 
@@ -14,7 +15,11 @@ from dmdqn_amd.agent import AgentConfig, BatchedDQN  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 40
 shared = "--shared" in sys.argv
 prec = "bf16" if "--bf16" in sys.argv else "fp16"
-E, A = 1024, 16
+def _opt(name, default):
+    return int(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else default
+
+
+E, A = _opt("--envs", 1024), _opt("--agents", 16)
 ag = BatchedDQN(E, A, AgentConfig(precision=prec, seed=0, shared_params=shared,
                                   replay_buffer_size=1000))
 g = torch.Generator(device="cuda").manual_seed(0)
