@@ -28,6 +28,8 @@ SIGNATURES = {
     "dmdqn_observe": [i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "dmdqn_replay_store": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dmdqn_replay_sample": [vp, i32, i32, i32, i32, vp, vp],
+    "dmdqn_replay_store_f32": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "dmdqn_replay_gather_f32": [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp],
     "dmdqn_stream_create_cumask": [u32, vp, vp],
     "dmdqn_stream_destroy": [vp],
 }

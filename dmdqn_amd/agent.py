@@ -38,7 +38,8 @@ class CLearn(C.Structure):
                                   "loss"]] + [
         (n, C.c_float) for n in ["gamma", "alpha", "c1", "c2", "eps"]] + [
         ("stamps", C.c_void_p), ("qstats", C.c_void_p), ("params_h", C.c_void_p),
-        ("loss_kind", C.c_int32), ("rn_out", C.c_void_p)]
+        ("loss_kind", C.c_int32), ("rn_out", C.c_void_p), ("row_format", C.c_int32),
+        ("xs", C.c_void_p), ("xn", C.c_void_p)]
 
 
 # ctypes signatures of the learn entry points: the C-ABI tests call them
@@ -232,6 +233,10 @@ class AgentConfig:
     # trained on the mean of the per-agent losses; gradients all-reduced over
     # RCCL across ranks.  Requires precision "fp16" and nn_layers [128, 128].
     shared_params: bool = False
+    # replay row storage: "int8" (batched path, exact for this env, others
+    # raise) | "f32" (any observation value, as dqn_agent.py:39-56 stores it;
+    # the per-agent drop-in DQNAgent uses it)
+    replay_rows: str = "int8"
 
     @classmethod
     def from_dict(cls, d):
@@ -298,7 +303,12 @@ class BatchedDQN:
             self.shared_work = torch.empty(NA * cfg.batch_size * 5, dtype=torch.uint8, device=dev)
         self.adam_m = torch.zeros_like(self.params)
         self.adam_v = torch.zeros_like(self.params)
-        self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev)
+        if cfg.replay_rows not in ("int8", "f32"):
+            raise ValueError("replay_rows must be 'int8' or 'f32'")
+        if self.shared and cfg.replay_rows != "int8":
+            raise ValueError("the shared-network learn reads int8 replay rows only")
+        self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev, row_format=cfg.replay_rows)
+        self._xs = self._xn = None  # float rows: the learn's pre-gathered batch
         if streams is not None:
             # shared (np_state, py_state) device streams, e.g. the process-global
             # ones behind the per-agent DQNAgent surface
@@ -338,8 +348,9 @@ class BatchedDQN:
         overlap "full"), which the fused kernel's LDS-heavy workgroups leave no
         room for.  fp16 / bf16, independent networks only."""
         if on:
-            if self.shared or self.cfg.precision not in H16_DTYPES:
-                raise ValueError("the split learn is for independent fp16 / bf16 networks")
+            if self.shared or self.cfg.precision not in H16_DTYPES or self.ring.row_format != "int8":
+                raise ValueError("the split learn is for independent fp16 / bf16 networks "
+                                 "on int8 replay rows")
             if self._split_grad is None:
                 self._split_grad = torch.empty((self.NA, self.P), dtype=torch.float32,
                                                device=self.device)
@@ -422,11 +433,19 @@ class BatchedDQN:
         if self.shared:
             self._learn_shared(alpha, c1, c2, eps, sync, qstats)
         else:
+            xs = xn = None
+            if ring.row_format == "f32":  # float rows: the batch gathered in order first
+                if self._xs is None:
+                    shape = (self.NA, cfg.batch_size, K.ROW_FLOATS)
+                    self._xs = torch.empty(shape, dtype=torch.float32, device=self.device)
+                    self._xn = torch.empty(shape, dtype=torch.float32, device=self.device)
+                ring.gather_f32(self.idx, self._xs, self._xn)
+                xs, xn = self._xs, self._xn
             self._ops.learn_step(ring.s, ring.n, ring.a, ring.d, ring.r, self.idx, self.params,
                                  self.adam_m, self.adam_v, self.target, self.target_h, self.loss,
                                  ring.start, self.H, PRECISIONS[cfg.precision], sync, cfg.gamma,
                                  alpha, c1, c2, eps, LOSSES[cfg.loss], qstats, self.rn_out,
-                                 self.stamps, grad=self._split_grad)
+                                 self.stamps, grad=self._split_grad, xs=xs, xn=xn)
         if self.learn_hook:
             self.learn_hook(False)
         self.learn_launches += 1
@@ -447,7 +466,10 @@ class BatchedDQN:
                       None if self.stamps is None else self.stamps.data_ptr(),
                       None if qstats is None else qstats.data_ptr(),
                       None if self.params_h is None else self.params_h.data_ptr(),
-                      LOSSES[cfg.loss], None if self.rn_out is None else self.rn_out.data_ptr())
+                      LOSSES[cfg.loss], None if self.rn_out is None else self.rn_out.data_ptr(),
+                      int(self.ring.row_format == "f32"),
+                      None if self._xs is None else self._xs.data_ptr(),
+                      None if self._xn is None else self._xn.data_ptr())
 
     def presample(self, n):
         """Draw the next learn's replay indices now (ReplayBuffer.sample,

@@ -14,6 +14,8 @@
 // f16) | H1 f32 [128][128] | H2 f32 [128][128] | per-row scratch.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 #include "qnet_layout.hpp"
 
@@ -88,13 +90,14 @@ __device__ __forceinline__ void dense_tile(const TX *X, int ldx, const float *WT
 }
 
 // Full forward of one 128-row batch: H1, H2 (post-ReLU) in LDS, Q -> z3[128][4].
-template <int H>
-__device__ void forward(const float *P, const _Float16 *X, float *H1, float *H2, float *z3) {
+// X: the f16 LDS image (int8 rows) or the f32 pre-gathered rows (float rows).
+template <int H, typename TX>
+__device__ void forward(const float *P, const TX *X, float *H1, float *H2, float *z3) {
     using L = Lay<H>;
     const int w = threadIdx.x >> 6;
     constexpr int NT = H / 16;  // column tiles per layer
     for (int nt = w; nt < NT; nt += 8)
-        dense_tile<H, D_, _Float16, true, 0>(X, DP, P + L::oW1T, P + L::ob1, H1, H, 16 * nt, 16);
+        dense_tile<H, D_, TX, true, 0>(X, DP, P + L::oW1T, P + L::ob1, H1, H, 16 * nt, 16);
     __syncthreads();
     for (int nt = w; nt < NT; nt += 8)
         dense_tile<H, H, float, true, H>(H1, H, P + L::oW2T, P + L::ob2, H2, H, 16 * nt, 16);
@@ -137,11 +140,14 @@ __device__ __forceinline__ void adam_el(float *w, float *m, float *v, float *tgt
     if (sync) tgt[i] = wi;
 }
 
-template <int H>
+// XF: float replay rows (DMDQN_ROWS_F32): X(S') / X(S) are read as f32 from the
+// pre-gathered a.xn / a.xs (global, batch order) instead of the f16 LDS image.
+template <int H, bool XF>
 __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     using L = Lay<H>;
     __shared__ __attribute__((aligned(16))) char smem[L::LDS];
-    _Float16 *X = (_Float16 *)(smem + L::X_OFF);
+    _Float16 *XL = (_Float16 *)(smem + L::X_OFF);
+    using TX = typename std::conditional<XF, float, _Float16>::type;
     float *H1 = (float *)(smem + L::H1_OFF);
     float *H2 = (float *)(smem + L::H2_OFF);
     char *sc = smem + L::SC_OFF;
@@ -226,7 +232,7 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
             int b = t / (DP / 4), q = t - b * (DP / 4);
             const char4 c = reinterpret_cast<const char4 *>(
                 ring + ((size_t)agent * a.cap + S.slot[b]) * DMDQN_ROW_BYTES)[q];
-            _Float16 *dst = X + b * DP + 4 * q;
+            _Float16 *dst = XL + b * DP + 4 * q;
             dst[0] = (_Float16)(float)c.x;
             dst[1] = (_Float16)(float)c.y;
             dst[2] = (_Float16)(float)c.z;
@@ -234,7 +240,13 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
         }
         __syncthreads();
     };
-    gather(a.ring_n);
+    const TX *X;
+    if constexpr (XF) {
+        X = a.xn + (size_t)agent * B_ * DP;
+    } else {
+        gather(a.ring_n);
+        X = XL;
+    }
     // ---- P2: target forward on S' -> z3 ; P3: online forward on S' -> a*, y
     forward<H>(a.target + agent * P, X, H1, H2, S.z3);
     // online forward on S': layer 3 reads H2 only, so its Q goes to the H1 region
@@ -251,7 +263,12 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     }
     __syncthreads();
     // ---- P4/P5: gather S, online forward keeping H1, H2; q, loss, dq
-    gather(a.ring_s);
+    if constexpr (XF) {
+        X = a.xs + (size_t)agent * B_ * DP;
+    } else {
+        gather(a.ring_s);
+        X = XL;
+    }
     forward<H>(Wp, X, H1, H2, S.z3);
     if (a.qstats) learn_qstats(a.qstats, agent, S.z3, S.act);
     float lsum = 0.0f;
@@ -471,8 +488,11 @@ static int check_learn_args(const dmdqn_learn_args *a) {
     DMDQN_REQUIRE(a->NA > 0 && a->cap >= a->batch && a->start >= 0 && a->start < a->cap,
                   "dmdqn_learn: NA=%d cap=%d start=%d", a->NA, a->cap, a->start);
     DMDQN_REQUIRE(a->batch == B_, "dmdqn_learn: batch must be %d (got %d)", B_, a->batch);
-    DMDQN_REQUIRE(a->ring_s && a->ring_n && a->ring_a && a->ring_d && a->ring_r && a->idx &&
-                      a->params && a->adam_m && a->adam_v && a->target,
+    DMDQN_REQUIRE(a->row_format == DMDQN_ROWS_I8 || a->row_format == DMDQN_ROWS_F32,
+                  "dmdqn_learn: row_format %d", a->row_format);
+    DMDQN_REQUIRE((a->row_format == DMDQN_ROWS_F32 ? (a->xs && a->xn) : (a->ring_s && a->ring_n)) &&
+                      a->ring_a && a->ring_d && a->ring_r && a->idx && a->params && a->adam_m &&
+                      a->adam_v && a->target,
                   "dmdqn_learn: null pointer");
     DMDQN_REQUIRE(a->precision >= 0 && a->precision <= 2, "dmdqn_learn: precision %d",
                   a->precision);
@@ -485,12 +505,15 @@ extern "C" int dmdqn_learn(const dmdqn_learn_args *a, void *stream) {
     if (int rc = check_learn_args(a)) return rc;
     if (a->precision == 1) return launch_learn_f16(a, as_stream(stream));
     if (a->precision == 2) return launch_learn_bf16(a, as_stream(stream));
+    const bool xf = a->row_format == DMDQN_ROWS_F32;
     if (a->hidden == 128) {
         DMDQN_REQUIRE(a->P == Lay<128>::P, "dmdqn_learn: P=%d != %d", a->P, Lay<128>::P);
-        hipLaunchKernelGGL(k_learn_f32<128>, dim3(a->NA), dim3(512), 0, as_stream(stream), *a);
+        auto k = xf ? k_learn_f32<128, true> : k_learn_f32<128, false>;
+        hipLaunchKernelGGL(k, dim3(a->NA), dim3(512), 0, as_stream(stream), *a);
     } else if (a->hidden == 64) {
         DMDQN_REQUIRE(a->P == Lay<64>::P, "dmdqn_learn: P=%d != %d", a->P, Lay<64>::P);
-        hipLaunchKernelGGL(k_learn_f32<64>, dim3(a->NA), dim3(512), 0, as_stream(stream), *a);
+        auto k = xf ? k_learn_f32<64, true> : k_learn_f32<64, false>;
+        hipLaunchKernelGGL(k, dim3(a->NA), dim3(512), 0, as_stream(stream), *a);
     } else {
         DMDQN_REQUIRE(false, "dmdqn_learn: hidden must be 64 or 128 (got %d)", a->hidden);
     }

@@ -202,6 +202,7 @@ extern "C" size_t dmdqn_learn_shared_work_bytes(int NA) {
 extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, int n_slabs,
                                        float *grad, float scale, void *work, void *stream) {
     DMDQN_REQUIRE(a && slab && grad, "dmdqn_learn_shared_grad: null argument");
+    DMDQN_REQUIRE(a->row_format == DMDQN_ROWS_I8, "dmdqn_learn_shared_grad: int8 replay rows only");
     DMDQN_REQUIRE(a->NA > 0 && a->cap >= a->batch && a->start >= 0 && a->start < a->cap,
                   "dmdqn_learn_shared_grad: NA=%d cap=%d start=%d", a->NA, a->cap, a->start);
     DMDQN_REQUIRE(a->batch == f16k::B_, "dmdqn_learn_shared_grad: batch must be %d", f16k::B_);

@@ -614,7 +614,9 @@ __device__ __forceinline__ void adam1(float *W, float *M, float *V, float *T, si
 // shared-parameter kernel (k_learn_shared_f16).  All are called by every
 // thread of the 512-thread workgroup.
 
-struct Rows { uint2 v[3]; };
+template <bool XF> struct RowsT { uint2 v[3]; };        // int8 rows: 3 x 8 features per thread
+template <> struct RowsT<true> { float4 v[6]; };        // float rows: the same 24 features
+using Rows = RowsT<false>;
 
 
 // Replay rows (int8, DMDQN_ROW_BYTES = one 128-B line each) of one agent's
@@ -644,6 +646,48 @@ __device__ __forceinline__ void gather_commit(h16 *R2, const Rows &g) {
             hv[e + 4] = (h16)(float)(int8_t)(g.v[i].y >> (8 * e));
         }
         *reinterpret_cast<half8 *>(R2 + hoff<DP>(b, 8 * q)) = hv;
+    }
+}
+
+// X(S) / X(S') of either row format into an f16 [128][96] image: int8 ring rows
+// through the slots (gather_issue / gather_commit), or the float rows
+// pre-gathered in batch order (a.xs / a.xn, DMDQN_ROWS_F32) cast to 16 bits
+// as Keras' mixed policy casts the layer input.
+template <bool XF>
+__device__ __forceinline__ void gather_x(const dmdqn_learn_args &a, int agent, bool next,
+                                         const int *slot, RowsT<XF> &g) {
+    if constexpr (XF) {
+        const float *X = (next ? a.xn : a.xs) + (size_t)agent * B_ * DP;
+        const int tid = fresh_tid();
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
+            g.v[2 * i] = *reinterpret_cast<const float4 *>(X + b * DP + 8 * q);
+            g.v[2 * i + 1] = *reinterpret_cast<const float4 *>(X + b * DP + 8 * q + 4);
+        }
+    } else {
+        gather_issue(next ? a.ring_n : a.ring_s, a, agent, slot, g);
+    }
+}
+
+template <bool XF>
+__device__ __forceinline__ void commit_x(h16 *R, const RowsT<XF> &g) {
+    if constexpr (XF) {
+        const int tid = fresh_tid();
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int t = tid + 512 * i, b = t / 12, q = t - 12 * (t / 12);
+            const float *f0 = &g.v[2 * i].x, *f1 = &g.v[2 * i + 1].x;
+            half8 hv;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                hv[e] = (h16)f0[e];
+                hv[e + 4] = (h16)f1[e];
+            }
+            *reinterpret_cast<half8 *>(R + hoff<DP>(b, 8 * q)) = hv;
+        }
+    } else {
+        gather_commit(R, g);
     }
 }
 
@@ -730,16 +774,29 @@ __device__ __forceinline__ void zscore(const Scratch &S) {
 }
 
 // Slots, then the s' rows -> X(S') in R2 plus the metadata, then the z-score.
-// X(S') is visible to every thread on return (zscore's barriers).
+// X(S') is visible to every thread on return (zscore's barriers).  XF: float
+// rows, the metadata from the per-slot arrays.
+template <bool XF = false>
 __device__ __forceinline__ void batch_head(const dmdqn_learn_args &a, int agent, h16 *R2,
                                            const Scratch &S) {
     batch_slots(a, agent, S);
-    Rows gn;
-    Meta mt;
-    gather_issue(a.ring_n, a, agent, S.slot, gn);
-    meta_issue(a, agent, S.slot, mt);
-    gather_commit(R2, gn);
-    meta_commit(mt, S);
+    RowsT<XF> gn;
+    gather_x<XF>(a, agent, true, S.slot, gn);
+    if constexpr (XF) {
+        const int tid = threadIdx.x;
+        if (tid < B_) {
+            const size_t r = (size_t)agent * a.cap + S.slot[tid];
+            S.act[tid] = a.ring_a[r] < NACT ? a.ring_a[r] : 0;
+            S.dn[tid] = a.ring_d[r] ? 1.0f : 0.0f;
+            S.r64[tid] = a.ring_r[r];
+        }
+        commit_x<XF>(R2, gn);
+    } else {
+        Meta mt;
+        meta_issue(a, agent, S.slot, mt);
+        gather_commit(R2, gn);
+        meta_commit(mt, S);
+    }
     zscore(S);
     if (a.rn_out && threadIdx.x < B_) a.rn_out[(size_t)agent * B_ + threadIdx.x] = S.rn[threadIdx.x];
 }
@@ -914,7 +971,7 @@ __device__ __forceinline__ void bwd_dz1(h16 *R1, const uint32_t *mask, const f32
 // gradient entry goes to gout[agent][P] (the 16-bit value Adam would receive)
 // and dmdqn_adam_agents applies the identical Adam step in a second launch,
 // which can share the chip with the next step's side-stream work.
-template <bool QSTATS, bool SYNC, bool GOUT>
+template <bool QSTATS, bool SYNC, bool GOUT, bool XF = false>
 __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, float *gout) {
     LEARN_SMEM_SETUP;
     const int agent = blockIdx.x;
@@ -935,7 +992,7 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, f
     else stage_out(Tp, W3L + NACT * H, B3L + NACT);
 
     // ---- slots, X(S') + metadata from the s' rows, z-score
-    batch_head(a, agent, R2, S);
+    batch_head<XF>(a, agent, R2, S);
     STAMP(1);
     STAMP(2);
     // ---- target(S') -> z3 ; online(S') -> Q ; y
@@ -951,10 +1008,10 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, f
                     [Wpc](Frags &f) { load_w2(Wpc, f); });
     STAMP(3);
     float *qo = (float *)DQ;
-    Rows gs;
+    RowsT<XF> gs;
     forward_x<false>(fr, on, R2, R1, R2, qo,
-                     [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); }, NoHook{},
-                     [&]() { gather_commit(R1, gs); });
+                     [&](Frags &) { gather_x<XF>(a, agent, false, S.slot, gs); }, NoHook{},
+                     [&]() { commit_x<XF>(R1, gs); });
     STAMP(4);
     STAMP(5);
     ddqn_target(a, qo, S);
@@ -1056,18 +1113,18 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, f
     f32x4 d1[8];
 #if DMDQN_GX_EARLY
     {
-        Rows gx;  // X(S) again for dW1: issued before dH1, lands in P2 once dZ2 is consumed
-        gather_issue(a.ring_s, a, agent, S.slot, gx);
+        RowsT<XF> gx;  // X(S) again for dW1: issued before dH1, lands in P2 once dZ2 is consumed
+        gather_x<XF>(a, agent, false, S.slot, gx);
         __builtin_amdgcn_sched_barrier(0);
         bwd_dh1_from_image(P1, P2, d1);
-        gather_commit(P2, gx);
+        commit_x<XF>(P2, gx);
     }
 #else
     bwd_dh1_from_image(P1, P2, d1);
     {
-        Rows gx;  // X(S) again for dW1 (P2 is free)
-        gather_issue(a.ring_s, a, agent, S.slot, gx);
-        gather_commit(P2, gx);
+        RowsT<XF> gx;  // X(S) again for dW1 (P2 is free)
+        gather_x<XF>(a, agent, false, S.slot, gx);
+        commit_x<XF>(P2, gx);
     }
 #endif
     STAMP(10);
@@ -1157,6 +1214,11 @@ int H16_LAUNCH(const dmdqn_learn_args *a, hipStream_t s) {
                                             : H16_LEARN_KERNEL<true, false, false>)
                           : (a->sync_target ? H16_LEARN_KERNEL<false, true, false>
                                             : H16_LEARN_KERNEL<false, false, false>);
+    if (a->row_format == DMDQN_ROWS_F32)  // float rows (the drop-in surface): X from a.xs / a.xn
+        kern = a->qstats ? (a->sync_target ? H16_LEARN_KERNEL<true, true, false, true>
+                                           : H16_LEARN_KERNEL<true, false, false, true>)
+                         : (a->sync_target ? H16_LEARN_KERNEL<false, true, false, true>
+                                           : H16_LEARN_KERNEL<false, false, false, true>);
     hipLaunchKernelGGL(kern, dim3(a->NA), dim3(512), 0, s, *a, (float *)nullptr);
     DMDQN_LAUNCH_CHECK("k_learn_" H16_NAME);
     return DMDQN_OK;
@@ -1168,6 +1230,7 @@ int H16_LAUNCH_GRAD(const dmdqn_learn_args *a, float *grad, hipStream_t s) {
                   "dmdqn_learn_grad: precision %d (" H16_NAME ") needs hidden=128 (P=%d)",
                   a->precision, H16K::L::P);
     using namespace H16K;
+    DMDQN_REQUIRE(a->row_format == DMDQN_ROWS_I8, "dmdqn_learn_grad: int8 replay rows only");
     auto kern = a->qstats ? H16_LEARN_KERNEL<true, false, true> : H16_LEARN_KERNEL<false, false, true>;
     hipLaunchKernelGGL(kern, dim3(a->NA), dim3(512), 0, s, *a, grad);
     DMDQN_LAUNCH_CHECK("k_learn_" H16_NAME " (gradient)");

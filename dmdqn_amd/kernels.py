@@ -17,6 +17,7 @@ MT_WORDS = 625
 OBS_DIM = 89
 LOCAL_DIM = 17
 ROW_BYTES = 128  # include/dmdqn.h DMDQN_ROW_BYTES (s' rows carry a, done, r at 96/97/104)
+ROW_FLOATS = 96  # DMDQN_ROW_FLOATS: float rows (the drop-in surface)
 
 
 def _check(t, dtype, shape=None, name="tensor"):
@@ -87,13 +88,24 @@ class ReplayRing:
 
     Each agent keeps the last `cap` transitions; deque position p (0 = oldest)
     lives in ring slot (start + p) % cap.  All agents add in lockstep, so one
-    host-side counter describes every ring."""
+    host-side counter describes every ring.
 
-    def __init__(self, NA, cap, device="cuda"):
-        self.NA, self.cap = NA, cap
+    row_format "int8" (the batched path): 128-byte int8 rows, exact for this
+    environment's integer features, anything else raises.  "f32" (the
+    per-agent drop-in surface): float32 rows of ROW_FLOATS, every value kept
+    as the reference's buffer keeps it (dqn_agent.py:39-56)."""
+
+    def __init__(self, NA, cap, device="cuda", row_format="int8"):
+        if row_format not in ("int8", "f32"):
+            raise ValueError("row_format must be 'int8' or 'f32'")
+        self.NA, self.cap, self.row_format = NA, cap, row_format
         z = dict(device=device)
-        self.s = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
-        self.n = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
+        if row_format == "f32":
+            self.s = torch.zeros((NA, cap, ROW_FLOATS), dtype=torch.float32, **z)
+            self.n = torch.zeros((NA, cap, ROW_FLOATS), dtype=torch.float32, **z)
+        else:
+            self.s = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
+            self.n = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
         self.a = torch.zeros((NA, cap), dtype=torch.uint8, **z)
         self.r = torch.zeros((NA, cap), dtype=torch.float64, **z)
         self.d = torch.zeros((NA, cap), dtype=torch.uint8, **z)
@@ -123,13 +135,25 @@ class ReplayRing:
         _check(rew, torch.float64, (NA,), "rew")
         _check(done, torch.uint8, (NA,), "done")
         slot = self.total % self.cap
-        _ops().replay_store(slot, obs_s, obs_n, act, rew, done, self.s, self.n, self.a, self.r,
-                            self.d, self.err)
+        if self.row_format == "f32":
+            _ops().replay_store_f32(slot, obs_s, obs_n, act, rew, done, self.s, self.n, self.a,
+                                    self.r, self.d)
+        else:
+            _ops().replay_store(slot, obs_s, obs_n, act, rew, done, self.s, self.n, self.a,
+                                self.r, self.d, self.err)
         self.total += 1
+
+    def gather_f32(self, idx, xs, xn):
+        """Float rows: the batch of deque positions idx [NA, batch] -> xs / xn
+        [NA, batch, ROW_FLOATS] in batch order (the learn reads them there)."""
+        _ops().replay_gather_f32(self.s, self.n, idx, self.start, xs, xn)
 
     def check(self):
         """Raise if a stored value was not exactly representable (syncs the
-        current stream, behind every store issued on it)."""
+        current stream, behind every store issued on it).  Float rows hold any
+        value: nothing to check."""
+        if self.row_format == "f32":
+            return
         if self.err.is_pinned():
             torch.cuda.current_stream(self.device).synchronize()
         if int(self.err[0]) != 0:
@@ -147,6 +171,8 @@ class ReplayRing:
         Episode ends and checkpoint saves call check(), which waits.  The
         reference stores float32 rows (dqn_agent.py:39-56), and this build's
         int8 rows must never silently hold a rounded value."""
+        if self.row_format == "f32":
+            return
         if not self.err.is_pinned():  # a CPU-device ring: nothing in flight
             self.check()
             return

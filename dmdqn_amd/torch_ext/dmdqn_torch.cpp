@@ -153,6 +153,46 @@ void replay_store(int64_t slot, const Tensor &obs_s, const Tensor &obs_n, const 
           "dmdqn_replay_store");
 }
 
+void replay_store_f32(int64_t slot, const Tensor &obs_s, const Tensor &obs_n, const Tensor &act_,
+                      const Tensor &rew, const Tensor &done, Tensor &rows_s, Tensor &rows_n,
+                      Tensor &ring_a, Tensor &ring_r, Tensor &ring_d) {
+    const int64_t NA = act_.numel();
+    TORCH_CHECK(NA > 0 && ring_a.numel() % NA == 0, "ring_a must be [NA, cap]");
+    const int64_t cap = ring_a.numel() / NA;
+    auto s = dptr<float>(obs_s, at::kFloat, "obs_s", NA * DMDQN_OBS_DIM);
+    auto n = dptr<float>(obs_n, at::kFloat, "obs_n", NA * DMDQN_OBS_DIM);
+    auto a = dptr<int32_t>(act_, at::kInt, "act", NA);
+    auto r = dptr<double>(rew, at::kDouble, "rew", NA);
+    auto d = dptr<uint8_t>(done, at::kByte, "done", NA);
+    auto rs = dptr<float>(rows_s, at::kFloat, "rows_s", NA * cap * DMDQN_ROW_FLOATS);
+    auto rn = dptr<float>(rows_n, at::kFloat, "rows_n", NA * cap * DMDQN_ROW_FLOATS);
+    auto ra = dptr<uint8_t>(ring_a, at::kByte, "ring_a", NA * cap);
+    auto rr = dptr<double>(ring_r, at::kDouble, "ring_r", NA * cap);
+    auto rd = dptr<uint8_t>(ring_d, at::kByte, "ring_d", NA * cap);
+    c10::hip::HIPGuardMasqueradingAsCUDA g(obs_s.device());
+    check(dmdqn_replay_store_f32((int)NA, int32_of(cap, "cap"), int32_of(slot, "slot"), s, n, a, r,
+                                 d, rs, rn, ra, rr, rd, stream_of(obs_s)),
+          "dmdqn_replay_store_f32");
+}
+
+void replay_gather_f32(const Tensor &rows_s, const Tensor &rows_n, const Tensor &idx,
+                       int64_t start, Tensor &xs, Tensor &xn) {
+    TORCH_CHECK(idx.dim() == 2, "idx must be [NA, batch]");
+    const int64_t NA = idx.size(0), B = idx.size(1);
+    TORCH_CHECK(rows_s.dim() == 3 && rows_s.size(0) == NA && rows_s.size(2) == DMDQN_ROW_FLOATS,
+                "rows_s must be [NA, cap, ", DMDQN_ROW_FLOATS, "]");
+    const int64_t cap = rows_s.size(1);
+    auto rs = dptr<float>(rows_s, at::kFloat, "rows_s", NA * cap * DMDQN_ROW_FLOATS);
+    auto rn = dptr<float>(rows_n, at::kFloat, "rows_n", NA * cap * DMDQN_ROW_FLOATS);
+    auto ix = dptr<int32_t>(idx, at::kInt, "idx", NA * B);
+    auto ps = dptr<float>(xs, at::kFloat, "xs", NA * B * DMDQN_ROW_FLOATS);
+    auto pn = dptr<float>(xn, at::kFloat, "xn", NA * B * DMDQN_ROW_FLOATS);
+    c10::hip::HIPGuardMasqueradingAsCUDA g(rows_s.device());
+    check(dmdqn_replay_gather_f32(rs, rn, ix, (int)NA, int32_of(cap, "cap"), int32_of(start, "start"),
+                                  (int)B, ps, pn, stream_of(rows_s)),
+          "dmdqn_replay_gather_f32");
+}
+
 void replay_sample(Tensor &py_state, int64_t A, int64_t n, int64_t k, Tensor &idx) {
     const int64_t E = py_state.numel() / MT;
     auto s = dptr<uint32_t>(py_state, at::kInt, "py_state", E * MT);
@@ -235,7 +275,8 @@ dmdqn_learn_args make_learn(const Tensor &ring_s, const Tensor &ring_n, const Te
                             int64_t hidden, int64_t precision, bool sync, double gamma,
                             double alpha, double c1, double c2, double eps, int64_t loss_kind,
                             const OptT &qstats, const OptT &rn_out, const OptT &params_h,
-                            const OptT &stamps, int64_t NA, int64_t NW) {
+                            const OptT &stamps, int64_t NA, int64_t NW,
+                            const OptT &xs = std::nullopt, const OptT &xn = std::nullopt) {
     dmdqn_learn_args a{};
     TORCH_CHECK(NA > 0 && ring_a.numel() % NA == 0, "ring_a must be [NA, cap]");
     const int64_t cap = ring_a.numel() / NA, B = idx.numel() / NA;
@@ -244,8 +285,15 @@ dmdqn_learn_args make_learn(const Tensor &ring_s, const Tensor &ring_n, const Te
     a.NA = (int)NA; a.cap = int32_of(cap, "cap"); a.start = int32_of(start, "start");
     a.batch = (int)B; a.hidden = (int)hidden; a.precision = (int)precision;
     a.sync_target = sync ? 1 : 0; a.P = (int)P;
-    a.ring_s = dptr<int8_t>(ring_s, at::kChar, "ring_s", NA * cap * DMDQN_ROW_BYTES);
-    a.ring_n = dptr<int8_t>(ring_n, at::kChar, "ring_n", NA * cap * DMDQN_ROW_BYTES);
+    TORCH_CHECK(xs.has_value() == xn.has_value(), "xs and xn go together");
+    if (xs.has_value()) {  // float rows: the batch pre-gathered (replay_gather_f32)
+        a.row_format = DMDQN_ROWS_F32;
+        a.xs = dptr<float>(*xs, at::kFloat, "xs", NA * B * DMDQN_ROW_FLOATS);
+        a.xn = dptr<float>(*xn, at::kFloat, "xn", NA * B * DMDQN_ROW_FLOATS);
+    } else {
+        a.ring_s = dptr<int8_t>(ring_s, at::kChar, "ring_s", NA * cap * DMDQN_ROW_BYTES);
+        a.ring_n = dptr<int8_t>(ring_n, at::kChar, "ring_n", NA * cap * DMDQN_ROW_BYTES);
+    }
     a.ring_a = dptr<uint8_t>(ring_a, at::kByte, "ring_a", NA * cap);
     a.ring_d = dptr<uint8_t>(ring_d, at::kByte, "ring_d", NA * cap);
     a.ring_r = dptr<double>(ring_r, at::kDouble, "ring_r", NA * cap);
@@ -274,12 +322,13 @@ void learn_step(const Tensor &ring_s, const Tensor &ring_n, const Tensor &ring_a
                 Tensor &adam_m, Tensor &adam_v, Tensor &target, const OptT &target_h, Tensor &loss,
                 int64_t start, int64_t hidden, int64_t precision, bool sync, double gamma,
                 double alpha, double c1, double c2, double eps, int64_t loss_kind,
-                const OptT &qstats, const OptT &rn_out, const OptT &stamps, const OptT &grad) {
+                const OptT &qstats, const OptT &rn_out, const OptT &stamps, const OptT &grad,
+                const OptT &xs, const OptT &xn) {
     const int64_t NA = loss.numel();
     dmdqn_learn_args a = make_learn(ring_s, ring_n, ring_a, ring_d, ring_r, idx, params, adam_m,
                                     adam_v, target, target_h, loss, start, hidden, precision, sync,
                                     gamma, alpha, c1, c2, eps, loss_kind, qstats, rn_out,
-                                    std::nullopt, stamps, NA, NA);
+                                    std::nullopt, stamps, NA, NA, xs, xn);
     c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
     if (grad.has_value()) {  // the split learn: gradient launch, then the Adam launch
         auto gr = dptr<float>(*grad, at::kFloat, "grad", NA * (int64_t)a.P);
@@ -370,6 +419,10 @@ void observe_meta(int64_t, int64_t, const Tensor &, const Tensor &, const Tensor
 void replay_store_meta(int64_t, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                        const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &) {}
 void replay_sample_meta(Tensor &, int64_t, int64_t, int64_t, Tensor &) {}
+void replay_store_f32_meta(int64_t, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
+                           const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &) {}
+void replay_gather_f32_meta(const Tensor &, const Tensor &, const Tensor &, int64_t, Tensor &,
+                            Tensor &) {}
 void sim_reset_meta(at::TensorList, at::TensorList, at::IntArrayRef, const OptT &) {}
 void sim_step_meta(at::TensorList, at::TensorList, at::IntArrayRef, at::ArrayRef<double>,
                    const OptT &, int64_t, int64_t, int64_t, int64_t, Tensor &, Tensor &, Tensor &,
@@ -377,7 +430,8 @@ void sim_step_meta(at::TensorList, at::TensorList, at::IntArrayRef, at::ArrayRef
 void learn_step_meta(const Tensor &, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                      const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, const OptT &, Tensor &,
                      int64_t, int64_t, int64_t, bool, double, double, double, double, double,
-                     int64_t, const OptT &, const OptT &, const OptT &, const OptT &) {}
+                     int64_t, const OptT &, const OptT &, const OptT &, const OptT &, const OptT &,
+                     const OptT &) {}
 void learn_shared_grad_meta(const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, Tensor &, int64_t, double, int64_t,
@@ -409,6 +463,12 @@ TORCH_LIBRARY(dmdqn, m) {
           "Tensor(e!) ring_d, Tensor(f!) err) -> ()");
     // random.sample(self.buffer, k) (dqn_agent.py:63)
     m.def("replay_sample(Tensor(a!) py_state, int A, int n, int k, Tensor(b!) idx) -> ()");
+    // ReplayBuffer.add / .sample on float rows (the per-agent drop-in, dqn_agent.py:39-64)
+    m.def("replay_store_f32(int slot, Tensor obs_s, Tensor obs_n, Tensor act, Tensor rew, "
+          "Tensor done, Tensor(a!) rows_s, Tensor(b!) rows_n, Tensor(c!) ring_a, Tensor(d!) ring_r, "
+          "Tensor(e!) ring_d) -> ()");
+    m.def("replay_gather_f32(Tensor rows_s, Tensor rows_n, Tensor idx, int start, Tensor(a!) xs, "
+          "Tensor(b!) xn) -> ()");
     // traci.load (train.py:190); setPhase x A + simulationStep x K (train.py:225-236)
     m.def("sim_reset(Tensor(a!)[] state, Tensor[] tables, int[] dims, Tensor? mask=None) -> ()");
     m.def("sim_step(Tensor(a!)[] state, Tensor[] tables, int[] dims, float[] idm, Tensor? actions, "
@@ -419,7 +479,8 @@ TORCH_LIBRARY(dmdqn, m) {
           "Tensor idx, Tensor(a!) params, Tensor(b!) adam_m, Tensor(c!) adam_v, Tensor(d!) target, "
           "Tensor(e!)? target_h, Tensor(f!) loss, int start, int hidden, int precision, bool sync, "
           "float gamma, float alpha, float c1, float c2, float eps, int loss_kind, "
-          "Tensor(g!)? qstats, Tensor(h!)? rn_out, Tensor(i!)? stamps, Tensor(j!)? grad=None) -> ()");
+          "Tensor(g!)? qstats, Tensor(h!)? rn_out, Tensor(i!)? stamps, Tensor(j!)? grad=None, "
+          "Tensor? xs=None, Tensor? xn=None) -> ()");
     // C5: per-agent gradients of one shared net, summed
     m.def("learn_shared_grad(Tensor ring_s, Tensor ring_n, Tensor ring_a, Tensor ring_d, "
           "Tensor ring_r, Tensor idx, Tensor params, Tensor target, Tensor target_h, "
@@ -444,6 +505,8 @@ TORCH_LIBRARY_IMPL(dmdqn, CUDA, m) {
     m.impl("observe", &observe);
     m.impl("replay_store", &replay_store);
     m.impl("replay_sample", &replay_sample);
+    m.impl("replay_store_f32", &replay_store_f32);
+    m.impl("replay_gather_f32", &replay_gather_f32);
     m.impl("sim_reset", &sim_reset);
     m.impl("sim_step", &sim_step);
     m.impl("learn_step", &learn_step);
@@ -460,6 +523,8 @@ TORCH_LIBRARY_IMPL(dmdqn, Meta, m) {
     m.impl("observe", &observe_meta);
     m.impl("replay_store", &replay_store_meta);
     m.impl("replay_sample", &replay_sample_meta);
+    m.impl("replay_store_f32", &replay_store_f32_meta);
+    m.impl("replay_gather_f32", &replay_gather_f32_meta);
     m.impl("sim_reset", &sim_reset_meta);
     m.impl("sim_step", &sim_step_meta);
     m.impl("learn_step", &learn_step_meta);

@@ -43,6 +43,13 @@ extern "C" {
 #define DMDQN_ROW_A 96
 #define DMDQN_ROW_D 97
 #define DMDQN_ROW_R 104
+/* Float replay rows (the per-agent drop-in surface, any observation value, as
+ * ReplayBuffer.add stores it, dqn_agent.py:39-56): DMDQN_ROW_FLOATS f32 per
+ * row (features 0..88, zero to 95); a, done and r live in the per-slot arrays
+ * only.  dmdqn_learn_args.row_format selects them. */
+#define DMDQN_ROW_FLOATS 96
+#define DMDQN_ROWS_I8 0
+#define DMDQN_ROWS_F32 1
 
 const char *dmdqn_last_error(void);
 int dmdqn_version(void);
@@ -124,6 +131,22 @@ int dmdqn_replay_store(int NA, int cap, int slot, const float *obs_s,
                        const uint8_t *done, int8_t *ring_s, int8_t *ring_n,
                        uint8_t *ring_a, double *ring_r, uint8_t *ring_d,
                        int32_t *err, void *stream);
+
+/* dmdqn_replay_store for float rows (DMDQN_ROWS_F32): rows_s / rows_n f32
+ * [NA][cap][DMDQN_ROW_FLOATS], every value stored as given (the reference's
+ * float32 buffer, dqn_agent.py:39-56); ring_a / ring_r / ring_d as above. */
+int dmdqn_replay_store_f32(int NA, int cap, int slot, const float *obs_s, const float *obs_n,
+                           const int32_t *act, const double *rew, const uint8_t *done,
+                           float *rows_s, float *rows_n, uint8_t *ring_a, double *ring_r,
+                           uint8_t *ring_d, void *stream);
+
+/* The float-row learn's gather (ReplayBuffer.sample :63-64 on float rows):
+ * xs / xn f32 [NA][batch][DMDQN_ROW_FLOATS] <- the rows of deque positions
+ * idx [NA][batch] (slot = (start + pos) % cap), in batch order.  The learn
+ * kernels then read X(S) / X(S') from xs / xn (dmdqn_learn_args.xs / .xn). */
+int dmdqn_replay_gather_f32(const float *rows_s, const float *rows_n, const int32_t *idx,
+                            int NA, int cap, int start, int batch, float *xs, float *xn,
+                            void *stream);
 
 /* Replaces random.sample(self.buffer, k) (dqn_agent.py:63): per env, agents
  * j = 0..A-1 in order draw k deque positions (0 = oldest) from a deque of
@@ -263,6 +286,16 @@ typedef struct dmdqn_learn_args {
     float *rn_out;                   /* diagnostics: NULL, or [NA][batch] the
                                         z-scored rewards the learn used
                                         (ReplayBuffer.sample :66-69, f32)     */
+    int32_t row_format;              /* DMDQN_ROWS_I8 (0, default): ring_s /
+                                        ring_n int8 rows; DMDQN_ROWS_F32: the
+                                        batch's rows pre-gathered into xs / xn
+                                        (dmdqn_replay_gather_f32), a / done / r
+                                        from ring_a / ring_d / ring_r; the
+                                        16-bit kernels cast them to 16 bits as
+                                        Keras' mixed policy does, the fp32
+                                        kernel reads them as f32.  Independent
+                                        nets only (not the shared C5 learn).  */
+    const float *xs, *xn;            /* DMDQN_ROWS_F32: [NA][batch][DMDQN_ROW_FLOATS] */
 } dmdqn_learn_args;
 
 int dmdqn_learn(const dmdqn_learn_args *args, void *stream);

@@ -53,7 +53,9 @@ class ReplayBuffer:
 
     def __init__(self, buffer_size: int, device="cuda"):
         self.device = torch.device(device)
-        self.ring = K.ReplayRing(1, buffer_size, device=self.device)
+        # float32 rows: any observation value is kept as the reference's
+        # buffer keeps it (:39-56); the batched path uses int8 rows
+        self.ring = K.ReplayRing(1, buffer_size, device=self.device, row_format="f32")
 
     def add(self, experience: tuple):
         state, action, reward, next_state, done = experience
@@ -108,6 +110,9 @@ class DQNAgent:
         # seed is cfg.seed mixed with a hash of its id (TF's stream itself cannot
         # be reproduced)
         cfg.seed = init_seed(cfg.seed, agent_id)
+        # float32 replay rows (additive key "replay_rows": "int8" opts back into
+        # the batched path's exact-integer rows)
+        cfg.replay_rows = config.get("replay_rows", "f32")
         self._core = BatchedDQN(1, 1, cfg, device=self.device, streams=_streams(self.device))
         self.replay_buffer = ReplayBuffer.__new__(ReplayBuffer)
         self.replay_buffer.device, self.replay_buffer.ring = self.device, self._core.ring
@@ -128,7 +133,7 @@ class DQNAgent:
 
     def remember(self, state, action, reward, next_state, done):
         self.replay_buffer.add((state, action, reward, next_state, done))  # :312-326
-        self.replay_buffer.ring.check()  # per-call host path: a non-int8 value raises now
+        self.replay_buffer.ring.check()  # int8 rows (opt-in): a non-int8 value raises now
 
     def learn(self):
         """One fused learn step; None while the buffer is underfilled (:333-335)."""

@@ -98,3 +98,24 @@ def test_debug_build_exports_and_reports_its_variant():
         lib = ctypes.CDLL(os.path.join(build.LIBDIR, build.libname(variant)))
         assert lib.dmdqn_debug_build() == want
         assert hasattr(lib, "dmdqn_debug_status")
+
+
+def test_learn_args_layout_matches_header(tmp_path):
+    """agent.CLearn (the ctypes mirror the C-ABI tests pass) has the size and
+    field offsets gcc gives include/dmdqn.h's dmdqn_learn_args."""
+    import ctypes
+    import subprocess
+    from dmdqn_amd.agent import CLearn
+    fields = [f for f, _ in CLearn._fields_]
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dmdqn.h"\nint main(void){'
+                   'printf("%zu", sizeof(dmdqn_learn_args));' +
+                   "".join(f'printf(" %zu", offsetof(dmdqn_learn_args, {f}));' for f in fields) +
+                   "return 0;}\n")
+    exe = tmp_path / "lay"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", f"-I{inc}", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got[0] == ctypes.sizeof(CLearn)
+    assert got[1:] == [getattr(CLearn, f).offset for f in fields]

@@ -393,8 +393,10 @@ def test_remember_non_integer_observation_raises():
 
 
 def test_dropin_remember_raises_immediately():
+    """With the opt-in int8 rows (the drop-in default is float rows,
+    tests/test_gpu_float_rows.py)."""
     from src.agents import dqn_agent as DA
-    ag = DA.DQNAgent(89, 4, "J_0_0", {"replay_buffer_size": 50})
+    ag = DA.DQNAgent(89, 4, "J_0_0", {"replay_buffer_size": 50, "replay_rows": "int8"})
     s = np.zeros((1, 89), np.float32)
     ag.remember(s, 1, -3.0, s, False)
     s2 = s.copy()
