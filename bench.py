@@ -218,6 +218,9 @@ def main():
                          "and the learn stream on the rest (CU-masked HIP streams)")
     ap.add_argument("--cu-stride", action="store_true",
                     help="--cu-split picks every k-th CU instead of CUs 0..N-1")
+    ap.add_argument("--no-fuse", action="store_true",
+                    help="act / sim / observe / store as four launches instead of the fused "
+                         "env step (dmdqn_env_step; bit-identical, A/B)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo; only barrier + timing use it")
     args = ap.parse_args()
@@ -256,7 +259,7 @@ def main():
     agent_cfg = AgentConfig(precision=args.precision, seed=1000 if args.shared else 1000 + rank,
                             shared_params=args.shared)
     tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side,
-                 split_learn=args.split_learn)
+                 split_learn=args.split_learn, fused=not args.no_fuse)
     E, A = tr.env.E, tr.env.A
     NA = E * A
     prefill = agent_cfg.replay_buffer_size if args.prefill_steps is None else args.prefill_steps
@@ -382,7 +385,9 @@ def main():
                 "precision": args.precision,
                 "schedule": {"none": "one stream",
                              "sample": "replay draws on a side stream beside act/sim/observe/store",
-                             "full": "act/sim/observe/sample of step t+1 beside learn t"}[args.overlap],
+                             "full": "act/sim/observe/sample of step t+1 beside learn t"}[args.overlap]
+                            + ("; act + sim + observe + store fused in one launch per env"
+                               if tr.fused else ""),
             },
             "roofline": {
                 "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared else

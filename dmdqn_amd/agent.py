@@ -375,6 +375,13 @@ class BatchedDQN:
     def act(self, obs, eps=None):
         """obs f32 [E, A, 89] -> actions int32 [E, A] (device).  eps overrides the
         schedule (evaluation, test.py:84-87)."""
+        eps, greedy, out = self.act_inputs(obs, eps)
+        return K.act(self.np_state, self.A, eps=eps, n_actions=N_ACTIONS, greedy=greedy, out=out)
+
+    def act_inputs(self, obs, eps=None):
+        """What a fused env step (TrafficEnv.step_fused) needs to draw act()'s
+        actions itself: (eps, greedy or None, the actions buffer to fill).
+        The greedy forward (eps < 1) is launched here, as act() does."""
         eps = self.current_epsilon() if eps is None else float(eps)
         greedy = None
         if eps < 1.0:
@@ -383,8 +390,15 @@ class BatchedDQN:
                                self.shared)
             greedy = self.greedy
         self.actions = self._act_bufs[1] if self.actions is self._act_bufs[0] else self._act_bufs[0]
-        return K.act(self.np_state, self.A, eps=eps, n_actions=N_ACTIONS, greedy=greedy,
-                     out=self.actions)
+        return eps, greedy, self.actions
+
+    def remembered(self):
+        """The bookkeeping of remember() after a fused env step stored the
+        transition into ring slot ring.total % ring.cap."""
+        self.ring.advance()
+        self.ring.poll()
+        if self.cfg.count_env_steps:
+            self.global_step_count += 1
 
     # -------------------------------------------------------------- replay
     def remember(self, obs, actions, rewards, next_obs, done):

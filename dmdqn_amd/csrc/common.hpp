@@ -169,6 +169,27 @@ struct MTWave {
     }
 };
 
+// numpy legacy random_sample: ((u>>5) * 2^26 + (u>>6)) / 2^53 (exact in f64).
+__device__ __forceinline__ double np_double(MTWave &w) {
+    int32_t a = (int32_t)(w.next() >> 5);
+    int32_t b = (int32_t)(w.next() >> 6);
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+
+// An observation value as an exact int8 replay byte (ReplayBuffer.add's float32
+// row, dqn_agent.py:39-56, holds this env's small integers exactly); anything
+// else sets *err = DMDQN_ERANGE and stores 0.
+__device__ __forceinline__ int8_t to_i8(float v, int32_t *err) {
+    float r = rintf(v);
+    if (!(r == v) || r < -128.0f || r > 127.0f) {
+        // every writer stores the same code: a plain store (err may be pinned
+        // host memory, where device atomics are not available)
+        *reinterpret_cast<volatile int32_t *>(err) = DMDQN_ERANGE;
+        return 0;
+    }
+    return (int8_t)(int)r;
+}
+
 // Learn metrics of dqn_agent.py:361-363 for one agent's batch: sum and sum of
 // squares of the online Q(S) values [128][4] (q_values_mean / _std) and the
 // histogram of the batch actions (action_distribution), added into

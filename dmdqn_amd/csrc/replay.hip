@@ -16,17 +16,6 @@
 
 namespace dmdqn {
 
-__device__ __forceinline__ int8_t to_i8(float v, int32_t *err) {
-    float r = rintf(v);
-    if (!(r == v) || r < -128.0f || r > 127.0f) {
-        // every writer stores the same code: a plain store (err may be pinned
-        // host memory, where device atomics are not available)
-        *reinterpret_cast<volatile int32_t *>(err) = DMDQN_ERANGE;
-        return 0;
-    }
-    return (int8_t)(int)r;
-}
-
 // One thread per (agent, 4-byte group): 32 groups of 4 bytes per row.
 __global__ void k_replay_store(int NA, int cap, int slot, const float *obs_s, const float *obs_n,
                                const int32_t *act, const double *rew, const uint8_t *done,

@@ -76,13 +76,6 @@ __global__ void __launch_bounds__(64) k_draw_u32(uint32_t *state, int count, uin
 }
 
 // ------------------------------------------------------------------ act
-// numpy legacy random_sample: ((u>>5) * 2^26 + (u>>6)) / 2^53 (exact in f64).
-__device__ __forceinline__ double np_double(MTWave &w) {
-    int32_t a = (int32_t)(w.next() >> 5);
-    int32_t b = (int32_t)(w.next() >> 6);
-    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
-}
-
 // draw_rand 0: no rand() draw, every action is randint (test.py:92 random mode)
 __global__ void __launch_bounds__(64) k_act(uint32_t *np_state, int A, double eps, uint32_t rng,
                                             uint32_t mask, const int32_t *greedy,

@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "common.hpp"
+#include "observe.hpp"
 #include "sim.hpp"
 
 namespace dmdqn {
@@ -543,6 +544,144 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
     SIM_PROF(5);
 }
 
+// ================================================================ fused env step
+// dmdqn_env_step: the act draws before the substeps (prologue) and the
+// observation, reward and replay store after them (epilogue) run inside the
+// sim block, with the same arithmetic as k_act (rng.hip), k_observe
+// (observe.hip) and k_replay_store (replay.hip): bit-identical results, three
+// fewer launches per step, and the halting counts / signals / observation
+// read from LDS instead of passed between kernels through HBM.
+constexpr size_t kMtBytes = 2 * MT_N * sizeof(uint32_t);
+
+// loc f32 [A][17], act i32 [A], sums f64 [A + 1], rew f64 [A]
+__host__ __device__ inline size_t tail_bytes(int A) {
+    return (((size_t)A * 18 * 4 + 7) & ~(size_t)7) + (size_t)(2 * A + 1) * 8;
+}
+
+// Where the prologue's MT stream and the epilogue's scratch go in the dynamic
+// LDS of a block whose own layout takes `base` bytes: at offset 0 when the
+// block's first bytes are dead there (free_start: before staging, free_end:
+// after the write-back), else past `base`.
+struct FuseLayout {
+    size_t mt_off, tail_off, bytes;
+};
+__host__ __device__ inline FuseLayout fuse_layout(size_t base, size_t free_start, size_t free_end,
+                                                  int A) {
+    FuseLayout f;
+    const size_t extra = (base + 15) & ~(size_t)15;
+    f.bytes = base;
+    f.mt_off = free_start >= kMtBytes ? 0 : extra;
+    if (f.mt_off && extra + kMtBytes > f.bytes) f.bytes = extra + kMtBytes;
+    f.tail_off = free_end >= tail_bytes(A) ? 0 : extra;
+    if (f.tail_off && extra + tail_bytes(A) > f.bytes) f.bytes = extra + tail_bytes(A);
+    return f;
+}
+
+// select_action for the env's A agents (k_act with draw_rand): every thread of
+// the block consumes the stream in lockstep (the draws are wave-uniform; the
+// MTWave loops and barriers are correct for a block of several waves, whose
+// extra lanes write identical values); thread j returns agent j's action.
+__device__ int fused_act(const dmdqn_env_fuse &F, int A, uint32_t *mtbuf) {
+    const int e = blockIdx.x;
+    const uint32_t rng = (uint32_t)(F.n_actions - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    MTWave w{mtbuf, mtbuf + MT_N, 0};
+    uint32_t *g = F.np_state + (size_t)e * DMDQN_MT_WORDS;
+    w.load(g);
+    int mine = 0;
+    for (int j = 0; j < A; j++) {
+        const double r = np_double(w);
+        int a;
+        if (r < F.eps) {  // dqn_agent.py:263-265
+            uint32_t v;
+            do { v = w.next() & mask; } while (v > rng);
+            a = (int)v;
+        } else {
+            a = F.greedy[(size_t)e * A + j];
+        }
+        if ((int)threadIdx.x == j) mine = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) w.store(g);
+    if ((int)threadIdx.x < A) F.actions[(size_t)e * A + threadIdx.x] = mine;
+    __syncthreads();  // the stream's LDS may be reused from here on (the LDS image)
+    return mine;
+}
+
+// k_observe + k_replay_store of this env from LDS: s_halt [A][12], s_phase /
+// s_ts [A] (phase start times, tspent = t - ts); my_act is thread a's action.
+// Every thread calls it after a barrier that completed those arrays.
+__device__ void fused_tail(const dmdqn_env_fuse &F, int R, int C, int t, bool done_e, int my_act,
+                           const int32_t *s_halt, const int32_t *s_phase, const int32_t *s_ts,
+                           char *scratch) {
+    const int A = R * C, e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    float *loc = reinterpret_cast<float *>(scratch);
+    int32_t *act = reinterpret_cast<int32_t *>(loc + A * 17);
+    double *sums = reinterpret_cast<double *>(scratch + (((size_t)A * 18 * 4 + 7) & ~(size_t)7));
+    double *rew = sums + A + 1;
+    const size_t eo = (size_t)e * A;
+    if (tid < A) act[tid] = my_act;
+    for (int i = tid; i < A * 17; i += nt) {  // get_own_state (order_lanes.py:430-499)
+        const int a = i / 17, f = i - a * 17;
+        const float v = local_feature(f, s_halt + a * 12, s_phase[a], t - s_ts[a], F.mode);
+        loc[i] = v;
+        F.local[eo * 17 + i] = v;
+    }
+    const float *pl = F.prev_local + eo * 17;
+    for (int a = tid; a < A; a += nt) {
+        double s = 0.0;
+        for (int k = 0; k < 12; k++) s += (double)pl[a * 17 + k];
+        sums[a] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double g = 0.0;
+        for (int a = 0; a < A; a++) g += sums[a];
+        sums[A] = -1.0 * g;
+    }
+    for (int i = tid; i < A * 89; i += nt) {  // build_state_vector (:502-555)
+        const int a = i / 89, k = i - a * 89;
+        F.obs[eo * 89 + i] = obs_feature(R, C, a, k, loc);
+    }
+    __syncthreads();
+    for (int a = tid; a < A; a += nt) {  // train.py:159-165, :254
+        const double r = combine_reward(-1.0 * sums[a], sums[A]);
+        rew[a] = r;
+        F.reward[eo + a] = r;
+    }
+    __syncthreads();
+    // ReplayBuffer.add: one thread per (agent, 4-byte group), as k_replay_store
+    constexpr int G = DMDQN_ROW_BYTES / 4;
+    for (int i = tid; i < A * G; i += nt) {
+        const int a = i / G, grp = i - a * G;
+        const size_t row = (eo + a) * (size_t)F.cap + F.slot;
+        const float *os = F.obs_s + (eo + a) * DMDQN_OBS_DIM;
+        uint32_t ws = 0, wn = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int k = grp * 4 + q;
+            if (k < DMDQN_OBS_DIM) {
+                ws |= (uint32_t)(uint8_t)to_i8(os[k], F.err) << (8 * q);
+                wn |= (uint32_t)(uint8_t)to_i8(obs_feature(R, C, a, k, loc), F.err) << (8 * q);
+            }
+        }
+        if (4 * grp == DMDQN_ROW_A) {
+            wn = (uint32_t)(uint8_t)act[a] | (done_e ? 1u : 0u) << 8;
+        } else if (4 * grp == DMDQN_ROW_R || 4 * grp == DMDQN_ROW_R + 4) {
+            const unsigned long long rb = __double_as_longlong(rew[a]);
+            wn = (uint32_t)(4 * grp == DMDQN_ROW_R ? rb : rb >> 32);
+        }
+        reinterpret_cast<uint32_t *>(F.ring_s + row * DMDQN_ROW_BYTES)[grp] = ws;
+        reinterpret_cast<uint32_t *>(F.ring_n + row * DMDQN_ROW_BYTES)[grp] = wn;
+        if (grp == 0) {
+            F.ring_a[row] = (uint8_t)act[a];
+            F.ring_r[row] = rew[a];
+            F.ring_d[row] = done_e ? 1 : 0;
+        }
+    }
+}
+
 // LDS image of one env's mutable state (kLDS path): compacted lanes' first C1
 // positions as (x, v) f32 pairs [NL][C1], their u16 route words [NL][C1] and
 // pdst [NL], then head, cnt, req, gfrom, fx, fv, lastx, lastv [NL], phase, ts
@@ -561,11 +700,12 @@ __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
 // pass C walks each lane's vehicles front to back); only occupied positions
 // move between HBM and LDS, and the lanes are written back compacted (head 0).
 // !kLDS: the same passes on global memory rings.
-template <bool kLDS, bool kAct>
+template <bool kLDS, bool kAct, bool kFuse>
 __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions,
                                                   int stride, int t0_arg, int K, int max_time,
                                                   int32_t *halt, int32_t *phase_out,
-                                                  int32_t *tspent, uint8_t *done) {
+                                                  int32_t *tspent, uint8_t *done,
+                                                  dmdqn_env_fuse F) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     const int t0 = S.t_env ? S.t_env[blockIdx.x] : t0_arg;  // the replica's own clock
     const uint64_t prof_t0 = __builtin_amdgcn_s_memrealtime();
@@ -578,6 +718,14 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
     EnvViewT<typename std::conditional<kLDS, uint16_t, int32_t>::type> V(S, blockIdx.x);
     const int A = V.A, NL = V.NL, cap = V.cap;
     const int tid = threadIdx.x, nt = blockDim.x;
+    // fused step: the act draws first (the MT stream lives in the image's dead
+    // position slots until staging), the halting counts later in the topology
+    // tables' place (dead after the substeps)
+    const size_t xv_bytes = kLDS ? (size_t)NL * V.C1 * 8 : 0;
+    const FuseLayout fl = fuse_layout(topo_off + topo_bytes(S.R, S.C), xv_bytes, xv_bytes, A);
+    int32_t *const s_halt = reinterpret_cast<int32_t *>(dyn + topo_off);
+    int my_act = 0;
+    if constexpr (kFuse) my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off));
     if constexpr (kLDS) {
         const int C1 = V.C1;
         const size_t NS = (size_t)NL * C1;
@@ -653,7 +801,12 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         for (int e = tid; e < 4 * A; e += nt) V.qptr[e] = G.qptr[e];
         if (tid < 4) V.stats[tid] = G.stats[tid];
     }
-    if (actions) {
+    if constexpr (kFuse) {
+        if (tid < A) {  // A <= blockDim (dmdqn_env_step)
+            V.phase[tid] = stride * my_act;
+            V.ts[tid] = t0;
+        }
+    } else if (actions) {
         for (int a = tid; a < A; a += nt) {
             V.phase[a] = stride * actions[(size_t)blockIdx.x * A + a];
             V.ts[a] = t0;
@@ -693,6 +846,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
                 }
             }
             halt[(size_t)blockIdx.x * 12 * A + l] = h;
+            if constexpr (kFuse) s_halt[l] = h;
         }
     }
     for (int e = tid; e < 4 * A; e += nt) pend += V.q_off[e + 1] - V.qptr[e];
@@ -733,6 +887,11 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         for (int e = tid; e < 4 * A; e += nt) G.qptr[e] = V.qptr[e];
         if (S.actuated)
             for (int i = tid; i < 12 * A; i += nt) G.last_det[i] = V.last_det[i];
+    }
+    if constexpr (kFuse) {
+        __syncthreads();  // the write-back has read the image: its slots are scratch now
+        const bool done_e = t >= max_time || (s_running + s_pending) == 0;
+        fused_tail(F, S.R, S.C, t, done_e, my_act, s_halt, V.phase, V.ts, dyn + fl.tail_off);
     }
 #ifdef DMDQN_SIM_PROFILE
     __syncthreads();
@@ -778,10 +937,16 @@ __device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP]
     lv = vv;
 }
 
-template <int NT>
+__host__ __device__ inline size_t sim_reg_lds_bytes(int R, int C) {
+    const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
+    return (size_t)NL * 9 * 4 + (size_t)A * 8 + (size_t)A * 48 + 16 + topo_bytes(R, C);
+}
+
+template <int NT, bool kFuse>
 __global__ void __launch_bounds__(NT, NT <= 256 ? 2 : 1)
 k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, int t0_arg, int K,
-               int max_time, int32_t *halt, int32_t *phase_out, int32_t *tspent, uint8_t *done) {
+               int max_time, int32_t *halt, int32_t *phase_out, int32_t *tspent, uint8_t *done,
+               dmdqn_env_fuse F) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     const int t0 = S.t_env ? S.t_env[blockIdx.x] : t0_arg;  // the replica's own clock
     const IdmK P(Pa);
@@ -842,9 +1007,23 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         qend = G.q_off[tid + 1];
         if (qp < qend) { qid = G.q_ids[qp]; qdst = G.q_dst[qp]; }
     }
-    for (int a = tid; a < A; a += NT) {
-        s_phase[a] = actions ? stride * actions[(size_t)blockIdx.x * A + a] : G.phase[a];
-        s_ts[a] = actions ? t0 : G.ts[a];
+    // fused step: the MT stream past the block's own LDS; the halting counts
+    // later in the topology tables' place, the epilogue's scratch in the
+    // published-lane arrays (both dead by then)
+    const FuseLayout fl = fuse_layout(sim_reg_lds_bytes(S.R, S.C), 0, (size_t)NL * 9 * 4, A);
+    int32_t *const s_halt = s_stats + 4;
+    int my_act = 0;
+    if constexpr (kFuse) {
+        my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off));
+        if (tid < A) {  // A <= NT (dmdqn_env_step)
+            s_phase[tid] = stride * my_act;
+            s_ts[tid] = t0;
+        }
+    } else {
+        for (int a = tid; a < A; a += NT) {
+            s_phase[a] = actions ? stride * actions[(size_t)blockIdx.x * A + a] : G.phase[a];
+            s_ts[a] = actions ? t0 : G.ts[a];
+        }
     }
     if (S.actuated)
         for (int i = tid; i < 12 * A; i += NT) s_ldet[i] = G.last_det[i];
@@ -1102,6 +1281,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             for (int i = 0; i < nm; i++)
                 if (i < n) hc += V_[i] < P.halt_speed ? 1 : 0;
             halt[(size_t)blockIdx.x * 12 * A + l] = hc;
+            if constexpr (kFuse) s_halt[l] = hc;
         }
     }
     atomicAdd(&s_stats[2], run);
@@ -1140,11 +1320,10 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         done[blockIdx.x] = (t >= max_time || (s_stats[2] + s_stats[3]) == 0) ? 1 : 0;
         if (S.t_env) S.t_env[blockIdx.x] = t;
     }
-}
-
-__host__ inline size_t sim_reg_lds_bytes(int R, int C) {
-    const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
-    return (size_t)NL * 9 * 4 + (size_t)A * 8 + (size_t)A * 48 + 16 + topo_bytes(R, C);
+    if constexpr (kFuse) {
+        const bool done_e = t >= max_time || (s_stats[2] + s_stats[3]) == 0;
+        fused_tail(F, S.R, S.C, t, done_e, my_act, s_halt, s_phase, s_ts, dyn + fl.tail_off);
+    }
 }
 
 __global__ void k_sim_reset(dmdqn_sim S, const uint8_t *mask) {
@@ -1200,9 +1379,11 @@ extern "C" int dmdqn_sim_reset_envs(const dmdqn_sim *sim, const uint8_t *mask, v
     return DMDQN_OK;
 }
 
-extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *actions,
-                              int action_stride, int t0, int K, int max_time, int32_t *halt,
-                              int32_t *phase, int32_t *tspent, uint8_t *done, void *stream) {
+// One launcher for dmdqn_sim_step (F == nullptr) and dmdqn_env_step.
+static int launch_sim(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *actions,
+                      const dmdqn_env_fuse *F, int action_stride, int t0, int K, int max_time,
+                      int32_t *halt, int32_t *phase, int32_t *tspent, uint8_t *done,
+                      void *stream) {
     int rc = check_sim(sim);
     if (rc) return rc;
     DMDQN_REQUIRE(idm && halt && phase && tspent && done, "dmdqn_sim_step: null output");
@@ -1225,35 +1406,62 @@ extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const 
     if (force && !strcmp(force, "reg")) { use_reg = reg_ok; use_lds = !reg_ok && fits_lds; }
     if (force && !strcmp(force, "lds")) { use_reg = false; use_lds = fits_lds; }
     if (force && !strcmp(force, "global")) { use_reg = false; use_lds = false; }
+    const dmdqn_env_fuse f = F ? *F : dmdqn_env_fuse{};
     if (use_reg) {
-        const size_t rlds = sim_reg_lds_bytes(sim->R, sim->C);
-        if (NL <= 256)
-            hipLaunchKernelGGL(k_sim_step_reg<256>, dim3(sim->E), dim3(256), rlds, as_stream(stream),
-                               *sim, *idm, actions, action_stride, t0, K, max_time, halt, phase,
-                               tspent, done);
-        else if (NL <= 512)
-            hipLaunchKernelGGL(k_sim_step_reg<512>, dim3(sim->E), dim3(512), rlds, as_stream(stream),
-                               *sim, *idm, actions, action_stride, t0, K, max_time, halt, phase,
-                               tspent, done);
-        else
-            hipLaunchKernelGGL(k_sim_step_reg<1024>, dim3(sim->E), dim3(1024), rlds,
-                               as_stream(stream), *sim, *idm, actions, action_stride, t0, K,
-                               max_time, halt, phase, tspent, done);
+        const int nt = NL <= 256 ? 256 : NL <= 512 ? 512 : 1024;
+        size_t rlds = sim_reg_lds_bytes(sim->R, sim->C);
+        if (F) rlds = fuse_layout(rlds, 0, (size_t)NL * 9 * 4, A).bytes;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(sim->E), dim3(nt), rlds, as_stream(stream), *sim, *idm,
+                               actions, action_stride, t0, K, max_time, halt, phase, tspent, done,
+                               f);
+        };
+        if (nt == 256) F ? go(k_sim_step_reg<256, true>) : go(k_sim_step_reg<256, false>);
+        else if (nt == 512) F ? go(k_sim_step_reg<512, true>) : go(k_sim_step_reg<512, false>);
+        else F ? go(k_sim_step_reg<1024, true>) : go(k_sim_step_reg<1024, false>);
         DMDQN_LAUNCH_CHECK("k_sim_step_reg");
         return DMDQN_OK;
     }
     // kAct: the actuated-mode detector bookkeeping is compiled in only when used
-    auto launch = [&](auto kern, size_t bytes) {
+    const size_t base = use_lds ? lds + topo : topo;
+    const size_t xvb = use_lds ? (size_t)NL * (sim->cap_lane < kLdsPos ? sim->cap_lane : kLdsPos) * 8 : 0;
+    const size_t bytes = F ? fuse_layout(base, xvb, xvb, A).bytes : base;
+    DMDQN_REQUIRE(bytes <= 160 * 1024 - 64, "dmdqn_env_step: %zu bytes of LDS", bytes);
+    auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(sim->E), dim3(256), bytes, as_stream(stream), *sim, *idm,
-                           actions, action_stride, t0, K, max_time, halt, phase, tspent, done);
+                           actions, action_stride, t0, K, max_time, halt, phase, tspent, done, f);
     };
     if (use_lds) {
-        if (sim->actuated) launch(k_sim_step<true, true>, lds + topo);
-        else launch(k_sim_step<true, false>, lds + topo);
+        if (sim->actuated) F ? launch(k_sim_step<true, true, true>) : launch(k_sim_step<true, true, false>);
+        else F ? launch(k_sim_step<true, false, true>) : launch(k_sim_step<true, false, false>);
     } else {
-        if (sim->actuated) launch(k_sim_step<false, true>, topo);
-        else launch(k_sim_step<false, false>, topo);
+        if (sim->actuated) F ? launch(k_sim_step<false, true, true>) : launch(k_sim_step<false, true, false>);
+        else F ? launch(k_sim_step<false, false, true>) : launch(k_sim_step<false, false, false>);
     }
     DMDQN_LAUNCH_CHECK("k_sim_step");
     return DMDQN_OK;
+}
+
+extern "C" int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *actions,
+                              int action_stride, int t0, int K, int max_time, int32_t *halt,
+                              int32_t *phase, int32_t *tspent, uint8_t *done, void *stream) {
+    return launch_sim(sim, idm, actions, nullptr, action_stride, t0, K, max_time, halt, phase,
+                      tspent, done, stream);
+}
+
+extern "C" int dmdqn_env_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const dmdqn_env_fuse *F,
+                              int action_stride, int t0, int K, int max_time, int32_t *halt,
+                              int32_t *phase, int32_t *tspent, uint8_t *done, void *stream) {
+    DMDQN_REQUIRE(F, "dmdqn_env_step: null fuse");
+    DMDQN_REQUIRE(sim && sim->R * sim->C <= 100, "dmdqn_env_step: at most 100 junctions");
+    DMDQN_REQUIRE(F->np_state && F->actions && F->n_actions >= 1, "dmdqn_env_step: act arguments");
+    DMDQN_REQUIRE(F->greedy || F->eps >= 1.0, "dmdqn_env_step: greedy actions required when eps < 1");
+    DMDQN_REQUIRE(F->mode == 0 || F->mode == 1, "dmdqn_env_step: mode must be 0 or 1");
+    DMDQN_REQUIRE(F->local && F->obs && F->prev_local && F->reward, "dmdqn_env_step: observe arrays");
+    DMDQN_REQUIRE(F->obs_s && F->ring_s && F->ring_n && F->ring_a && F->ring_r && F->ring_d && F->err,
+                  "dmdqn_env_step: replay arrays");
+    DMDQN_REQUIRE(F->cap > 0 && F->slot >= 0 && F->slot < F->cap, "dmdqn_env_step: cap=%d slot=%d",
+                  F->cap, F->slot);
+    return launch_sim(sim, idm, nullptr, F, action_stride, t0, K, max_time, halt, phase, tspent,
+                      done, stream);
 }

@@ -205,10 +205,44 @@ class TrafficEnv:
                            self.halt, self.phase, self.tspent, self.done_u8)
         if self.sim_hook:
             self.sim_hook(False)
-        self.t += cfg.step_duration
         prev = self.local
-        self.local, self.obs, reward = K.observe(self.R, self.C, self.halt, self.phase,
-                                                 self.tspent, self.mode, prev_local=prev)
+        local, obs, reward = K.observe(self.R, self.C, self.halt, self.phase, self.tspent,
+                                       self.mode, prev_local=prev)
+        return self._finish_step(local, obs, reward)
+
+    def step_fused(self, np_state, eps, greedy, actions, ring, obs_s, n_actions=4):
+        """act + step + remember of one loop iteration in ONE launch per replica
+        (dmdqn_env_step, train.py:211-282 up to agent.replay()): select_action's
+        draws from np_state (eps; greedy [E,A] when eps < 1) into actions
+        [E,A], setPhase + K substeps, the observation / reward, and the
+        transition (obs_s, action, reward, obs', the replica's done flag) into
+        ring slot ring.total % ring.cap (int8 rows; the caller advances the
+        ring).  Bit-identical to act -> step -> ReplayRing.store; returns what
+        step() returns."""
+        if self.local is None:
+            raise RuntimeError("call reset() first")
+        if ring.row_format != "int8" or ring.NA != self.E * self.A:
+            raise ValueError("step_fused stores int8 rows of E*A agents")
+        cfg, E, A, dev = self.cfg, self.E, self.A, self.device
+        local = torch.empty((E, A, K.LOCAL_DIM), dtype=torch.float32, device=dev)
+        obs = torch.empty((E, A, K.OBS_DIM), dtype=torch.float32, device=dev)
+        reward = torch.empty((E, A), dtype=torch.float64, device=dev)
+        if self.sim_hook:
+            self.sim_hook(True)
+        self._ops.env_step(self._sim_state, self._sim_tables, self._sim_dims, self._idm,
+                           cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time,
+                           self.halt, self.phase, self.tspent, self.done_u8, np_state, greedy,
+                           actions, float(eps), int(n_actions), self.mode, local, obs, self.local,
+                           reward, obs_s, ring.total % ring.cap, ring.s, ring.n, ring.a, ring.r,
+                           ring.d, ring.err)
+        if self.sim_hook:
+            self.sim_hook(False)
+        return self._finish_step(local, obs, reward)
+
+    def _finish_step(self, local, obs, reward):
+        cfg = self.cfg
+        self.t += cfg.step_duration
+        self.local, self.obs = local, obs
         info = {"simulation_time": float(self.t), "done_flags": self.done_u8}
         if self.drains_early:
             # the reference rule per replica (done_u8, from the last substep):

@@ -141,6 +141,11 @@ class ReplayRing:
         else:
             _ops().replay_store(slot, obs_s, obs_n, act, rew, done, self.s, self.n, self.a,
                                 self.r, self.d, self.err)
+        self.advance()
+
+    def advance(self):
+        """One transition per agent was written at slot total % cap (store(),
+        or a fused env step, env.TrafficEnv.step_fused)."""
         self.total += 1
 
     def gather_f32(self, idx, xs, xn):

@@ -22,7 +22,7 @@ ENTRY_POINTS = {
     "dmdqn_observe": "observe",
     "dmdqn_replay_store": "replay_store", "dmdqn_replay_sample": "replay_sample",
     "dmdqn_sim_reset": "sim_reset", "dmdqn_sim_reset_envs": "sim_reset",
-    "dmdqn_sim_step": "sim_step", "dmdqn_learn": "learn_step",
+    "dmdqn_sim_step": "sim_step", "dmdqn_env_step": "env_step", "dmdqn_learn": "learn_step",
     "dmdqn_learn_grad": "learn_step", "dmdqn_adam_agents": "learn_step",
     "dmdqn_replay_store_f32": "replay_store_f32", "dmdqn_replay_gather_f32": "replay_gather_f32",
     "dmdqn_learn_shared_grad": "learn_shared_grad", "dmdqn_adam": "adam",

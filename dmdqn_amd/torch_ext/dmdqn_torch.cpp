@@ -267,6 +267,54 @@ void sim_step(at::TensorList state, at::TensorList tables, at::IntArrayRef dims,
           "dmdqn_sim_step");
 }
 
+// act + sim_step + observe + replay_store (int8 rows) in one launch per env.
+void env_step(at::TensorList state, at::TensorList tables, at::IntArrayRef dims,
+              at::ArrayRef<double> idm, int64_t stride, int64_t t0, int64_t K, int64_t max_time,
+              Tensor &halt, Tensor &phase, Tensor &tspent, Tensor &done, Tensor &np_state,
+              const OptT &greedy, Tensor &actions, double eps, int64_t n_actions, int64_t mode,
+              Tensor &local, Tensor &obs, const Tensor &prev_local, Tensor &reward,
+              const Tensor &obs_s, int64_t slot, Tensor &ring_s, Tensor &ring_n, Tensor &ring_a,
+              Tensor &ring_r, Tensor &ring_d, Tensor &err) {
+    dmdqn_sim s = make_sim(state, tables, dims);
+    TORCH_CHECK(idm.size() == 12, "idm: 12 constants (include/dmdqn.h dmdqn_idm order)");
+    dmdqn_idm p{(float)idm[0], (float)idm[1], (float)idm[2], (float)idm[3], (float)idm[4],
+                (float)idm[5], (float)idm[6], (float)idm[7], (float)idm[8], (float)idm[9],
+                (float)idm[10], (float)idm[11]};
+    const int64_t A = (int64_t)s.R * s.C, E = s.E, NA = E * A;
+    auto h = dptr<int32_t>(halt, at::kInt, "halt", E * A * 12);
+    auto ph = dptr<int32_t>(phase, at::kInt, "phase", E * A);
+    auto ts = dptr<int32_t>(tspent, at::kInt, "tspent", E * A);
+    auto d = dptr<uint8_t>(done, at::kByte, "done", E);
+    TORCH_CHECK(ring_a.numel() % NA == 0 && ring_a.numel() > 0, "ring_a must be [E*A, cap]");
+    const int64_t cap = ring_a.numel() / NA;
+    dmdqn_env_fuse f{};
+    f.np_state = dptr<uint32_t>(np_state, at::kInt, "np_state", E * MT);
+    f.greedy = optr<int32_t>(greedy, at::kInt, "greedy", NA);
+    f.actions = dptr<int32_t>(actions, at::kInt, "actions", NA);
+    f.eps = eps;
+    f.n_actions = int32_of(n_actions, "n_actions");
+    f.mode = (int)mode;
+    f.local = dptr<float>(local, at::kFloat, "local", NA * DMDQN_LOCAL_DIM);
+    f.obs = dptr<float>(obs, at::kFloat, "obs", NA * DMDQN_OBS_DIM);
+    f.prev_local = dptr<float>(prev_local, at::kFloat, "prev_local", NA * DMDQN_LOCAL_DIM);
+    f.reward = dptr<double>(reward, at::kDouble, "reward", NA);
+    f.obs_s = dptr<float>(obs_s, at::kFloat, "obs_s", NA * DMDQN_OBS_DIM);
+    f.cap = int32_of(cap, "cap");
+    f.slot = int32_of(slot, "slot");
+    f.ring_s = dptr<int8_t>(ring_s, at::kChar, "ring_s", NA * cap * DMDQN_ROW_BYTES);
+    f.ring_n = dptr<int8_t>(ring_n, at::kChar, "ring_n", NA * cap * DMDQN_ROW_BYTES);
+    f.ring_a = dptr<uint8_t>(ring_a, at::kByte, "ring_a", NA * cap);
+    f.ring_r = dptr<double>(ring_r, at::kDouble, "ring_r", NA * cap);
+    f.ring_d = dptr<uint8_t>(ring_d, at::kByte, "ring_d", NA * cap);
+    TORCH_CHECK(err.is_cuda() || err.is_pinned(), "err must be a device tensor or pinned host memory");
+    TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() == 1, "err must be one int32");
+    f.err = reinterpret_cast<int32_t *>(err.data_ptr());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(halt.device());
+    check(dmdqn_env_step(&s, &p, &f, (int)stride, int32_of(t0, "t0"), (int)K,
+                         int32_of(max_time, "max_time"), h, ph, ts, d, stream_of(halt)),
+          "dmdqn_env_step");
+}
+
 // ---------------------------------------------------------------- learn
 dmdqn_learn_args make_learn(const Tensor &ring_s, const Tensor &ring_n, const Tensor &ring_a,
                             const Tensor &ring_d, const Tensor &ring_r, const Tensor &idx,
@@ -427,6 +475,11 @@ void sim_reset_meta(at::TensorList, at::TensorList, at::IntArrayRef, const OptT 
 void sim_step_meta(at::TensorList, at::TensorList, at::IntArrayRef, at::ArrayRef<double>,
                    const OptT &, int64_t, int64_t, int64_t, int64_t, Tensor &, Tensor &, Tensor &,
                    Tensor &) {}
+void env_step_meta(at::TensorList, at::TensorList, at::IntArrayRef, at::ArrayRef<double>, int64_t,
+                   int64_t, int64_t, int64_t, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &,
+                   const OptT &, Tensor &, double, int64_t, int64_t, Tensor &, Tensor &,
+                   const Tensor &, Tensor &, const Tensor &, int64_t, Tensor &, Tensor &, Tensor &,
+                   Tensor &, Tensor &, Tensor &) {}
 void learn_step_meta(const Tensor &, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                      const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, const OptT &, Tensor &,
                      int64_t, int64_t, int64_t, bool, double, double, double, double, double,
@@ -474,6 +527,14 @@ TORCH_LIBRARY(dmdqn, m) {
     m.def("sim_step(Tensor(a!)[] state, Tensor[] tables, int[] dims, float[] idm, Tensor? actions, "
           "int stride, int t0, int K, int max_time, Tensor(b!) halt, Tensor(c!) phase, "
           "Tensor(d!) tspent, Tensor(e!) done) -> ()");
+    // the env side of one loop iteration in one launch: select_action, setPhase + K
+    // substeps, observation / reward, ReplayBuffer.add (train.py:211-282)
+    m.def("env_step(Tensor(a!)[] state, Tensor[] tables, int[] dims, float[] idm, int stride, "
+          "int t0, int K, int max_time, Tensor(b!) halt, Tensor(c!) phase, Tensor(d!) tspent, "
+          "Tensor(e!) done, Tensor(f!) np_state, Tensor? greedy, Tensor(g!) actions, float eps, "
+          "int n_actions, int mode, Tensor(h!) local, Tensor(i!) obs, Tensor prev_local, "
+          "Tensor(j!) reward, Tensor obs_s, int slot, Tensor(k!) ring_s, Tensor(l!) ring_n, "
+          "Tensor(m!) ring_a, Tensor(n!) ring_r, Tensor(o!) ring_d, Tensor(p!) err) -> ()");
     // DQNAgent.learn + the target sync (dqn_agent.py:328-387)
     m.def("learn_step(Tensor ring_s, Tensor ring_n, Tensor ring_a, Tensor ring_d, Tensor ring_r, "
           "Tensor idx, Tensor(a!) params, Tensor(b!) adam_m, Tensor(c!) adam_v, Tensor(d!) target, "
@@ -509,6 +570,7 @@ TORCH_LIBRARY_IMPL(dmdqn, CUDA, m) {
     m.impl("replay_gather_f32", &replay_gather_f32);
     m.impl("sim_reset", &sim_reset);
     m.impl("sim_step", &sim_step);
+    m.impl("env_step", &env_step);
     m.impl("learn_step", &learn_step);
     m.impl("learn_shared_grad", &learn_shared_grad);
     m.impl("adam", &adam);
@@ -527,6 +589,7 @@ TORCH_LIBRARY_IMPL(dmdqn, Meta, m) {
     m.impl("replay_gather_f32", &replay_gather_f32_meta);
     m.impl("sim_reset", &sim_reset_meta);
     m.impl("sim_step", &sim_step_meta);
+    m.impl("env_step", &env_step_meta);
     m.impl("learn_step", &learn_step_meta);
     m.impl("learn_shared_grad", &learn_shared_grad_meta);
     m.impl("adam", &adam_meta);

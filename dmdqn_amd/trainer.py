@@ -13,12 +13,15 @@ the learn.  Every schedule gives each kernel exactly the inputs of the
 sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
 
   "none"    (default) one stream: act, sim, observe, store, sample, learn.
+            With fused=True (default; int8 replay rows) act, sim, observe and
+            store are ONE launch per replica (dmdqn_env_step, bit-identical).
   "sample"  the replay draws of step t run on a side stream beside
             act/sim/observe/store of step t (all latency-bound, low occupancy);
             the side stream waits for learn t-1, so nothing shares the GPU
             with a learn.
               side:  [wait learn t-1] sample_t (ev_s)
               main:  act_t sim_t observe_t store_t [wait ev_s] learn_t
+            (fused: main runs env_step_t [wait ev_s] learn_t).
   "full"    step t+1's act -> sim -> observe -> sample run on the side stream
             while learn t runs; only remember (which overwrites ring slots
             learn t may read) waits for learn t.  A greedy act (epsilon < 1)
@@ -56,7 +59,7 @@ class StepStats:
 
 class Trainer:
     def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
-                 overlap="none", side_stream=None, split_learn=False):
+                 overlap="none", side_stream=None, split_learn=False, fused=True):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
         if overlap is True or overlap is False:
             overlap = "full" if overlap else "none"
@@ -79,6 +82,9 @@ class Trainer:
         # Adam and the step lost 3 % (3.01 vs 3.09 M steps/s).
         if split_learn:
             self.agent.set_split_learn(True)
+        # fused: act + env step + remember as one launch (TrafficEnv.step_fused)
+        # on the one-stream schedules; "full" splits them across its streams
+        self.fused = bool(fused) and overlap != "full" and self.agent.ring.row_format == "int8"
         self.obs = self.env.reset()
         self.episode = 0
         self.step_count = 0
@@ -104,13 +110,24 @@ class Trainer:
         if self.overlap == "sample":
             return self._step_side_sample(collect_stats)
         env, agent = self.env, self.agent
-        actions = agent.act(self.obs)                          # train.py:211-222
-        next_obs, reward, done, info = env.step(actions)       # train.py:225-270
-        agent.remember(self.obs, actions, reward, next_obs, info["done"])  # train.py:274-282
+        next_obs, reward, done, info = self._env_side()
         loss = agent.learn(collect_stats=collect_stats)
         self.last_loss, self.last_reward = loss, reward
         self.obs = self._after_step(done, next_obs, info)
         return StepStats(loss is not None, done)
+
+    def _env_side(self):
+        """act -> env step -> remember (train.py:211-282), fused or as three calls."""
+        env, agent = self.env, self.agent
+        if self.fused:
+            eps, greedy, out = agent.act_inputs(self.obs)
+            res = env.step_fused(agent.np_state, eps, greedy, out, agent.ring, self.obs)
+            agent.remembered()
+            return res
+        actions = agent.act(self.obs)                          # train.py:211-222
+        next_obs, reward, done, info = env.step(actions)       # train.py:225-270
+        agent.remember(self.obs, actions, reward, next_obs, info["done"])  # train.py:274-282
+        return next_obs, reward, done, info
 
     def _step_side_sample(self, collect_stats):
         env, agent, side = self.env, self.agent, self.side
@@ -125,9 +142,7 @@ class Trainer:
             if agent.presample(min(agent.ring.total + 1, agent.ring.cap)):
                 ev_s = torch.cuda.Event()
                 ev_s.record(side)
-        actions = agent.act(self.obs)                          # train.py:211-222
-        next_obs, reward, done, info = env.step(actions)       # train.py:225-270
-        agent.remember(self.obs, actions, reward, next_obs, info["done"])  # train.py:274-282
+        next_obs, reward, done, info = self._env_side()
         if ev_s is not None:
             main.wait_event(ev_s)
         loss = agent.learn(collect_stats=collect_stats)

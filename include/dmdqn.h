@@ -233,6 +233,42 @@ int dmdqn_sim_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t *ac
                    int action_stride, int t0, int K, int max_time, int32_t *halt,
                    int32_t *phase, int32_t *tspent, uint8_t *done, void *stream);
 
+/* The env side of one loop iteration in ONE launch (one block per env):
+ * select_action's draws, setPhase + K substeps, the observation / reward and
+ * ReplayBuffer.add -- train.py:211-282 up to agent.replay() -- with the same
+ * results as dmdqn_act, dmdqn_sim_step, dmdqn_observe and dmdqn_replay_store
+ * issued in that order (int8 rows), bit for bit.  The block keeps the halting
+ * counts, signals and observation in LDS between them instead of four kernels
+ * passing them through HBM (three fewer launches per step). */
+typedef struct dmdqn_env_fuse {
+    /* act (dmdqn_act): np_state [E][DMDQN_MT_WORDS]; greedy [E*A] (NULL when
+     * eps >= 1); actions [E*A] out */
+    uint32_t *np_state;
+    const int32_t *greedy;
+    int32_t *actions;
+    double eps;
+    int32_t n_actions;
+    /* observe (dmdqn_observe): mode 0 / 1; local [E][A][17], obs [E][A][89],
+     * reward [E][A] out; prev_local [E][A][17] the pre-step local state */
+    int32_t mode;
+    float *local, *obs;
+    const float *prev_local;
+    double *reward;
+    /* remember (dmdqn_replay_store, done = the step's done flag of the env):
+     * obs_s [E][A][89] the observation the act saw; rings of NA = E*A agents */
+    const float *obs_s;
+    int32_t cap, slot;
+    int8_t *ring_s, *ring_n;
+    uint8_t *ring_a;
+    double *ring_r;
+    uint8_t *ring_d;
+    int32_t *err;
+} dmdqn_env_fuse;
+
+int dmdqn_env_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const dmdqn_env_fuse *fuse,
+                   int action_stride, int t0, int K, int max_time, int32_t *halt,
+                   int32_t *phase, int32_t *tspent, uint8_t *done, void *stream);
+
 /* ------------------------------------------------------------------ learn
  * Replaces DQNAgent.learn (src/agents/dqn_agent.py:328-380) + the target sync
  * (:376-377, :382-387) for NA independent agents in ONE launch (one workgroup

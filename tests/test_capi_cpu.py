@@ -46,7 +46,8 @@ def test_python_bindings_cover_header(lib):
     host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy"}
     assert declared - host_only <= set(ops.ENTRY_POINTS), sorted(declared - host_only -
                                                                  set(ops.ENTRY_POINTS))
-    ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_reset_envs", "dmdqn_sim_step"}
+    ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_reset_envs", "dmdqn_sim_step",
+                              "dmdqn_env_step"}
     assert ctypes_only <= set(_lib.SIGNATURES), sorted(ctypes_only - set(_lib.SIGNATURES))
 
 
