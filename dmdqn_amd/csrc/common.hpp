@@ -176,6 +176,25 @@ __device__ __forceinline__ double np_double(MTWave &w) {
     return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
 }
 
+// select_action's draws without staging the stream, when every agent's draw
+// count is fixed: eps >= 1 (the reference's training path keeps epsilon at
+// 1.0, A-1) and a power-of-two action count (randint never redraws).  Then
+// rand() always passes (r < 1 <= eps) and agent j consumes the `per` words
+// per*j .. per*j + per-1 of the stream (per = 3: two for rand(), one for
+// randint; per = 1: randint alone, test.py:92-93) and its action is the last
+// one & mask: one load of the raw state per agent.  Valid while the A*per
+// words lie inside the current 624-word block (mti + A*per <= 624), i.e. no
+// twist is due; the caller checks act_fast_ok and writes the new position
+// mti + A*per after every thread has read the old one.
+__device__ __forceinline__ bool act_fast_ok(int mti, int A, int per, double eps, uint32_t rng,
+                                           uint32_t mask, int draw_rand) {
+    return (!draw_rand || eps >= 1.0) && rng == mask && mti + A * per <= MT_N;
+}
+__device__ __forceinline__ int32_t act_fast(const uint32_t *g, int mti, int j, int per,
+                                            uint32_t mask) {
+    return (int32_t)(mt_temper(g[mti + per * j + per - 1]) & mask);
+}
+
 // An observation value as an exact int8 replay byte (ReplayBuffer.add's float32
 // row, dqn_agent.py:39-56, holds this env's small integers exactly); anything
 // else sets *err = DMDQN_ERANGE and stores 0.

@@ -84,6 +84,13 @@ __global__ void __launch_bounds__(64) k_act(uint32_t *np_state, int A, double ep
     MTWave w{mt, tmp, 0};
     const int e = blockIdx.x;
     uint32_t *g = np_state + (size_t)e * DMDQN_MT_WORDS;
+    const int per = draw_rand ? 3 : 1, mti0 = (int)g[MT_N];
+    if (act_fast_ok(mti0, A, per, eps, rng, mask, draw_rand)) {  // one wave: reads before the write
+        for (int j = threadIdx.x; j < A; j += 64)
+            actions[(size_t)e * A + j] = act_fast(g, mti0, j, per, mask);
+        if (threadIdx.x == 0) g[MT_N] = (uint32_t)(mti0 + A * per);
+        return;
+    }
     w.load(g);
     for (int j = 0; j < A; j++) {
         const double r = draw_rand ? np_double(w) : 0.0;

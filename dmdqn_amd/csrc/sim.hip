@@ -553,9 +553,10 @@ __device__ __forceinline__ void substep(View &V, const Topo &T, const IdmK &P, i
 // read from LDS instead of passed between kernels through HBM.
 constexpr size_t kMtBytes = 2 * MT_N * sizeof(uint32_t);
 
-// loc f32 [A][17], act i32 [A], sums f64 [A + 1], rew f64 [A]
+// fused_tail's scratch: loc f32 [A][17], act i32 [A], nbr i32 [A][4], then
+// (16-byte aligned) the observation rows f32 [A][92] and sums f64 [A + 1]
 __host__ __device__ inline size_t tail_bytes(int A) {
-    return (((size_t)A * 18 * 4 + 7) & ~(size_t)7) + (size_t)(2 * A + 1) * 8;
+    return (((size_t)A * 22 * 4 + 15) & ~(size_t)15) + (size_t)A * 92 * 4 + (size_t)(A + 1) * 8;
 }
 
 // Where the prologue's MT stream and the epilogue's scratch go in the dynamic
@@ -581,13 +582,24 @@ __host__ __device__ inline FuseLayout fuse_layout(size_t base, size_t free_start
 // the block consumes the stream in lockstep (the draws are wave-uniform; the
 // MTWave loops and barriers are correct for a block of several waves, whose
 // extra lanes write identical values); thread j returns agent j's action.
-__device__ int fused_act(const dmdqn_env_fuse &F, int A, uint32_t *mtbuf) {
+// The fixed-count case (act_fast: the training path) reads each agent's word
+// straight from the raw state -- no LDS, no barrier -- and leaves the stream
+// position to fused_act_done; the general case stages the stream in mtbuf.
+__device__ int fused_act(const dmdqn_env_fuse &F, int A, uint32_t *mtbuf, bool &fast) {
     const int e = blockIdx.x;
     const uint32_t rng = (uint32_t)(F.n_actions - 1);
     uint32_t mask = rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
-    MTWave w{mtbuf, mtbuf + MT_N, 0};
     uint32_t *g = F.np_state + (size_t)e * DMDQN_MT_WORDS;
+    const int mti0 = (int)g[MT_N];
+    fast = act_fast_ok(mti0, A, 3, F.eps, rng, mask, 1);
+    if (fast) {
+        if ((int)threadIdx.x >= A) return 0;
+        const int a = act_fast(g, mti0, threadIdx.x, 3, mask);
+        F.actions[(size_t)e * A + threadIdx.x] = a;
+        return a;
+    }
+    MTWave w{mtbuf, mtbuf + MT_N, 0};
     w.load(g);
     int mine = 0;
     for (int j = 0; j < A; j++) {
@@ -609,30 +621,80 @@ __device__ int fused_act(const dmdqn_env_fuse &F, int A, uint32_t *mtbuf) {
     return mine;
 }
 
+// After a barrier that follows every thread's read of the old position.
+__device__ __forceinline__ void fused_act_done(const dmdqn_env_fuse &F, int A, bool fast) {
+    if (fast && threadIdx.x == 0) {
+        uint32_t *g = F.np_state + (size_t)blockIdx.x * DMDQN_MT_WORDS;
+        g[MT_N] = g[MT_N] + (uint32_t)(3 * A);
+    }
+}
+
+// The epilogue's inputs that do not depend on the substeps, loaded before
+// them (their latency hides behind the staging): the packed int8 s-row words
+// of this thread's first two (agent, 4-byte group) store slots, and the
+// reward's pre-step sum of agent `tid` (train.py:159-165).
+constexpr int kPreWords = 2;
+struct TailPre {
+    uint32_t ws[kPreWords];
+    double sum;
+};
+__device__ __forceinline__ uint32_t s_row_word(const dmdqn_env_fuse &F, size_t agent, int grp) {
+    const float *os = F.obs_s + agent * DMDQN_OBS_DIM;
+    uint32_t ws = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int k = grp * 4 + q;
+        if (k < DMDQN_OBS_DIM) ws |= (uint32_t)(uint8_t)to_i8(os[k], F.err) << (8 * q);
+    }
+    return ws;
+}
+__device__ TailPre fused_prefetch(const dmdqn_env_fuse &F, int A) {
+    constexpr int G = DMDQN_ROW_BYTES / 4;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const size_t eo = (size_t)blockIdx.x * A;
+    TailPre p;
+#pragma unroll
+    for (int it = 0; it < kPreWords; it++) {
+        const int i = tid + it * nt;
+        p.ws[it] = i < A * G ? s_row_word(F, eo + i / G, i % G) : 0u;
+    }
+    p.sum = 0.0;
+    if (tid < A) {
+        const float *pl = F.prev_local + (eo + tid) * 17;
+        for (int k = 0; k < 12; k++) p.sum += (double)pl[k];
+    }
+    return p;
+}
+
 // k_observe + k_replay_store of this env from LDS: s_halt [A][12], s_phase /
 // s_ts [A] (phase start times, tspent = t - ts); my_act is thread a's action.
-// Every thread calls it after a barrier that completed those arrays.
+// Every thread calls it after a barrier that completed those arrays.  The
+// observation rows are built once, into LDS (stride kObsLd: 16-byte aligned
+// rows) and HBM; the s'-row bytes are packed from the LDS rows.
+constexpr int kObsLd = 92;
+__host__ __device__ inline size_t tail_obs_off(int A) {
+    return (((size_t)A * (17 + 1 + 4) * 4 + 15) & ~(size_t)15);
+}
 __device__ void fused_tail(const dmdqn_env_fuse &F, int R, int C, int t, bool done_e, int my_act,
-                           const int32_t *s_halt, const int32_t *s_phase, const int32_t *s_ts,
-                           char *scratch) {
+                           const TailPre &pre, const int32_t *s_halt, const int32_t *s_phase,
+                           const int32_t *s_ts, char *scratch) {
     const int A = R * C, e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-    float *loc = reinterpret_cast<float *>(scratch);
-    int32_t *act = reinterpret_cast<int32_t *>(loc + A * 17);
-    double *sums = reinterpret_cast<double *>(scratch + (((size_t)A * 18 * 4 + 7) & ~(size_t)7));
-    double *rew = sums + A + 1;
+    float *loc = reinterpret_cast<float *>(scratch);          // [A][17]
+    int32_t *act = reinterpret_cast<int32_t *>(loc + A * 17);  // [A]
+    int32_t *nbr = act + A;                                   // [A][4]
+    float *img = reinterpret_cast<float *>(scratch + tail_obs_off(A));  // [A][kObsLd]
+    double *sums = reinterpret_cast<double *>(img + (size_t)A * kObsLd);  // [A + 1]
     const size_t eo = (size_t)e * A;
-    if (tid < A) act[tid] = my_act;
+    if (tid < A) {
+        act[tid] = my_act;
+        sums[tid] = pre.sum;
+    }
+    for (int i = tid; i < 4 * A; i += nt) nbr[i] = neighbor(R, C, i >> 2, i & 3);
     for (int i = tid; i < A * 17; i += nt) {  // get_own_state (order_lanes.py:430-499)
         const int a = i / 17, f = i - a * 17;
         const float v = local_feature(f, s_halt + a * 12, s_phase[a], t - s_ts[a], F.mode);
         loc[i] = v;
         F.local[eo * 17 + i] = v;
-    }
-    const float *pl = F.prev_local + eo * 17;
-    for (int a = tid; a < A; a += nt) {
-        double s = 0.0;
-        for (int k = 0; k < 12; k++) s += (double)pl[a * 17 + k];
-        sums[a] = s;
     }
     __syncthreads();
     if (tid == 0) {
@@ -640,44 +702,52 @@ __device__ void fused_tail(const dmdqn_env_fuse &F, int R, int C, int t, bool do
         for (int a = 0; a < A; a++) g += sums[a];
         sums[A] = -1.0 * g;
     }
-    for (int i = tid; i < A * 89; i += nt) {  // build_state_vector (:502-555)
-        const int a = i / 89, k = i - a * 89;
-        F.obs[eo * 89 + i] = obs_feature(R, C, a, k, loc);
+    for (int i = tid; i < A * DMDQN_OBS_DIM; i += nt) {  // build_state_vector (:502-555)
+        const int a = i / DMDQN_OBS_DIM, k = i - a * DMDQN_OBS_DIM;
+        float v;
+        if (k < 17) {
+            v = loc[a * 17 + k];
+        } else if (k < 21) {
+            v = nbr[a * 4 + k - 17] >= 0 ? 1.0f : 0.0f;
+        } else {
+            const int d = (k - 21) / 17, f = (k - 21) - d * 17, b = nbr[a * 4 + d];
+            v = b >= 0 ? loc[b * 17 + f] : -1.0f;
+        }
+        img[a * kObsLd + k] = v;
+        F.obs[eo * DMDQN_OBS_DIM + i] = v;
     }
+    if (tid < A)
+        for (int k = DMDQN_OBS_DIM; k < kObsLd; k++) img[tid * kObsLd + k] = 0.0f;
     __syncthreads();
-    for (int a = tid; a < A; a += nt) {  // train.py:159-165, :254
-        const double r = combine_reward(-1.0 * sums[a], sums[A]);
-        rew[a] = r;
-        F.reward[eo + a] = r;
-    }
-    __syncthreads();
-    // ReplayBuffer.add: one thread per (agent, 4-byte group), as k_replay_store
+    // ReplayBuffer.add: one thread per (agent, 4-byte group), as k_replay_store;
+    // the reward (train.py:159-165, :254) by the threads that store it
     constexpr int G = DMDQN_ROW_BYTES / 4;
-    for (int i = tid; i < A * G; i += nt) {
+    const double gsum = sums[A];
+    for (int it = 0, i = tid; i < A * G; it++, i += nt) {
         const int a = i / G, grp = i - a * G;
         const size_t row = (eo + a) * (size_t)F.cap + F.slot;
-        const float *os = F.obs_s + (eo + a) * DMDQN_OBS_DIM;
-        uint32_t ws = 0, wn = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int k = grp * 4 + q;
-            if (k < DMDQN_OBS_DIM) {
-                ws |= (uint32_t)(uint8_t)to_i8(os[k], F.err) << (8 * q);
-                wn |= (uint32_t)(uint8_t)to_i8(obs_feature(R, C, a, k, loc), F.err) << (8 * q);
-            }
+        const uint32_t ws = it < kPreWords ? pre.ws[it < kPreWords ? it : 0] : s_row_word(F, eo + a, grp);
+        uint32_t wn = 0;
+        if (4 * grp < DMDQN_OBS_DIM) {  // (row floats 89..91 are zero: bytes 89..95 stay 0)
+            const float4 o = *reinterpret_cast<const float4 *>(img + a * kObsLd + 4 * grp);
+            wn = (uint32_t)(uint8_t)to_i8(o.x, F.err) | (uint32_t)(uint8_t)to_i8(o.y, F.err) << 8 |
+                 (uint32_t)(uint8_t)to_i8(o.z, F.err) << 16 | (uint32_t)(uint8_t)to_i8(o.w, F.err) << 24;
         }
+        const bool rw = grp == 0 || 4 * grp == DMDQN_ROW_R || 4 * grp == DMDQN_ROW_R + 4;
+        const double r = rw ? combine_reward(-1.0 * sums[a], gsum) : 0.0;
         if (4 * grp == DMDQN_ROW_A) {
             wn = (uint32_t)(uint8_t)act[a] | (done_e ? 1u : 0u) << 8;
         } else if (4 * grp == DMDQN_ROW_R || 4 * grp == DMDQN_ROW_R + 4) {
-            const unsigned long long rb = __double_as_longlong(rew[a]);
+            const unsigned long long rb = __double_as_longlong(r);
             wn = (uint32_t)(4 * grp == DMDQN_ROW_R ? rb : rb >> 32);
         }
         reinterpret_cast<uint32_t *>(F.ring_s + row * DMDQN_ROW_BYTES)[grp] = ws;
         reinterpret_cast<uint32_t *>(F.ring_n + row * DMDQN_ROW_BYTES)[grp] = wn;
         if (grp == 0) {
             F.ring_a[row] = (uint8_t)act[a];
-            F.ring_r[row] = rew[a];
+            F.ring_r[row] = r;
             F.ring_d[row] = done_e ? 1 : 0;
+            F.reward[eo + a] = r;
         }
     }
 }
@@ -725,7 +795,12 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
     const FuseLayout fl = fuse_layout(topo_off + topo_bytes(S.R, S.C), xv_bytes, xv_bytes, A);
     int32_t *const s_halt = reinterpret_cast<int32_t *>(dyn + topo_off);
     int my_act = 0;
-    if constexpr (kFuse) my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off));
+    bool act_fast = false;
+    TailPre pre{};
+    if constexpr (kFuse) {
+        my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off), act_fast);
+        pre = fused_prefetch(F, A);
+    }
     if constexpr (kLDS) {
         const int C1 = V.C1;
         const size_t NS = (size_t)NL * C1;
@@ -813,6 +888,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         }
     }
     __syncthreads();
+    if constexpr (kFuse) fused_act_done(F, A, act_fast);
     QNext qn[QSLOTS];
 #pragma unroll
     for (int q = 0; q < QSLOTS; q++) {
@@ -891,7 +967,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
     if constexpr (kFuse) {
         __syncthreads();  // the write-back has read the image: its slots are scratch now
         const bool done_e = t >= max_time || (s_running + s_pending) == 0;
-        fused_tail(F, S.R, S.C, t, done_e, my_act, s_halt, V.phase, V.ts, dyn + fl.tail_off);
+        fused_tail(F, S.R, S.C, t, done_e, my_act, pre, s_halt, V.phase, V.ts, dyn + fl.tail_off);
     }
 #ifdef DMDQN_SIM_PROFILE
     __syncthreads();
@@ -1013,8 +1089,11 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     const FuseLayout fl = fuse_layout(sim_reg_lds_bytes(S.R, S.C), 0, (size_t)NL * 9 * 4, A);
     int32_t *const s_halt = s_stats + 4;
     int my_act = 0;
+    bool act_fast = false;
+    TailPre pre{};
     if constexpr (kFuse) {
-        my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off));
+        my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off), act_fast);
+        pre = fused_prefetch(F, A);
         if (tid < A) {  // A <= NT (dmdqn_env_step)
             s_phase[tid] = stride * my_act;
             s_ts[tid] = t0;
@@ -1030,6 +1109,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     if (tid < 2) s_stats[tid] = G.stats[tid];
     if (tid == 2 || tid == 3) s_stats[tid] = 0;
     __syncthreads();
+    if constexpr (kFuse) fused_act_done(F, A, act_fast);
     const float len = own ? lane_length(T, e) : 0.0f;
 
     // TL at time t: natural phase advance (and the actuated gap-out of phase 0)
@@ -1322,7 +1402,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     }
     if constexpr (kFuse) {
         const bool done_e = t >= max_time || (s_stats[2] + s_stats[3]) == 0;
-        fused_tail(F, S.R, S.C, t, done_e, my_act, s_halt, s_phase, s_ts, dyn + fl.tail_off);
+        fused_tail(F, S.R, S.C, t, done_e, my_act, pre, s_halt, s_phase, s_ts, dyn + fl.tail_off);
     }
 }
 
