@@ -229,42 +229,52 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
         uint32_t *first = bm + words;
         const uint32_t tmask = (1u << tlog) - 1u;
         for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
-        for (uint32_t t = l; t <= tmask; t += 64) first[t] = 0xffffffffu;
+        for (uint32_t t = l; t <= tmask + 1u; t += 64) first[t] = 0xffffffffu;
         __syncthreads();
         // Two words per lane per iteration (a 128-word chunk, word q = 64h + l):
-        // half the dependent rounds of LDS traffic per drawn index.
+        // half the dependent rounds of LDS traffic per drawn index.  Every LDS
+        // access is issued unconditionally (lanes with nothing to do address
+        // the dummy table entry first[T] or OR 0 into bm[0]): one wave's LDS
+        // operations complete in issue order, so each group of reads costs one
+        // wait and no exec-mask branches.
         constexpr int HW = 2;
+        const uint32_t dummy = tmask + 1u;
         int j = 0, i = 0;
+        int32_t *out = idx + (size_t)e * A * k;  // agent j's i-th pick
         while (j < A) {
             if (w.mti >= MT_N) w.refill();
             const int cnt = min(64 * HW, MT_N - w.mti);
-            uint32_t r[HW], slot[HW], key[HW];
-            bool cand[HW], dup[HW], pend[HW];
+            uint32_t r[HW], slot[HW], key[HW], bw[HW];
+            bool inr[HW], cand[HW], dup[HW], pend[HW];
 #pragma unroll
             for (int h = 0; h < HW; h++) {
                 const int q = 64 * h + l;
-                const bool live = q < cnt;
-                r[h] = getbits(tmp[w.mti + (live ? q : 0)], kb);
-                cand[h] = live && r[h] < n;
-                if (cand[h]) cand[h] = !((bm[r[h] >> 5] >> (r[h] & 31)) & 1u);
-                slot[h] = r[h] & tmask;
-                key[h] = ((r[h] >> tlog) << 7) | (uint32_t)q;
+                r[h] = getbits(tmp[w.mti + (q < cnt ? q : 0)], kb);
+                inr[h] = q < cnt && r[h] < n;
+            }
+#pragma unroll
+            for (int h = 0; h < HW; h++) bw[h] = bm[inr[h] ? r[h] >> 5 : 0u];
+#pragma unroll
+            for (int h = 0; h < HW; h++) {
+                cand[h] = inr[h] && !((bw[h] >> (r[h] & 31)) & 1u);
+                slot[h] = cand[h] ? (r[h] & tmask) : dummy;
+                key[h] = cand[h] ? (((r[h] >> tlog) << 7) | (uint32_t)(64 * h + l)) : 0xffffffffu;
                 dup[h] = false;
                 pend[h] = cand[h];
             }
-            // a repeat of an earlier candidate word in the same chunk is rejected.
-            // One wave: its LDS operations complete in issue order, so the reads
-            // see every word's min and the resets follow every read.
+            // a repeat of an earlier candidate word in the same chunk is rejected:
+            // the reads see every word's min, the resets follow every read
             while (__ballot(pend[0] || pend[1])) {
+                uint32_t win[HW], sl[HW];
 #pragma unroll
-                for (int h = 0; h < HW; h++)
-                    if (pend[h]) atomicMin(&first[slot[h]], key[h]);
-                uint32_t win[HW];
+                for (int h = 0; h < HW; h++) {
+                    sl[h] = pend[h] ? slot[h] : dummy;
+                    atomicMin(&first[sl[h]], pend[h] ? key[h] : 0xffffffffu);
+                }
 #pragma unroll
-                for (int h = 0; h < HW; h++) win[h] = pend[h] ? first[slot[h]] : 0u;
+                for (int h = 0; h < HW; h++) win[h] = first[sl[h]];
 #pragma unroll
-                for (int h = 0; h < HW; h++)
-                    if (pend[h]) first[slot[h]] = 0xffffffffu;
+                for (int h = 0; h < HW; h++) first[sl[h]] = 0xffffffffu;
 #pragma unroll
                 for (int h = 0; h < HW; h++) {
                     const bool mine = pend[h] && (win[h] >> 7) == (key[h] >> 7);  // same r
@@ -286,21 +296,19 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
                     consumed = 64 + __ffsll((unsigned long long)__ballot(a1 && c1 == need - 1));
                 }
             }
-            if (a0 && c0 < taken) {
-                DMDQN_DBG(r[0] < n, DBG_SAMPLE);
-                idx[((size_t)e * A + j) * k + i + c0] = (int32_t)r[0];
-                atomicOr(&bm[r[0] >> 5], 1u << (r[0] & 31));
-            }
-            if (a1 && c1 < taken) {
-                DMDQN_DBG(r[1] < n, DBG_SAMPLE);
-                idx[((size_t)e * A + j) * k + i + c1] = (int32_t)r[1];
-                atomicOr(&bm[r[1] >> 5], 1u << (r[1] & 31));
-            }
+            const bool t0 = a0 && c0 < taken, t1 = a1 && c1 < taken;
+            DMDQN_DBG(!t0 || r[0] < n, DBG_SAMPLE);
+            DMDQN_DBG(!t1 || r[1] < n, DBG_SAMPLE);
+            if (t0) out[i + c0] = (int32_t)r[0];
+            if (t1) out[i + c1] = (int32_t)r[1];
+            atomicOr(&bm[t0 ? r[0] >> 5 : 0u], t0 ? 1u << (r[0] & 31) : 0u);
+            atomicOr(&bm[t1 ? r[1] >> 5 : 0u], t1 ? 1u << (r[1] & 31) : 0u);
             w.mti += consumed;
             i += taken;
             if (i == k) {
                 j++;
                 i = 0;
+                out += k;
                 for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
             }
             __syncthreads();
@@ -381,11 +389,11 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
     int tlog = 0;
     if (!pool) {
         const size_t quad = 39 * 1024;
-        const size_t room = (quad >= lds + 4096) ? quad - lds : 32 * 1024;
+        const size_t room = (quad >= lds + 4096 + 4) ? quad - lds - 4 : 32 * 1024;
         while (tlog < 20 && ((size_t)4 << (tlog + 1)) <= room && (1u << tlog) < (uint32_t)n) tlog++;
         const char *cap = getenv("DMDQN_SAMPLE_TLOG");
         if (cap && atoi(cap) >= 0 && atoi(cap) < tlog) tlog = atoi(cap);
-        lds += (size_t)4 << tlog;
+        lds += ((size_t)4 << tlog) + 4;  // + the dummy entry first[T]
     }
     DMDQN_REQUIRE(lds <= 160 * 1024, "dmdqn_replay_sample: n=%d too large for LDS", n);
     hipLaunchKernelGGL(k_sample, dim3(E), dim3(64), lds, as_stream(stream), py_state, A,
