@@ -318,6 +318,108 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
     w.store(g);
 }
 
+// Set branch with NW waves on one env stream (dmdqn_replay_sample picks it
+// for n > setsize): each iteration decides a chunk of 64*NW consecutive
+// words -- one per thread -- instead of 128 per wave, so an agent's ~210
+// words (n = 10000: acceptance n / 2^14) usually take one iteration instead
+// of two, and the per-word instruction stream is spread over NW SIMDs (one
+// wave on one stream is issue-bound: ~250 instructions per 128 words).  Same
+// decisions as k_sample's set branch word for word: out-of-range and
+// already-selected words (LDS bitmap) are rejected, a repeat within the chunk
+// is rejected by the first-lane table (block-wide: atomicMin, barrier, read,
+// barrier, reset), positions come from the block prefix of the accepted
+// flags, and the agent whose k-th pick falls inside the chunk consumes it up
+// to that word.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int A, uint32_t n, int k,
+                                                       int tlog, int32_t *idx) {
+    constexpr int NT = 64 * NW;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ int s_cnt[NW];
+    __shared__ int s_cons;
+    uint32_t *mt = smem, *tmp = smem + MT_N, *bm = smem + 2 * MT_N;
+    const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
+    uint32_t *first = bm + words;  // [T + 1]: entry T is the dummy
+    const uint32_t tmask = (1u << tlog) - 1u, dummy = tmask + 1u;
+    const int tid = threadIdx.x, wv = tid >> 6, e = blockIdx.x;
+    uint32_t *g = py_state + (size_t)e * DMDQN_MT_WORDS;
+    for (int t = tid; t < MT_N; t += NT) mt[t] = g[t];
+    int mti = (int)g[MT_N];
+    __syncthreads();
+    for (int t = tid; t < MT_N; t += NT) tmp[t] = mt_temper(mt[t]);
+    for (uint32_t t = tid; t < words; t += NT) bm[t] = 0u;
+    for (uint32_t t = tid; t <= dummy; t += NT) first[t] = 0xffffffffu;
+    __syncthreads();
+    int j = 0, i = 0;
+    int32_t *out = idx + (size_t)e * A * k;  // agent j's i-th pick
+    while (j < A) {
+        if (mti >= MT_N) {  // block-uniform
+            mt_twist_wave(mt);  // every lane of every wave: identical duplicate writes
+            for (int t = tid; t < MT_N; t += NT) tmp[t] = mt_temper(mt[t]);
+            __syncthreads();
+            mti = 0;
+        }
+        const int cnt = min(NT, MT_N - mti);
+        const bool live = tid < cnt;
+        const uint32_t r = getbits(tmp[mti + (live ? tid : 0)], kb);
+        const bool inr = live && r < n;
+        const uint32_t bw = bm[inr ? r >> 5 : 0u];
+        const bool cand = inr && !((bw >> (r & 31)) & 1u);
+        const uint32_t slot = cand ? (r & tmask) : dummy;
+        const uint32_t key = cand ? (((r >> tlog) << 9) | (uint32_t)tid) : 0xffffffffu;
+        bool pend = cand, dup = false;
+        while (__syncthreads_or(pend)) {
+            const uint32_t sl = pend ? slot : dummy;
+            atomicMin(&first[sl], pend ? key : 0xffffffffu);
+            __syncthreads();
+            const uint32_t win = first[sl];
+            __syncthreads();
+            first[sl] = 0xffffffffu;
+            const bool mine = pend && (win >> 9) == (key >> 9);  // same r
+            if (mine) dup = win != key;
+            pend = pend && !mine;
+        }
+        const bool acc = cand && !dup;
+        const uint64_t b = __ballot(acc);
+        if ((tid & 63) == 0) s_cnt[wv] = __popcll(b);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < NW; w2++) {
+            const int c2 = s_cnt[w2];
+            before += w2 < wv ? c2 : 0;
+            total += c2;
+        }
+        const int ln = tid & 63;
+        const uint64_t below = ln ? (~0ull >> (64 - ln)) : 0ull;
+        const int c = before + __popcll(b & below), need = k - i;
+        int taken = total, consumed = cnt;
+        if (total >= need) {  // block-uniform
+            taken = need;
+            if (acc && c == need - 1) s_cons = tid + 1;
+            __syncthreads();
+            consumed = s_cons;
+        }
+        if (acc && c < taken) {
+            DMDQN_DBG(r < n, DBG_SAMPLE);
+            out[i + c] = (int32_t)r;
+            atomicOr(&bm[r >> 5], 1u << (r & 31));
+        }
+        mti += consumed;
+        i += taken;
+        if (i == k) {
+            j++;
+            i = 0;
+            out += k;
+            __syncthreads();  // every OR of this chunk is in before the clear
+            for (uint32_t t = tid; t < words; t += NT) bm[t] = 0u;
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < MT_N; t += NT) g[t] = mt[t];
+    if (tid == 0) g[MT_N] = (uint32_t)mti;
+}
+
 DMDQN_DBG_READER(dbg_flags_rng)
 
 }  // namespace dmdqn
@@ -396,6 +498,15 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
         lds += ((size_t)4 << tlog) + 4;  // + the dummy entry first[T]
     }
     DMDQN_REQUIRE(lds <= 160 * 1024, "dmdqn_replay_sample: n=%d too large for LDS", n);
+    // set branch: four waves per stream (k_sample_set); DMDQN_SAMPLE_WAVES=1
+    // keeps the one-wave kernel (A/B)
+    const char *sw = getenv("DMDQN_SAMPLE_WAVES");
+    if (!pool && !(sw && atoi(sw) == 1)) {
+        hipLaunchKernelGGL(k_sample_set<4>, dim3(E), dim3(256), lds, as_stream(stream), py_state, A,
+                           (uint32_t)n, k, tlog, idx);
+        DMDQN_LAUNCH_CHECK("k_sample_set");
+        return DMDQN_OK;
+    }
     hipLaunchKernelGGL(k_sample, dim3(E), dim3(64), lds, as_stream(stream), py_state, A,
                        (uint32_t)n, k, setsize, tlog, idx);
     DMDQN_LAUNCH_CHECK("k_sample");
