@@ -675,6 +675,7 @@ constexpr int kObsLd = 92;
 __host__ __device__ inline size_t tail_obs_off(int A) {
     return (((size_t)A * (17 + 1 + 4) * 4 + 15) & ~(size_t)15);
 }
+template <bool kPre = true>
 __device__ void fused_tail(const dmdqn_env_fuse &F, int R, int C, int t, bool done_e, int my_act,
                            const TailPre &pre, const int32_t *s_halt, const int32_t *s_phase,
                            const int32_t *s_ts, char *scratch) {
@@ -687,7 +688,14 @@ __device__ void fused_tail(const dmdqn_env_fuse &F, int R, int C, int t, bool do
     const size_t eo = (size_t)e * A;
     if (tid < A) {
         act[tid] = my_act;
-        sums[tid] = pre.sum;
+        if constexpr (kPre) {
+            sums[tid] = pre.sum;
+        } else {
+            const float *pl = F.prev_local + (eo + tid) * 17;
+            double sm = 0.0;
+            for (int q = 0; q < 12; q++) sm += (double)pl[q];
+            sums[tid] = sm;
+        }
     }
     for (int i = tid; i < 4 * A; i += nt) nbr[i] = neighbor(R, C, i >> 2, i & 3);
     for (int i = tid; i < A * 17; i += nt) {  // get_own_state (order_lanes.py:430-499)
@@ -726,7 +734,8 @@ __device__ void fused_tail(const dmdqn_env_fuse &F, int R, int C, int t, bool do
     for (int it = 0, i = tid; i < A * G; it++, i += nt) {
         const int a = i / G, grp = i - a * G;
         const size_t row = (eo + a) * (size_t)F.cap + F.slot;
-        const uint32_t ws = it < kPreWords ? pre.ws[it < kPreWords ? it : 0] : s_row_word(F, eo + a, grp);
+        const uint32_t ws = kPre && it < kPreWords ? pre.ws[it < kPreWords ? it : 0]
+                                                   : s_row_word(F, eo + a, grp);
         uint32_t wn = 0;
         if (4 * grp < DMDQN_OBS_DIM) {  // (row floats 89..91 are zero: bytes 89..95 stay 0)
             const float4 o = *reinterpret_cast<const float4 *>(img + a * kObsLd + 4 * grp);
@@ -997,17 +1006,55 @@ __device__ __forceinline__ int wave_max_uniform(int x) {
     return __builtin_amdgcn_readfirstlane(x);
 }
 
+// A lane's vehicle speeds.  In registers for blocks of up to 512 threads.
+// A 1024-thread block (8x8: 128 VGPRs per thread) cannot hold three RCAP
+// arrays, and the compiler then demotes one dynamically indexed array to
+// scratch memory (every access a vector-memory round trip; ~130 MB of scratch
+// write-back per C5 launch): there the speeds live in an LDS column
+// [RCAP][NT] (thread-contiguous, conflict-free) as a ring from head h, so a
+// pop moves the head instead of 23 values.
+struct VColL {
+    float *p;  // this thread's column, stride nt
+    int h, nt;
+    __device__ __forceinline__ float &at(int i) const {
+        const int s = h + i;
+        return p[(s >= RCAP ? s - RCAP : s) * nt];
+    }
+};
+// V_ accessors: the register array, or (kL) the LDS column
+template <bool kL>
+__device__ __forceinline__ float vget(const float (&V_)[RCAP], const VColL &c, int i) {
+    if constexpr (kL) return c.at(i);
+    else return V_[i];
+}
+template <bool kL>
+__device__ __forceinline__ void vset(float (&V_)[RCAP], const VColL &c, int i, float x) {
+    if constexpr (kL) c.at(i) = x;
+    else V_[i] = x;
+}
+template <bool kL>
+__device__ __forceinline__ void vpop(float (&V_)[RCAP], VColL &c) {
+    if constexpr (kL) {
+        c.h = c.h + 1 == RCAP ? 0 : c.h + 1;
+    } else {
+#pragma unroll
+        for (int i = 0; i < RCAP - 1; i++) V_[i] = V_[i + 1];
+    }
+}
+
 // append a vehicle at the back of a register lane (constant indices only)
-__device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP], int (&D_)[RCAP],
-                                            int &n, float &lx, float &lv, float xv, float vv,
-                                            int dv) {
+template <bool kL>
+__device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP], const VColL &c,
+                                            int (&D_)[RCAP], int &n, float &lx, float &lv, float xv,
+                                            float vv, int dv) {
 #pragma unroll
     for (int i = 0; i < RCAP; i++) {
         const bool here = i == n;
         X_[i] = here ? xv : X_[i];
-        V_[i] = here ? vv : V_[i];
+        if constexpr (!kL) V_[i] = here ? vv : V_[i];
         D_[i] = here ? dv : D_[i];
     }
+    if constexpr (kL) c.at(n) = vv;
     n++;
     lx = xv;
     lv = vv;
@@ -1016,6 +1063,15 @@ __device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP]
 __host__ __device__ inline size_t sim_reg_lds_bytes(int R, int C) {
     const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
     return (size_t)NL * 9 * 4 + (size_t)A * 8 + (size_t)A * 48 + 16 + topo_bytes(R, C);
+}
+
+// Offset of the speed columns (1024-thread blocks) past the block's own LDS
+// (and the fused step's MT stream / epilogue scratch).
+__host__ __device__ inline size_t reg_vcol_off(int R, int C, bool fused) {
+    const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
+    size_t b = sim_reg_lds_bytes(R, C);
+    if (fused) b = fuse_layout(b, 0, (size_t)NL * 9 * 4, A).bytes;
+    return (b + 15) & ~(size_t)15;
 }
 
 template <int NT, bool kFuse>
@@ -1043,7 +1099,10 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     // ---- this thread's lane (registers) and origin queue
     const bool own = tid < NL;
     const int l = tid, e = tid / 3, kf = tid - 3 * (tid / 3);
+    constexpr bool kL = NT > 512;  // speeds in the LDS column (VColL)
     float X_[RCAP], V_[RCAP];
+    VColL Vc{nullptr, 0, NT};
+    if constexpr (kL) Vc.p = reinterpret_cast<float *>(dyn + reg_vcol_off(S.R, S.C, kFuse)) + tid;
     int D_[RCAP];
     int n = 0;
     float lx = 0.0f, lv = 0.0f;
@@ -1060,7 +1119,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 int sl = h + i;
                 if (sl >= cap) sl -= cap;
                 X_[i] = G.x[base + sl];
-                V_[i] = G.v[base + sl];
+                vset<kL>(V_, Vc, i, G.v[base + sl]);
                 D_[i] = G.dst[base + sl];
             }
         }
@@ -1093,7 +1152,8 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     TailPre pre{};
     if constexpr (kFuse) {
         my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off), act_fast);
-        pre = fused_prefetch(F, A);
+        // (1024-thread blocks have no VGPRs to hold the prefetch across the substeps)
+        if constexpr (!kL) pre = fused_prefetch(F, A);
         if (tid < A) {  // A <= NT (dmdqn_env_step)
             s_phase[tid] = stride * my_act;
             s_ts[tid] = t0;
@@ -1140,7 +1200,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             const int d_ = s_ins[l];                                    \
             if (d_ != -1) {                                             \
                 DMDQN_DBG(n < RCAP, DBG_SIM_RING);                      \
-                lane_append(X_, V_, D_, n, lx, lv, P.length, 0.0f, d_); \
+                lane_append<kL>(X_, V_, Vc, D_, n, lx, lv, P.length, 0.0f, d_); \
                 s_ins[l] = -1;                                          \
             }                                                           \
         }                                                               \
@@ -1155,7 +1215,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         int rq = -1;
         float fx = 0.0f, fv = 0.0f;
         if (own && n > 0) {
-            const float x0 = X_[0], v0 = V_[0];
+            const float x0 = X_[0], v0 = vget<kL>(V_, Vc, 0);
             const int d0 = D_[0];
             float acc;
             if (e >= 4 * A || on_final_edge(d0, e)) {  // exit edge or last edge: free road
@@ -1233,7 +1293,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         {
             const int nm = wave_max_uniform(own ? n : 0);
             if (own && n > 0) {
-                const float lead_x_old0 = X_[0], lead_v_old0 = V_[0];
+                const float lead_x_old0 = X_[0], lead_v_old0 = vget<kL>(V_, Vc, 0);
                 float lead_x_new = fx, fvn = fv;
                 bool pop = false;
                 if (rq == kArrive) {
@@ -1250,15 +1310,15 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 }
                 if (!pop) {
                     X_[0] = lead_x_new;
-                    V_[0] = fvn;
+                    vset<kL>(V_, Vc, 0, fvn);
                 }
                 const float dp = len - P.det_dist, dpl = dp + P.length;
                 bool det = lead_x_new >= dp && lead_x_old0 < dpl;
                 float lead_x_old = lead_x_old0, lead_v_old = lead_v_old0;
-                float last_x = X_[0], last_v = V_[0];
+                float last_x = X_[0], last_v = vget<kL>(V_, Vc, 0);
                 for (int i = 1; i < nm; i++) {
                     if (i < n) {
-                        const float xi = X_[i], vi = V_[i];
+                        const float xi = X_[i], vi = vget<kL>(V_, Vc, i);
                         const float gap = (lead_x_old - P.length) - xi;
                         const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
                         float vn = clamp_speed(vi + acc, P);
@@ -1274,7 +1334,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                             }
                         }
                         X_[i] = xn;
-                        V_[i] = vn;
+                        vset<kL>(V_, Vc, i, vn);
                         det = det || (xn >= dp && xi < dpl);
                         lead_x_old = xi;
                         lead_v_old = vi;
@@ -1287,9 +1347,9 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
 #pragma unroll
                     for (int i = 0; i < RCAP - 1; i++) {
                         X_[i] = X_[i + 1];
-                        V_[i] = V_[i + 1];
                         D_[i] = D_[i + 1];
                     }
+                    vpop<kL>(V_, Vc);
                     n--;
                 }
                 lx = last_x;
@@ -1316,7 +1376,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 }
                 if (xe < 0.0f) xe = 0.0f;
                 DMDQN_DBG(n < cap && n < RCAP, DBG_SIM_RING);  // pass B granted only with room
-                lane_append(X_, V_, D_, n, lx, lv, xe, vin, dv);
+                lane_append<kL>(X_, V_, Vc, D_, n, lx, lv, xe, vin, dv);
                 s_cnt[l] = n;
                 s_lx[l] = lx;
                 s_lv[l] = lv;
@@ -1359,7 +1419,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         if (own && l < 12 * A) {
             int hc = 0;
             for (int i = 0; i < nm; i++)
-                if (i < n) hc += V_[i] < P.halt_speed ? 1 : 0;
+                if (i < n) hc += vget<kL>(V_, Vc, i) < P.halt_speed ? 1 : 0;
             halt[(size_t)blockIdx.x * 12 * A + l] = hc;
             if constexpr (kFuse) s_halt[l] = hc;
         }
@@ -1384,7 +1444,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             for (int i = 0; i < nm; i++) {
                 if (i < n) {
                     G.x[base + i] = X_[i];
-                    G.v[base + i] = V_[i];
+                    G.v[base + i] = vget<kL>(V_, Vc, i);
                     G.dst[base + i] = D_[i];
                 }
             }
@@ -1402,7 +1462,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     }
     if constexpr (kFuse) {
         const bool done_e = t >= max_time || (s_stats[2] + s_stats[3]) == 0;
-        fused_tail(F, S.R, S.C, t, done_e, my_act, pre, s_halt, s_phase, s_ts, dyn + fl.tail_off);
+        fused_tail<!kL>(F, S.R, S.C, t, done_e, my_act, pre, s_halt, s_phase, s_ts, dyn + fl.tail_off);
     }
 }
 
@@ -1491,6 +1551,8 @@ static int launch_sim(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t 
         const int nt = NL <= 256 ? 256 : NL <= 512 ? 512 : 1024;
         size_t rlds = sim_reg_lds_bytes(sim->R, sim->C);
         if (F) rlds = fuse_layout(rlds, 0, (size_t)NL * 9 * 4, A).bytes;
+        if (nt > 512) rlds = reg_vcol_off(sim->R, sim->C, F != nullptr) + (size_t)RCAP * nt * 4;
+        DMDQN_REQUIRE(rlds <= 160 * 1024, "dmdqn_sim_step: register path needs %zu bytes of LDS", rlds);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(sim->E), dim3(nt), rlds, as_stream(stream), *sim, *idm,
                                actions, action_stride, t0, K, max_time, halt, phase, tspent, done,
