@@ -479,8 +479,11 @@ __device__ __forceinline__ f32x4 fwd_tile_pipe(const Net &N, const half8 bx[3], 
 #ifndef NEXT_NT
 #define NEXT_NT 2  // 16-row tiles per weight read in k_shared_next
 #endif
+#ifndef NEXT_WAVES
+#define NEXT_WAVES 8  // waves (agents in flight) per k_shared_next workgroup
+#endif
 constexpr int NEXT_WAVE_BYTES = B_ * 8 + B_ * 4 + B_ * 4;
-constexpr int NEXT_LDS = 2 * NET_BYTES + 8 * NEXT_WAVE_BYTES;
+constexpr int NEXT_LDS = 2 * NET_BYTES + NEXT_WAVES * NEXT_WAVE_BYTES;
 static_assert(NEXT_LDS <= 160 * 1024, "k_shared_next LDS");
 
 __device__ __forceinline__ int ring_slot(const dmdqn_learn_args &a, int pos) {
@@ -492,7 +495,7 @@ __device__ __forceinline__ int ring_slot(const dmdqn_learn_args &a, int pos) {
 // reads run ahead: the next agent's deque positions while this agent runs,
 // this agent's row metadata (a, done, r) in one burst at its start, and each
 // tile's X(S') one tile ahead.
-__global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, float *y_out,
+__global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_args a, float *y_out,
                                                         uint8_t *act_out) {
     __shared__ __attribute__((aligned(16))) char smem[NEXT_LDS];
     stage_net(reinterpret_cast<const h16 *>(a.params_h), smem);
@@ -504,8 +507,8 @@ __global__ void __launch_bounds__(512, 1) k_shared_next(dmdqn_learn_args a, floa
     double *r64 = reinterpret_cast<double *>(wsc);
     int *slots = reinterpret_cast<int *>(wsc + B_ * 8);
     uint32_t *tw = reinterpret_cast<uint32_t *>(wsc + B_ * 12);
-    const int stride = gridDim.x * 8;
-    int agent = blockIdx.x * 8 + w;
+    const int stride = gridDim.x * NEXT_WAVES;
+    int agent = blockIdx.x * NEXT_WAVES + w;
     constexpr int RT = 16 * NEXT_NT;
     // deque positions of rows l and l + 64 (metadata) and 16n + i (the first
     // tiles' X)
@@ -1479,8 +1482,9 @@ __global__ void __launch_bounds__(64 * (8 / NT), 1) k_shared_grad3(dmdqn_learn_a
 int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *slab, int n_slabs,
                      hipStream_t s) {
     using namespace shk;
-    const int next_blocks = (a->NA + 7) / 8 < n_slabs ? (a->NA + 7) / 8 : n_slabs;
-    hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(512), 0, s, *a, y, act);
+    const int next_wg = (a->NA + NEXT_WAVES - 1) / NEXT_WAVES;
+    const int next_blocks = next_wg < n_slabs ? next_wg : n_slabs;
+    hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(64 * NEXT_WAVES), 0, s, *a, y, act);
     DMDQN_LAUNCH_CHECK("k_shared_next");
     const char *gv = getenv("DMDQN_SHARED_GRAD");  // A/B: "2" = the row-owning pass
     if (gv && gv[0] == '2') {
