@@ -137,6 +137,30 @@ __device__ inline void mt_twist_wave(uint32_t *mt) {
     __syncthreads();
 }
 
+// The same twist by a block of NT >= 256 threads: one word per thread per
+// phase instead of four chunks of 64 lanes (every lane past the first wave
+// would redo them).
+template <int NT>
+__device__ inline void mt_twist_block(uint32_t *mt) {
+    static_assert(NT >= 256, "one word per thread per phase");
+    const int k = threadIdx.x;
+    uint32_t nv = 0;
+    if (k < 227) nv = mt_mix(mt[k], mt[k + 1], mt[k + MT_M]);
+    __syncthreads();
+    if (k < 227) mt[k] = nv;
+    __syncthreads();
+    if (k < 227) nv = mt_mix(mt[227 + k], mt[228 + k], mt[k]);
+    __syncthreads();
+    if (k < 227) mt[227 + k] = nv;
+    __syncthreads();
+    if (k < 169) nv = mt_mix(mt[454 + k], mt[455 + k], mt[227 + k]);
+    __syncthreads();
+    if (k < 169) mt[454 + k] = nv;
+    __syncthreads();
+    if (k == 0) mt[623] = mt_mix(mt[623], mt[0], mt[MT_M - 1]);
+    __syncthreads();
+}
+
 // Wave-resident stream: raw state words in LDS plus a tempered copy of the
 // current block (tempered in parallel right after each twist) so the
 // sequential consumer does one LDS read per draw.

@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
     int32_t *out = idx + (size_t)e * A * k;  // agent j's i-th pick
     while (j < A) {
         if (mti >= MT_N) {  // block-uniform
-            mt_twist_wave(mt);  // every lane of every wave: identical duplicate writes
+            mt_twist_block<NT>(mt);
             for (int t = tid; t < MT_N; t += NT) tmp[t] = mt_temper(mt[t]);
             __syncthreads();
             mti = 0;

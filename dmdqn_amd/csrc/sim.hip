@@ -593,12 +593,8 @@ __device__ int fused_act(const dmdqn_env_fuse &F, int A, uint32_t *mtbuf, bool &
     uint32_t *g = F.np_state + (size_t)e * DMDQN_MT_WORDS;
     const int mti0 = (int)g[MT_N];
     fast = act_fast_ok(mti0, A, 3, F.eps, rng, mask, 1);
-    if (fast) {
-        if ((int)threadIdx.x >= A) return 0;
-        const int a = act_fast(g, mti0, threadIdx.x, 3, mask);
-        F.actions[(size_t)e * A + threadIdx.x] = a;
-        return a;
-    }
+    if (fast)  // stored by fused_act_done: the load's latency hides behind the staging
+        return (int)threadIdx.x < A ? act_fast(g, mti0, threadIdx.x, 3, mask) : 0;
     MTWave w{mtbuf, mtbuf + MT_N, 0};
     w.load(g);
     int mine = 0;
@@ -622,8 +618,11 @@ __device__ int fused_act(const dmdqn_env_fuse &F, int A, uint32_t *mtbuf, bool &
 }
 
 // After a barrier that follows every thread's read of the old position.
-__device__ __forceinline__ void fused_act_done(const dmdqn_env_fuse &F, int A, bool fast) {
-    if (fast && threadIdx.x == 0) {
+__device__ __forceinline__ void fused_act_done(const dmdqn_env_fuse &F, int A, bool fast,
+                                               int my_act) {
+    if (!fast) return;
+    if ((int)threadIdx.x < A) F.actions[(size_t)blockIdx.x * A + threadIdx.x] = my_act;
+    if (threadIdx.x == 0) {
         uint32_t *g = F.np_state + (size_t)blockIdx.x * DMDQN_MT_WORDS;
         g[MT_N] = g[MT_N] + (uint32_t)(3 * A);
     }
@@ -634,6 +633,10 @@ __device__ __forceinline__ void fused_act_done(const dmdqn_env_fuse &F, int A, b
 // of this thread's first two (agent, 4-byte group) store slots, and the
 // reward's pre-step sum of agent `tid` (train.py:159-165).
 constexpr int kPreWords = 2;
+#ifndef DMDQN_FUSE_PREFETCH
+#define DMDQN_FUSE_PREFETCH 1
+#endif
+constexpr bool kFusePre = DMDQN_FUSE_PREFETCH;  // LDS path (A/B switch)
 struct TailPre {
     uint32_t ws[kPreWords];
     double sum;
@@ -808,7 +811,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
     TailPre pre{};
     if constexpr (kFuse) {
         my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off), act_fast);
-        pre = fused_prefetch(F, A);
+        if constexpr (kFusePre) pre = fused_prefetch(F, A);
     }
     if constexpr (kLDS) {
         const int C1 = V.C1;
@@ -897,7 +900,7 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         }
     }
     __syncthreads();
-    if constexpr (kFuse) fused_act_done(F, A, act_fast);
+    if constexpr (kFuse) fused_act_done(F, A, act_fast, my_act);
     QNext qn[QSLOTS];
 #pragma unroll
     for (int q = 0; q < QSLOTS; q++) {
@@ -976,7 +979,8 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
     if constexpr (kFuse) {
         __syncthreads();  // the write-back has read the image: its slots are scratch now
         const bool done_e = t >= max_time || (s_running + s_pending) == 0;
-        fused_tail(F, S.R, S.C, t, done_e, my_act, pre, s_halt, V.phase, V.ts, dyn + fl.tail_off);
+        fused_tail<kFusePre>(F, S.R, S.C, t, done_e, my_act, pre, s_halt, V.phase, V.ts,
+                             dyn + fl.tail_off);
     }
 #ifdef DMDQN_SIM_PROFILE
     __syncthreads();
@@ -1169,7 +1173,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     if (tid < 2) s_stats[tid] = G.stats[tid];
     if (tid == 2 || tid == 3) s_stats[tid] = 0;
     __syncthreads();
-    if constexpr (kFuse) fused_act_done(F, A, act_fast);
+    if constexpr (kFuse) fused_act_done(F, A, act_fast, my_act);
     const float len = own ? lane_length(T, e) : 0.0f;
 
     // TL at time t: natural phase advance (and the actuated gap-out of phase 0)
