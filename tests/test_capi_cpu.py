@@ -78,6 +78,16 @@ def test_host_side_argument_check_without_gpu(lib):
     assert b"dmdqn_act" in lib.dmdqn_last_error()
 
 
+def test_env_step_argument_check_without_gpu(lib):
+    """dmdqn_env_step (the fused act / sim / observe / store launch) refuses a
+    missing fuse block, a missing sim and incomplete act arguments on the host."""
+    rc = lib.dmdqn_env_step(None, None, None, 3, 0, 10, 2400, None, None, None, None, None)
+    assert rc == -1 and b"null fuse" in lib.dmdqn_last_error()
+    fuse = ctypes.create_string_buffer(512)  # all-zero dmdqn_env_fuse
+    rc = lib.dmdqn_env_step(None, None, fuse, 3, 0, 10, 2400, None, None, None, None, None)
+    assert rc == -1 and b"junctions" in lib.dmdqn_last_error()
+
+
 def test_replay_sample_lds_limit_checked_on_host(lib):
     """The sampler's LDS plan (MT state + n-bit bitmap + first-lane table) is
     checked before launch: an n whose bitmap alone exceeds LDS is refused."""
