@@ -1173,7 +1173,12 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     if (tid < 2) s_stats[tid] = G.stats[tid];
     if (tid == 2 || tid == 3) s_stats[tid] = 0;
     __syncthreads();
-    if constexpr (kFuse) fused_act_done(F, A, act_fast, my_act);
+    if constexpr (kFuse) {
+        fused_act_done(F, A, act_fast, my_act);
+        // parked in the MT stream's LDS (dead from here on) instead of a VGPR
+        // held across the substeps (this kernel is at its register limit)
+        if (tid < A) reinterpret_cast<int32_t *>(dyn + fl.mt_off)[tid] = my_act;
+    }
     const float len = own ? lane_length(T, e) : 0.0f;
 
     // TL at time t: natural phase advance (and the actuated gap-out of phase 0)
@@ -1466,7 +1471,9 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     }
     if constexpr (kFuse) {
         const bool done_e = t >= max_time || (s_stats[2] + s_stats[3]) == 0;
-        fused_tail<!kL>(F, S.R, S.C, t, done_e, my_act, pre, s_halt, s_phase, s_ts, dyn + fl.tail_off);
+        const int act_back = tid < A ? reinterpret_cast<const int32_t *>(dyn + fl.mt_off)[tid] : 0;
+        fused_tail<!kL>(F, S.R, S.C, t, done_e, act_back, pre, s_halt, s_phase, s_ts,
+                        dyn + fl.tail_off);
     }
 }
 

@@ -15,3 +15,4 @@ tail -1 $O/bench_c3.json
 timeout -k 10 300 python bench.py --rows 2 --cols 2 --envs 256 --precision bf16 --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err
 timeout -k 10 300 python bench.py --shared --rows 8 --cols 8 --envs 256 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err
 for f in $O/bench_c2.json $O/bench_c5.json; do tail -1 $f | cut -c1-200; done
+bash tools/prof_quick.sh gpurun_out/final/c5prof --shared --rows 8 --cols 8 --envs 256 --steps 30 | grep -E "sim_step|sample"
