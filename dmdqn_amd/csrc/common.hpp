@@ -161,6 +161,24 @@ __device__ inline void mt_twist_block(uint32_t *mt) {
     __syncthreads();
 }
 
+// The next 624-word block of the stream whose current raw block is cur,
+// written to nxt (cur unchanged): the same recurrence as mt_twist_wave with
+// the freshly written words read from nxt, so the phases need no read/write
+// split.  A block of NT >= 256 threads, one word per thread per phase.
+template <int NT>
+__device__ inline void mt_twist_into(const uint32_t *cur, uint32_t *nxt) {
+    static_assert(NT >= 256, "one word per thread per phase");
+    const int k = threadIdx.x;
+    if (k < 227) nxt[k] = mt_mix(cur[k], cur[k + 1], cur[k + MT_M]);
+    __syncthreads();
+    if (k < 227) nxt[227 + k] = mt_mix(cur[227 + k], cur[228 + k], nxt[k]);
+    __syncthreads();
+    if (k < 169) nxt[454 + k] = mt_mix(cur[454 + k], cur[455 + k], nxt[227 + k]);
+    __syncthreads();
+    if (k == 0) nxt[623] = mt_mix(cur[623], nxt[0], nxt[MT_M - 1]);
+    __syncthreads();
+}
+
 // Wave-resident stream: raw state words in LDS plus a tempered copy of the
 // current block (tempered in parallel right after each twist) so the
 // sequential consumer does one LDS read per draw.

@@ -337,32 +337,38 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     __shared__ int s_cnt[NW];
     __shared__ int s_cons;
-    uint32_t *mt = smem, *tmp = smem + MT_N, *bm = smem + 2 * MT_N;
+    // two raw 624-word blocks of the stream: the current one and, once a chunk
+    // reaches past it, the next (twisted ahead out of place); words are
+    // tempered as they are read, so a chunk is always 64*NW words long
+    uint32_t *cur = smem, *nxt = smem + MT_N, *bm = smem + 2 * MT_N;
     const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
     uint32_t *first = bm + words;  // [T + 1]: entry T is the dummy
     const uint32_t tmask = (1u << tlog) - 1u, dummy = tmask + 1u;
     const int tid = threadIdx.x, wv = tid >> 6, e = blockIdx.x;
     uint32_t *g = py_state + (size_t)e * DMDQN_MT_WORDS;
-    for (int t = tid; t < MT_N; t += NT) mt[t] = g[t];
+    for (int t = tid; t < MT_N; t += NT) cur[t] = g[t];
     int mti = (int)g[MT_N];
-    __syncthreads();
-    for (int t = tid; t < MT_N; t += NT) tmp[t] = mt_temper(mt[t]);
+    bool ahead = false;  // nxt holds the block after cur
     for (uint32_t t = tid; t < words; t += NT) bm[t] = 0u;
     for (uint32_t t = tid; t <= dummy; t += NT) first[t] = 0xffffffffu;
     __syncthreads();
     int j = 0, i = 0;
     int32_t *out = idx + (size_t)e * A * k;  // agent j's i-th pick
     while (j < A) {
-        if (mti >= MT_N) {  // block-uniform
-            mt_twist_block<NT>(mt);
-            for (int t = tid; t < MT_N; t += NT) tmp[t] = mt_temper(mt[t]);
-            __syncthreads();
-            mti = 0;
+        if (mti >= MT_N) {  // block-uniform: enter the next block
+            if (!ahead) mt_twist_into<NT>(cur, nxt);
+            uint32_t *t2 = cur; cur = nxt; nxt = t2;
+            mti -= MT_N;
+            ahead = false;
         }
-        const int cnt = min(NT, MT_N - mti);
-        const bool live = tid < cnt;
-        const uint32_t r = getbits(tmp[mti + (live ? tid : 0)], kb);
-        const bool inr = live && r < n;
+        if (!ahead && mti + NT > MT_N) {
+            mt_twist_into<NT>(cur, nxt);
+            ahead = true;
+        }
+        const int cnt = NT;
+        const int w = mti + tid;
+        const uint32_t r = getbits(mt_temper(w < MT_N ? cur[w] : nxt[w - MT_N]), kb);
+        const bool inr = r < n;
         const uint32_t bw = bm[inr ? r >> 5 : 0u];
         const bool cand = inr && !((bw >> (r & 31)) & 1u);
         const uint32_t slot = cand ? (r & tmask) : dummy;
@@ -416,7 +422,12 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
         }
         __syncthreads();
     }
-    for (int t = tid; t < MT_N; t += NT) g[t] = mt[t];
+    if (mti > MT_N) {  // the last pick ended in the next block (at exactly 624 the
+                       // stored state stays (cur, 624), as CPython's would)
+        uint32_t *t2 = cur; cur = nxt; nxt = t2;
+        mti -= MT_N;
+    }
+    for (int t = tid; t < MT_N; t += NT) g[t] = cur[t];
     if (tid == 0) g[MT_N] = (uint32_t)mti;
 }
 
