@@ -344,13 +344,20 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
     const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
     uint32_t *first = bm + words;  // [T + 1]: entry T is the dummy
     const uint32_t tmask = (1u << tlog) - 1u, dummy = tmask + 1u;
+    // first-lane table entries: (round << ib) | (imask - ((r >> tlog) << 9 | tid)),
+    // taken with atomicMax: the current round's entries beat every older one
+    // and, among themselves, the smallest (r >> tlog, word) wins -- the table
+    // never needs resetting between rounds
+    const uint32_t ib = 9u + (kb > (uint32_t)tlog ? kb - (uint32_t)tlog : 0u);
+    const uint32_t imask = (1u << ib) - 1u, emax = (uint32_t)(((uint64_t)1 << (32 - ib)) - 1u);
+    uint32_t ep = 1;  // round number (0 = empty)
     const int tid = threadIdx.x, wv = tid >> 6, e = blockIdx.x;
     uint32_t *g = py_state + (size_t)e * DMDQN_MT_WORDS;
     for (int t = tid; t < MT_N; t += NT) cur[t] = g[t];
     int mti = (int)g[MT_N];
     bool ahead = false;  // nxt holds the block after cur
     for (uint32_t t = tid; t < words; t += NT) bm[t] = 0u;
-    for (uint32_t t = tid; t <= dummy; t += NT) first[t] = 0xffffffffu;
+    for (uint32_t t = tid; t <= dummy; t += NT) first[t] = 0u;
     __syncthreads();
     int j = 0, i = 0;
     int32_t *out = idx + (size_t)e * A * k;  // agent j's i-th pick
@@ -372,19 +379,23 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
         const uint32_t bw = bm[inr ? r >> 5 : 0u];
         const bool cand = inr && !((bw >> (r & 31)) & 1u);
         const uint32_t slot = cand ? (r & tmask) : dummy;
-        const uint32_t key = cand ? (((r >> tlog) << 9) | (uint32_t)tid) : 0xffffffffu;
+        const uint32_t inner = ((r >> tlog) << 9) | (uint32_t)tid;
         bool pend = cand, dup = false;
-        while (__syncthreads_or(pend)) {
+        do {  // the read of a round sees its every write, the next round's writes wait for it
+            if (ep >= emax) {  // block-uniform, after the last round's reads: restart the rounds
+                for (uint32_t t = tid; t <= dummy; t += NT) first[t] = 0u;
+                __syncthreads();
+                ep = 1;
+            }
             const uint32_t sl = pend ? slot : dummy;
-            atomicMin(&first[sl], pend ? key : 0xffffffffu);
+            atomicMax(&first[sl], pend ? (ep << ib) | (imask - inner) : 0u);
             __syncthreads();
-            const uint32_t win = first[sl];
-            __syncthreads();
-            first[sl] = 0xffffffffu;
-            const bool mine = pend && (win >> 9) == (key >> 9);  // same r
-            if (mine) dup = win != key;
+            const uint32_t wi = imask - (first[sl] & imask);  // the winner's (r >> tlog, word)
+            const bool mine = pend && (wi >> 9) == (inner >> 9);  // same r
+            if (mine) dup = wi != inner;
             pend = pend && !mine;
-        }
+            ep++;
+        } while (__syncthreads_or(pend));
         const bool acc = cand && !dup;
         const uint64_t b = __ballot(acc);
         if ((tid & 63) == 0) s_cnt[wv] = __popcll(b);
