@@ -381,6 +381,7 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
         const uint32_t slot = cand ? (r & tmask) : dummy;
         const uint32_t inner = ((r >> tlog) << 9) | (uint32_t)tid;
         bool pend = cand, dup = false;
+        uint64_t b;
         do {  // the read of a round sees its every write, the next round's writes wait for it
             if (ep >= emax) {  // block-uniform, after the last round's reads: restart the rounds
                 for (uint32_t t = tid; t <= dummy; t += NT) first[t] = 0u;
@@ -395,11 +396,12 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
             if (mine) dup = wi != inner;
             pend = pend && !mine;
             ep++;
+            // the accepted count per wave, final in the round that leaves no lane
+            // pending (the loop's barrier publishes it)
+            b = __ballot(cand && !dup && !pend);
+            if ((tid & 63) == 0) s_cnt[wv] = __popcll(b);
         } while (__syncthreads_or(pend));
         const bool acc = cand && !dup;
-        const uint64_t b = __ballot(acc);
-        if ((tid & 63) == 0) s_cnt[wv] = __popcll(b);
-        __syncthreads();
         int before = 0, total = 0;
 #pragma unroll
         for (int w2 = 0; w2 < NW; w2++) {
@@ -410,26 +412,26 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
         const int ln = tid & 63;
         const uint64_t below = ln ? (~0ull >> (64 - ln)) : 0ull;
         const int c = before + __popcll(b & below), need = k - i;
-        int taken = total, consumed = cnt;
-        if (total >= need) {  // block-uniform
-            taken = need;
+        if (total >= need) {  // block-uniform: agent j's last chunk (no bitmap update needed)
             if (acc && c == need - 1) s_cons = tid + 1;
+            if (acc && c < need) {
+                DMDQN_DBG(r < n, DBG_SAMPLE);
+                out[i + c] = (int32_t)r;
+            }
             __syncthreads();
-            consumed = s_cons;
-        }
-        if (acc && c < taken) {
-            DMDQN_DBG(r < n, DBG_SAMPLE);
-            out[i + c] = (int32_t)r;
-            atomicOr(&bm[r >> 5], 1u << (r & 31));
-        }
-        mti += consumed;
-        i += taken;
-        if (i == k) {
+            mti += s_cons;
             j++;
             i = 0;
             out += k;
-            __syncthreads();  // every OR of this chunk is in before the clear
             for (uint32_t t = tid; t < words; t += NT) bm[t] = 0u;
+        } else {
+            if (acc) {
+                DMDQN_DBG(r < n, DBG_SAMPLE);
+                out[i + c] = (int32_t)r;
+                atomicOr(&bm[r >> 5], 1u << (r & 31));
+            }
+            mti += cnt;
+            i += total;
         }
         __syncthreads();
     }
