@@ -107,12 +107,14 @@ def cpu_baseline(rows, cols, steps=60, seed=0):
 
 
 def read_traffic(workload_key):
-    """(per-launch HBM bytes, where they come from) for a kernel from the
+    """(per-launch HBM bytes, where they come from, stale) for a kernel from the
     committed PMC passes (profiles/learn_pmc.json, written by tools/pmc_learn.py
     from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench).
     The counters cannot be read inside this process, so the figure is NOT
-    measured in this run: traffic_source names the pass it comes from.
-    (None, None) when no pass exists for this workload."""
+    measured in this run: traffic_source names the pass it comes from, and
+    stale is True when the kernel sources it measured (their digest, recorded
+    by the pass) are not this tree's (dmdqn_amd.build.source_digest); an entry
+    without a digest counts as stale.  (None, None, None) when no pass exists."""
     p = os.path.join(ROOT, "profiles", "learn_pmc.json")
     try:
         with open(p) as f:
@@ -120,11 +122,14 @@ def read_traffic(workload_key):
     except Exception:
         e = None
     if not e:
-        return None, None
+        return None, None, None
+    from dmdqn_amd.build import source_digest
+    dg = e.get("sources_digest") or {}
+    stale = not dg or dg.get("sha256_16") != source_digest(dg.get("kind", "learn"))
     src = (f"profiles/learn_pmc.json[{workload_key}]: committed rocprofv3 PMC pass "
            f"({e.get('source', 'tools/profile_bench.sh')}; FETCH_SIZE x2 + WRITE_SIZE, "
            f"mean of {e['dispatches'][0]} launches), not measured in this run")
-    return e.get("hbm_bytes_per_launch"), src
+    return e.get("hbm_bytes_per_launch"), src, stale
 
 
 def config_name(rows, cols, envs, precision, shared, world):
@@ -147,7 +152,7 @@ def sim_state_fits_lds(rows, cols, cap=24):
     return state + topo <= 160 * 1024 - 64
 
 
-def _sim_roofline(E, K, vbar, sim_ms, traffic, traffic_src, in_lds=True):
+def _sim_roofline(E, K, vbar, sim_ms, traffic, traffic_src, traffic_stale, in_lds=True):
     """Sim-only HBM figure: 20*K*V-bar algorithmic bytes per env
     step over the average k_sim_step duration (HIP events over the
     SIM_PROBE_STEPS untimed steps that follow the timed region)."""
@@ -159,7 +164,8 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, traffic_src, in_lds=True):
     return {"kernel": f"k_sim_step (K IDM substeps per launch, {where})",
             "bound": "hbm", "achieved": round(b / t / 1e9, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 5),
-            "traffic": traffic, "traffic_source": traffic_src,
+            "traffic": traffic, "traffic_source": traffic_src, "traffic_stale": traffic_stale,
+            "traffic_ratio": round(traffic / b, 3) if traffic and b else None,
             "bytes_per_launch": int(b), "mean_running_vehicles": round(vbar, 1),
             "avg_launch_ms": round(t * 1e3, 4),
             "timed_over": f"{SIM_PROBE_STEPS} back-to-back launches after the timed region",
@@ -223,6 +229,10 @@ def main():
                          "env step (dmdqn_env_step; bit-identical, A/B)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo; only barrier + timing use it")
+    ap.add_argument("--dist-timeout", type=float, default=None,
+                    help="seconds any collective (rendezvous, barrier, timing max) may take "
+                         "before the run exits non-zero naming the rank and call "
+                         "(default DMDQN_DIST_TIMEOUT_S or 180)")
     args = ap.parse_args()
 
     import torch
@@ -234,7 +244,8 @@ def main():
     local = int(os.environ.get("DMDQN_DEVICE_OVERRIDE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    D.init(backend=args.dist_backend, device=dev)  # only barrier + timing max use it
+    D.init(backend=args.dist_backend, device=dev,  # only barrier + timing max use it
+           timeout_s=args.dist_timeout)
 
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.env import EnvConfig
@@ -285,7 +296,7 @@ def main():
         (starts if before else ends).append(ev)
 
     learn_before = tr.agent.learn_launches
-    D.barrier()
+    D.barrier(args.dist_timeout)
     torch.cuda.synchronize(dev)
     tr.agent.learn_hook = hook
     from dmdqn_amd import kernels as KM
@@ -297,7 +308,7 @@ def main():
     t_wait = KM.POLL_WAIT_S[0] - wait0  # ... of which blocked on the lagged replay check
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    D.barrier()
+    D.barrier(args.dist_timeout)
     tr.agent.learn_hook = None
     n_learn = tr.agent.learn_launches - learn_before
 
@@ -330,7 +341,7 @@ def main():
     sim_ms = [s0.elapsed_time(s1) / SIM_PROBE_STEPS]
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    el_max = D.max_over_ranks(el, device=dev)
+    el_max = D.max_over_ranks(el, device=dev, timeout_s=args.dist_timeout)
 
     if rank == 0:
         value = args.steps * NA * world / el_max
@@ -341,9 +352,9 @@ def main():
         avg_learn_s = float(np.mean(learn_ms)) / 1e3 if learn_ms else float("nan")
         achieved = bpl / avg_learn_s / 1e9
         wl = f"{args.rows}x{args.cols}x{args.envs}"
-        traffic, traffic_src = read_traffic(f"{wl}_{args.precision}" +
-                                            ("_shared" if args.shared else ""))
-        sim_traffic, sim_src = read_traffic(f"{wl}_sim")
+        traffic, traffic_src, traffic_stale = read_traffic(f"{wl}_{args.precision}" +
+                                                           ("_shared" if args.shared else ""))
+        sim_traffic, sim_src, sim_stale = read_traffic(f"{wl}_sim")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.rows, args.cols, args.cpu_steps)
@@ -399,6 +410,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_stale": traffic_stale,
                 "bytes_per_launch": bpl,
                 "avg_launch_ms": round(avg_learn_s * 1e3, 4),
                 "learn_share_of_step": round(avg_learn_s / (el_max / args.steps), 3),
@@ -410,7 +422,7 @@ def main():
             "step_roofline": _step_roofline(value, tr.env.cfg.step_duration, vbar, A, P,
                                             args.shared, NA),
             "sim_roofline": _sim_roofline(E, tr.env.cfg.step_duration, vbar, sim_ms,
-                                          sim_traffic, sim_src,
+                                          sim_traffic, sim_src, sim_stale,
                                           sim_state_fits_lds(args.rows, args.cols)),
             "mfma": {
                 "kernel": ("k_shared_next + k_shared_grad" if args.shared else LEARN_KERNELS[args.precision]) +
@@ -429,4 +441,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    from dmdqn_amd.dist import DistError
+    try:
+        main()
+    except DistError as e:  # name the rank and the collective, exit non-zero (no hang)
+        print(json.dumps({"error": str(e), "rank": int(os.environ.get("RANK", "0"))}),
+              file=sys.stderr, flush=True)
+        sys.exit(3)

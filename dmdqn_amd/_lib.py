@@ -3,6 +3,7 @@
 The product path calls the HIP library only; if the library is missing or a
 call fails, it raises -- there is no CPU fallback.
 """
+import contextlib
 import ctypes as C
 import os
 
@@ -32,6 +33,8 @@ SIGNATURES = {
     "dmdqn_replay_gather_f32": [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp],
     "dmdqn_stream_create_cumask": [u32, vp, vp],
     "dmdqn_stream_destroy": [vp],
+    "dmdqn_set_option": [i32, i32],
+    "dmdqn_get_option": [i32],
 }
 
 
@@ -82,6 +85,33 @@ def call(name, *args):
     if rc != 0:
         raise DmdqnError(f"{name} failed (rc={rc}): {lib.dmdqn_last_error().decode()}")
     return rc
+
+
+# include/dmdqn.h DMDQN_OPT_*: the launchers' test / A-B hooks, read from the
+# environment once at library load and changed only through set_option
+OPTIONS = {"sim_path": (0, {"auto": 0, "reg": 1, "lds": 2, "global": 3}),
+           "sample_tlog": (1, {None: 32})}
+
+
+def set_option(name, value):
+    """Set a run-time option (sim_path: auto | reg | lds | global; sample_tlog:
+    0..20 or None = no cap); returns the previous value in the same form."""
+    which, names = OPTIONS[name]
+    inv = {v: k for k, v in names.items()}
+    lib = load()
+    old = lib.dmdqn_get_option(which)
+    call("dmdqn_set_option", which, names.get(value, value))
+    return inv.get(old, old)
+
+
+@contextlib.contextmanager
+def option(name, value):
+    """set_option for the duration of a with-block."""
+    old = set_option(name, value)
+    try:
+        yield
+    finally:
+        set_option(name, old)
 
 
 DEBUG_BITS = {1: "sim ring slot", 2: "sim route leaves the grid", 4: "replay index >= n",

@@ -62,6 +62,28 @@ DEFAULT_FP = ["-ffp-contract=off"]
 EXTRA = os.environ.get("DMDQN_EXTRA_FLAGS", "").split()
 
 
+# The sources whose code a PMC traffic figure describes (profiles/learn_pmc.json
+# records their digest; bench.py flags a figure measured on other sources as
+# stale): the learn kernels, and the env step (sim + fused observe / store).
+KERNEL_SOURCES = {
+    "learn": ["learn.hip", "learn_f16.hip", "learn_bf16.hip", "learn_h16.hpp", "learn_shared.hip",
+              "qnet_layout.hpp", "common.hpp"],
+    "sim": ["sim.hip", "sim.hpp", "observe.hpp", "common.hpp"],
+}
+
+
+def source_digest(kind):
+    """sha256 (hex, 16 chars) over the KERNEL_SOURCES of `kind` and the compile
+    flags, in a fixed order."""
+    import hashlib
+    h = hashlib.sha256(" ".join(COMMON).encode())
+    for name in KERNEL_SOURCES[kind]:
+        h.update(name.encode())
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 

@@ -39,11 +39,12 @@ _AGENT_TENSORS = ["params", "target", "adam_m", "adam_v", "np_state", "py_state"
 # different value would restore tensors that mean something else (or leave
 # derived state stale), so load() refuses it.
 _AGENT_FIXED = ["precision", "shared_params", "nn_layers", "replay_buffer_size", "batch_size",
-                "seed", "loss", "target_update_frequency", "count_env_steps"]
+                "seed", "loss", "target_update_frequency", "count_env_steps", "replay_rows"]
 _ENV_FIXED = ["rows", "cols", "num_envs", "env_offset", "seed", "signal_features", "cap_lane",
               "end_ms", "period_ms", "step_duration", "max_sim_time", "action_stride", "scenario",
               "actuated"]
-_DEFAULTS = {"loss": "mse", "actuated": False}  # fields added after format 4 was introduced
+# fields added after format 4 was introduced
+_DEFAULTS = {"loss": "mse", "actuated": False, "replay_rows": "int8"}
 
 
 def _check_cfg(saved, cur, fields, what):

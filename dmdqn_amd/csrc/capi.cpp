@@ -1,6 +1,8 @@
 // capi.cpp -- error reporting and version of the C ABI (include/dmdqn.h).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "common.hpp"
 
@@ -14,18 +16,32 @@ void set_error(const char *fmt, ...) {
     va_end(ap);
 }
 
+// Run-time options (dmdqn.h DMDQN_OPT_*), from the environment at load time.
+static int g_opt[2] = {0, 32};
+
+__attribute__((constructor)) static void read_options() {
+    const char *p = getenv("DMDQN_SIM_PATH");
+    if (p) g_opt[DMDQN_OPT_SIM_PATH] = !strcmp(p, "reg") ? 1 : !strcmp(p, "lds") ? 2
+                                       : !strcmp(p, "global") ? 3 : 0;
+    const char *t = getenv("DMDQN_SAMPLE_TLOG");
+    if (t && atoi(t) >= 0 && atoi(t) <= 20) g_opt[DMDQN_OPT_SAMPLE_TLOG] = atoi(t);
+}
+
+int option(int which) { return g_opt[which]; }
+
 // per-source-file debug flags (common.hpp DMDQN_DBG_READER)
 int dbg_flags_sim();
 int dbg_flags_rng();
 int dbg_flags_learn();
+int dbg_flags_replay();
 namespace f16k { int dbg_flags(); }
 namespace bf16k { int dbg_flags(); }
 }  // namespace dmdqn
 
 extern "C" int dmdqn_debug_status(void) {
     using namespace dmdqn;
-    const int f[5] = {dbg_flags_sim(), dbg_flags_rng(), dbg_flags_learn(), f16k::dbg_flags(),
-                      bf16k::dbg_flags()};
+    const int f[6] = {dbg_flags_sim(), dbg_flags_rng(), dbg_flags_learn(), f16k::dbg_flags(),
+                      bf16k::dbg_flags(), dbg_flags_replay()};
     int v = 0;
     for (int x : f) {
         if (x < 0) return -1;
@@ -40,6 +56,23 @@ extern "C" int dmdqn_debug_build(void) {
 #else
     return 0;
 #endif
+}
+
+extern "C" int dmdqn_set_option(int opt, int value) {
+    DMDQN_REQUIRE(opt == DMDQN_OPT_SIM_PATH || opt == DMDQN_OPT_SAMPLE_TLOG,
+                  "dmdqn_set_option: unknown option %d", opt);
+    DMDQN_REQUIRE(opt != DMDQN_OPT_SIM_PATH || (value >= 0 && value <= 3),
+                  "dmdqn_set_option: sim path %d (0 auto, 1 reg, 2 lds, 3 global)", value);
+    DMDQN_REQUIRE(opt != DMDQN_OPT_SAMPLE_TLOG || (value >= 0 && value <= 20) || value == 32,
+                  "dmdqn_set_option: sample tlog %d (0 .. 20, or 32 = no cap)", value);
+    dmdqn::g_opt[opt] = value;
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_get_option(int opt) {
+    DMDQN_REQUIRE(opt == DMDQN_OPT_SIM_PATH || opt == DMDQN_OPT_SAMPLE_TLOG,
+                  "dmdqn_get_option: unknown option %d", opt);
+    return dmdqn::g_opt[opt];
 }
 
 extern "C" const char *dmdqn_last_error(void) { return dmdqn::g_err; }

@@ -31,6 +31,10 @@ void set_error(const char *fmt, ...);
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Run-time options (include/dmdqn.h DMDQN_OPT_*): read from the environment
+// once, when the library loads (capi.cpp), then only through dmdqn_set_option.
+int option(int which);
+
 // ---------------------------------------------------------------- debug-bounds build
 // Built with -DDMDQN_DEBUG_BOUNDS (python -m dmdqn_amd.build --debug ->
 // libdmdqn_hip_debug.so): kernels check the indices they derive and

@@ -1,130 +1,13 @@
 // learn_f16.hip -- the f16 instantiation of learn_h16.hpp (the reference's
 // tf.keras mixed_float16 policy, train.py:61: f16 MFMA operands, f32
 // accumulate, f32 master weights + Adam), plus the shared-parameter learn
-// (configuration C5) and the flat Keras-3 Adam it is followed by.
+// (configuration C5, SURVEY 8e: the two passes are in learn_shared.hip; the
+// slab reduction is here) and the flat Keras-3 Adam it is followed by.
 #define DMDQN_H16_BF16 0
 #include "learn_h16.hpp"
 
 namespace dmdqn {
 namespace f16k {
-
-// ----------------------------------------------------------------------------
-// Shared-parameter DQN (not in the reference): ONE online /
-// target network for every agent.  Persistent workgroups (one per CU, 256
-// VGPRs) hold both networks' fragments in registers for the whole launch and
-// loop over agents; each agent's batch runs the same forward/backward as the
-// independent kernel, and its gradient tiles accumulate straight into MFMA
-// accumulators that live across the agent loop.  Each workgroup then writes
-// its partial sum (kernel layout, P floats) to slab[blockIdx.x].  No Adam
-// here: k_reduce_slabs + (RCCL all-reduce across ranks) + k_adam follow.
-template <bool QSTATS>
-__global__ void __launch_bounds__(512, 2) k_learn_shared_f16(dmdqn_learn_args a, float *slab) {
-    LEARN_SMEM_SETUP;
-    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
-    const float *Wp = a.params;
-    const _Float16 *TH = a.target_h ? reinterpret_cast<const _Float16 *>(a.target_h) : nullptr;
-    const _Float16 *WH = reinterpret_cast<const _Float16 *>(a.params_h);
-    Frags fr;
-    stage_out(Wp, W3L, B3L);
-    if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
-    else stage_out(a.target, W3L + NACT * H, B3L + NACT);
-    const half8 ones = ones8();
-    // dW2 accumulators (64 KB f32) live in LDS -- one workgroup per CU leaves
-    // room -- laid out [wave][tile][lane] so each access is one contiguous
-    // 1 KB wave row; the rest stay in registers.
-    __shared__ f32x4 G2L[8 * 8 * 64];
-    f32x4 G3 = {0.f, 0.f, 0.f, 0.f}, GB3 = G3, GB2 = G3, GB1 = G3, G1[6];
-#pragma unroll
-    for (int t = 0; t < 8; t++) G2L[(w * 8 + t) * 64 + l] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 6; t++) G1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int agent = blockIdx.x; agent < a.NA; agent += gridDim.x) {
-        // the shared nets are L2-resident: reload the fragments per agent (as
-        // the independent kernel does from HBM) rather than pin 72 VGPRs
-        if (TH) load_frags(TH, fr);
-        else load_frags(a.target, fr);
-        batch_head(a, agent, R2, S);  // X(S') in R2, metadata, z-score
-        // buffer plan of k_learn_f16: the backward runs on (P1, P2) = (R2, R1)
-        forward_x<true>(fr, tg, R2, R1, R1, S.z3, [WH](Frags &f) { load_w1(WH, f); },
-                        [WH](Frags &f) { load_w2(WH, f); });  // X(S') stays in R2
-        float *qo = (float *)DQ;
-        Rows gs;
-        forward_x<false>(fr, on, R2, R1, R2, qo,
-                         [&](Frags &) { gather_issue(a.ring_s, a, agent, S.slot, gs); }, NoHook{},
-                         [&]() { gather_commit(R1, gs); });
-        ddqn_target(a, qo, S);
-        forward_x<false>(fr, on, R1, R2, R1, S.z3);
-        _Float16 *const P1 = R2, *const P2 = R1;
-        loss_dq<QSTATS>(a, agent, DQ, S);
-        // dW3 / db3
-#pragma unroll
-        for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 dqf = frag_tr(DQ, 16, b0, 0);
-            G3 = mfma(frag_tr_h(P2, b0, 16 * w), dqf, G3);
-            GB3 = mfma(ones, dqf, GB3);
-        }
-        __syncthreads();
-        bwd_dz2(P2, on, S);
-        h1_mask(P1, mask);
-        // dW2 / db2 (tile by tile, accumulating into the LDS accumulators)
-        {
-            half8 av[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                av[q] = frag_tr_h(P1, 32 * q, 16 * w);
-                GB2 = mfma(ones, frag_tr_h(P2, 32 * q, 16 * w), GB2);
-            }
-#pragma unroll
-            for (int t = 0; t < 8; t++) {
-                f32x4 c = G2L[(w * 8 + t) * 64 + l];
-#pragma unroll
-                for (int q = 0; q < 4; q++) c = mfma(av[q], frag_tr_h(P2, 32 * q, 16 * t), c);
-                G2L[(w * 8 + t) * 64 + l] = c;
-            }
-        }
-        __syncthreads();
-        f32x4 d1[8];
-        bwd_dh1(P1, P2, fr, d1);
-        {
-            Rows gx;
-            gather_issue(a.ring_s, a, agent, S.slot, gx);
-            gather_commit(P2, gx);
-        }
-        bwd_dz1(P1, mask, d1);
-        __syncthreads();
-        // dW1 / db1
-#pragma unroll
-        for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 bv = frag_tr_h(P1, b0, 16 * w);
-            GB1 = mfma(ones, bv, GB1);
-#pragma unroll
-            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr_h<DP>(P2, b0, 16 * t), bv, G1[t]);
-        }
-        __syncthreads();  // P1 / P2 / scratch are rewritten by the next agent
-    }
-    // partial sums of this workgroup, kernel layout (every index written once)
-    float *G = slab + (size_t)blockIdx.x * L::P;
-    if (lr < NACT) {
-        *reinterpret_cast<float4 *>(G + L::oW3T + lr * H + 16 * w + 4 * lg) =
-            make_float4(G3[0], G3[1], G3[2], G3[3]);
-        if (w == 0 && lg == 0) G[L::ob3 + lr] = GB3[0];
-    }
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const f32x4 c = G2L[(w * 8 + t) * 64 + l];
-        *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(16 * t + lr, 16 * w + 4 * lg, H)) =
-            make_float4(c[0], c[1], c[2], c[3]);
-    }
-    if (lg == 0) G[L::ob2 + 16 * w + lr] = GB2[0];
-#pragma unroll
-    for (int t = 0; t < 6; t++)
-        if (t < 5 || lg < 2)  // tile 5: features 80..87 (89..95 do not exist)
-            *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(16 * w + lr, 16 * t + 4 * lg)) =
-                make_float4(G1[t][0], G1[t][1], G1[t][2], G1[t][3]);
-    if (lg == 0) G[L::ob1 + 16 * w + lr] = GB1[0];
-    if (lg == 2) G[L::oW1X + 16 * w + lr] = G1[5][0];  // feature 88
-}
 
 // grad[i] = scale * sum_w slab[w][i] in a fixed order: wave v of a block sums
 // slabs v, v + 8, v + 16, ... for 64 float4 columns, then the 8 partials are
@@ -216,21 +99,12 @@ extern "C" int dmdqn_learn_shared_grad(const dmdqn_learn_args *a, float *slab, i
     DMDQN_REQUIRE(a->loss_kind == DMDQN_LOSS_MSE || a->loss_kind == DMDQN_LOSS_HUBER,
                   "dmdqn_learn_shared_grad: loss_kind %d", a->loss_kind);
     DMDQN_REQUIRE(a->target_h, "dmdqn_learn_shared_grad: target_h (the f16 target) required");
+    DMDQN_REQUIRE(work, "dmdqn_learn_shared_grad: work (dmdqn_learn_shared_work_bytes) required");
     hipStream_t s = as_stream(stream);
-    const char *v1 = getenv("DMDQN_SHARED_V1");  // A/B against the one-pass kernel
-    if (work && !(v1 && v1[0] == '1')) {
-        float *y = reinterpret_cast<float *>(work);
-        uint8_t *act = reinterpret_cast<uint8_t *>(y + (size_t)a->NA * f16k::B_);
-        int rc = launch_shared_v2(a, y, act, slab, n_slabs, s);
-        if (rc) return rc;
-    } else if (a->qstats) {
-        hipLaunchKernelGGL(f16k::k_learn_shared_f16<true>, dim3(n_slabs), dim3(512), 0, s, *a, slab);
-        DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
-    } else {
-        hipLaunchKernelGGL(f16k::k_learn_shared_f16<false>, dim3(n_slabs), dim3(512), 0, s, *a,
-                           slab);
-        DMDQN_LAUNCH_CHECK("k_learn_shared_f16");
-    }
+    float *y = reinterpret_cast<float *>(work);
+    uint8_t *act = reinterpret_cast<uint8_t *>(y + (size_t)a->NA * f16k::B_);
+    const int rc = launch_shared_v2(a, y, act, slab, n_slabs, s);
+    if (rc) return rc;
     hipLaunchKernelGGL(f16k::k_reduce_slabs, dim3((f16k::L::P / 4 + 63) / 64), dim3(512), 0, s,
                        slab, n_slabs, scale, grad);
     DMDQN_LAUNCH_CHECK("k_reduce_slabs");

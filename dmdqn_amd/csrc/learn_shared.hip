@@ -1,29 +1,28 @@
 // learn_shared.hip -- the shared-parameter learn of configuration C5 (SURVEY
 // 8e; not in the reference, which trains one network per junction) as two
-// batched passes over every agent's 128-row batch, with the ONE network
-// resident in LDS for the whole launch (f16, the reference's mixed_float16
-// rounding points: learn_h16.hpp).
+// batched passes over every agent's 128-row batch (f16, the reference's
+// mixed_float16 rounding points: learn_h16.hpp).
 //
 //   k_shared_next   per agent: z-score (dqn_agent.py:66-69), X(S') from the
 //                   s' rows, target and online forwards of S', first-max
 //                   argmax, y = r^ + (gamma (1 - d)) Q_t(S')[a*] (:342-347);
 //                   writes y and the batch actions.  Both nets in LDS.
-//   k_shared_grad   per agent: X(S), online forward, MSE / Huber dL/dQ, and
+//   k_shared_grad3  per agent: X(S), online forward, MSE / Huber dL/dQ, and
 //                   the backward; the weight gradients of all the agents a
 //                   workgroup walks accumulate in registers and are written
 //                   once per workgroup as a partial slab (k_reduce_slabs,
-//                   RCCL all-reduce and k_adam follow, as before).
+//                   RCCL all-reduce and k_adam follow).
 //
-// Each forward runs "wave owns rows": a wave takes a 16-row tile through all
+// The S' pass runs "wave owns rows": a wave takes a 16-row tile through all
 // three layers in registers.  The transposed GEMMs Z^T = W^T X^T leave each
 // lane with 4 consecutive neurons of one row (MFMA C layout), and two such
 // tiles are exactly the 8 K-values the next layer's B operand needs when the
 // next layer's weights are stored with that K order (kperm below) -- so the
 // activations never go through LDS in the forward, and no barrier is needed.
 // The weight fragments come from LDS (one 16-byte read per lane per MFMA,
-// conflict-free).  Only the weight-gradient reductions over the batch rows
-// need the whole agent's activations: those are staged in LDS images and
-// reduced by "neuron owning" waves (4 barriers per agent).
+// conflict-free).  The gradient pass runs "wave owns neurons" (below): each
+// wave keeps its weight slice in registers and the layers exchange
+// activations through LDS images.
 #include <math.h>
 
 #include "common.hpp"
@@ -192,21 +191,6 @@ __device__ void stage_net(const h16 *WH, char *p) {
     for (int j = threadIdx.x; j < 2 * H + NACT; j += nt) bb[j] = WH[L::ob1 + j];
 }
 
-// The backward-only pieces of the online net: W2B and W3R.
-constexpr int W2B_BYTES = W2_BYTES, W3R_BYTES = NACT * H * 2;
-
-__device__ void stage_bwd(const h16 *WH, half8 *w2b, h16 *w3r) {
-    const int nt = blockDim.x;
-    for (int ent = threadIdx.x; ent < 8 * 4 * 64; ent += nt) {
-        const int t = ent / 256, s = (ent / 64) & 3, l = ent & 63, i = l & 15, g = l >> 4;
-        half8 v;
-#pragma unroll
-        for (int e = 0; e < 8; e++) v[e] = WH[L::oW2T + qn_wt(kperm(s, g, e), 16 * t + i, H)];
-        w2b[ent] = v;
-    }
-    for (int k = threadIdx.x; k < NACT * H; k += nt) w3r[k] = WH[L::oW3T + k];
-}
-
 // Diagnostics (tools/stamp_shared.py): when a stamps buffer is passed, lane 0
 // of the wave (next) / thread 0 of the workgroup (grad) writes the phase ends
 // of each agent it handles, s_memrealtime (100 MHz), into stamps[agent][k].
@@ -333,144 +317,6 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
     for (int n = 0; n < NT; n++)
 #pragma unroll
         for (int e = 0; e < 4; e++) q[n][e] = g == 0 ? r16(r16(c[n][e]) + (float)N.b3[e]) : 0.0f;
-}
-
-// One tile, fragments read with (!DB) or one tile ahead of (DB) the tile: hb1 / hb2 = the layer-1 / layer-2
-// activations as next-layer operands (permuted K order); returns Q on the
-// lanes g = 0 (Q[row i][0..3]; other lanes hold zeros).  DB: each output
-// tile's weight fragments are read from LDS one tile ahead (double-buffered,
-// order pinned by scheduling barriers: the LDS latency hides behind the
-// previous tile's MFMAs without the scheduler hoisting every read at once);
-// !DB reads them with the tile (28 fewer VGPRs: the gradient pass, whose
-// accumulators live across the whole launch, would spill).
-template <bool DB>
-__device__ __forceinline__ f32x4 fwd_tile(const Net &N, const half8 bx[3], half8 hb1[4],
-                                          half8 hb2[4]) {
-    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    {
-        half8 cur[3], nxt[3];
-        if (DB)
-#pragma unroll
-            for (int s = 0; s < 3; s++) cur[s] = N.w1[s * 64 + l];
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            if (!DB)
-#pragma unroll
-                for (int s = 0; s < 3; s++) cur[s] = N.w1[(t * 3 + s) * 64 + l];
-            if (DB && t < 7)
-#pragma unroll
-                for (int s = 0; s < 3; s++) nxt[s] = N.w1[((t + 1) * 3 + s) * 64 + l];
-            f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < 3; s++) c = mfma(cur[s], bx[s], c);
-            dense_out(c, N.b1, t, hb1);
-            if (DB)
-#pragma unroll
-                for (int s = 0; s < 3; s++) cur[s] = nxt[s];
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    {
-        half8 cur[4], nxt[4];
-        if (DB)
-#pragma unroll
-            for (int s = 0; s < 4; s++) cur[s] = N.w2[s * 64 + l];
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            if (!DB)
-#pragma unroll
-                for (int s = 0; s < 4; s++) cur[s] = N.w2[(t * 4 + s) * 64 + l];
-            if (DB && t < 7)
-#pragma unroll
-                for (int s = 0; s < 4; s++) nxt[s] = N.w2[((t + 1) * 4 + s) * 64 + l];
-            else if (DB)
-#pragma unroll
-                for (int s = 0; s < 4; s++) nxt[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
-            f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < 4; s++) c = mfma(cur[s], hb1[s], c);
-            dense_out(c, N.b2, t, hb2);
-            if (DB)
-#pragma unroll
-                for (int s = 0; s < 4; s++) cur[s] = nxt[s];
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (!DB)
-#pragma unroll
-            for (int s = 0; s < 4; s++) cur[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; s++) c = mfma(cur[s], hb2[s], c);  // layer 3 (cur = W3 fragments)
-        f32x4 q;
-#pragma unroll
-        for (int e = 0; e < 4; e++) q[e] = g == 0 ? r16(r16(c[e]) + (float)N.b3[e]) : 0.0f;
-        return q;
-    }
-}
-
-// One tile, software-pipelined without a second fragment buffer (the
-// gradient pass: its accumulators live across the whole launch): an output
-// tile's MFMAs issue, then the NEXT tile's weight fragments and bias are read
-// into the registers the MFMAs just consumed, then this tile's bias + relu --
-// the LDS latency hides behind the MFMA drain and the VALU epilogue.  The
-// scheduling barriers pin that order.  Same result as fwd_tiles<1, *>.
-__device__ __forceinline__ f32x4 fwd_tile_pipe(const Net &N, const half8 bx[3], half8 hb1[4],
-                                               half8 hb2[4]) {
-    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    half8 w[4];
-    half4v bias = *reinterpret_cast<const half4v *>(N.b1 + 4 * g);
-#pragma unroll
-    for (int s = 0; s < 3; s++) w[s] = N.w1[s * 64 + l];
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 3; s++) c = mfma(w[s], bx[s], c);
-        __builtin_amdgcn_sched_barrier(0);
-        const half4v bt = bias;
-        if (t < 7) {
-#pragma unroll
-            for (int s = 0; s < 3; s++) w[s] = N.w1[((t + 1) * 3 + s) * 64 + l];
-            bias = *reinterpret_cast<const half4v *>(N.b1 + 16 * (t + 1) + 4 * g);
-        } else {
-#pragma unroll
-            for (int s = 0; s < 4; s++) w[s] = N.w2[s * 64 + l];
-            bias = *reinterpret_cast<const half4v *>(N.b2 + 4 * g);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const half4v z = __builtin_convertvector(c, half4v) + bt;
-#pragma unroll
-        for (int e = 0; e < 4; e++) hb1[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; s++) c = mfma(w[s], hb1[s], c);
-        __builtin_amdgcn_sched_barrier(0);
-        const half4v bt = bias;
-        if (t < 7) {
-#pragma unroll
-            for (int s = 0; s < 4; s++) w[s] = N.w2[((t + 1) * 4 + s) * 64 + l];
-            bias = *reinterpret_cast<const half4v *>(N.b2 + 16 * (t + 1) + 4 * g);
-        } else {
-#pragma unroll
-            for (int s = 0; s < 4; s++) w[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const half4v z = __builtin_convertvector(c, half4v) + bt;
-#pragma unroll
-        for (int e = 0; e < 4; e++) hb2[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; s++) c = mfma(w[s], hb2[s], c);  // layer 3 (w = W3 fragments)
-    f32x4 q;
-#pragma unroll
-    for (int e = 0; e < 4; e++) q[e] = g == 0 ? r16(r16(c[e]) + (float)N.b3[e]) : 0.0f;
-    return q;
 }
 
 // ---------------------------------------------------------------- pass 1: S'
@@ -619,18 +465,6 @@ __global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_
 }
 
 // ---------------------------------------------------------------- pass 2: gradients
-// LDS: online net (forward, W2B, W3R) + H1 / H2 images (reused for dZ1 / X)
-// + DQ image [128][16] + per-row dq / action + loss partials.
-constexpr int OFF_W2B = NET_BYTES;
-constexpr int OFF_W3R = OFF_W2B + W2B_BYTES;
-constexpr int OFF_I1 = OFF_W3R + W3R_BYTES;      // H1, then dZ1   [128][128] f16
-constexpr int OFF_I2 = OFF_I1 + B_ * H * 2;      // H2 -> dZ2, then X [128][96]
-constexpr int OFF_DQ = OFF_I2 + B_ * H * 2;      // [128][16] f16
-constexpr int OFF_SC = OFF_DQ + B_ * 16 * 2;     // dq f32 [128], act int [128], loss [8]
-constexpr int GRAD_LDS = OFF_SC + B_ * 4 + B_ * 4 + 8 * 4;
-static_assert(GRAD_LDS <= 160 * 1024, "k_shared_grad LDS");
-static_assert(OFF_I1 % 16 == 0 && OFF_DQ % 16 == 0, "aligned images");
-
 // Per-row loss term and dL/dq (common.hpp loss_term), rounded as TF's ops.
 __device__ __forceinline__ void row_loss(int kind, float diff, float &term, float &dq) {
 #pragma clang fp contract(off)
@@ -642,353 +476,6 @@ __device__ __forceinline__ void row_loss(int kind, float diff, float &term, floa
         term = diff * diff;
         dq = 2.0f * diff * (1.0f / (float)B_);
     }
-}
-
-struct Pref {  // one row per lane i: the next agent's inputs, in flight
-    XTile x;
-    float y;
-    uint32_t act;
-};
-
-// The row this lane feeds in the row phases (16w + i) of `agent`, whose deque
-// position pos was loaded one agent earlier.
-__device__ __forceinline__ void pref_issue(const dmdqn_learn_args &a, const float *y_in,
-                                           const uint8_t *act_in, int agent, int pos, Pref &p) {
-    const int w = threadIdx.x >> 6, i = threadIdx.x & 15;
-    const int b = 16 * w + i;
-    int s = a.start + pos;
-    if (s >= a.cap) s -= a.cap;
-    x_issue(a.ring_s + ((size_t)agent * a.cap + s) * DMDQN_ROW_BYTES, p.x);
-    p.y = y_in[(size_t)agent * B_ + b];
-    p.act = act_in[(size_t)agent * B_ + b];
-}
-
-__device__ __forceinline__ int pos_of(const dmdqn_learn_args &a, int agent) {
-    return agent < a.NA ? a.idx[(size_t)agent * B_ + 16 * (threadIdx.x >> 6) + (threadIdx.x & 15)]
-                        : 0;
-}
-
-// Tuning switches (tools/build_exp.py + tools/stamp_shared.py, same box, all
-// bit-identical): SH_PIPE_FWD = the forward of fwd_tile_pipe (R.fwd 2.5 ->
-// 2.0 us per agent, but 9 more spilled VGPRs slow W1 by more); SH_PIPE_BWD =
-// the dH1 / dW2 / dW1 fragment reads one step ahead and the dZ2 conversion's
-// reads batched (10.4 -> 9.8 us per agent).
-#ifndef SH_PIPE_FWD
-#define SH_PIPE_FWD 0
-#endif
-#ifndef SH_PIPE_BWD
-#define SH_PIPE_BWD 1
-#endif
-
-template <bool QSTATS>
-__global__ void __launch_bounds__(512, 1) k_shared_grad(dmdqn_learn_args a, const float *y_in,
-                                                        const uint8_t *act_in, float *slab) {
-    __shared__ __attribute__((aligned(16))) char smem[GRAD_LDS];
-    const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
-    stage_net(WH, smem);
-    stage_bwd(WH, reinterpret_cast<half8 *>(smem + OFF_W2B), reinterpret_cast<h16 *>(smem + OFF_W3R));
-    const Net on = net_at(smem);
-    const half8 *w2b = reinterpret_cast<const half8 *>(smem + OFF_W2B);
-    const h16 *w3r = reinterpret_cast<const h16 *>(smem + OFF_W3R);
-    h16 *I1 = reinterpret_cast<h16 *>(smem + OFF_I1), *I2 = reinterpret_cast<h16 *>(smem + OFF_I2);
-    h16 *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
-    float *sdq = reinterpret_cast<float *>(smem + OFF_SC);
-    int *sact = reinterpret_cast<int *>(smem + OFF_SC + B_ * 4);
-    float *sloss = reinterpret_cast<float *>(smem + OFF_SC + 2 * B_ * 4);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    const int row = 16 * w + i;  // this lane's batch row in the row phases
-    half8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
-    // gradient accumulators, across every agent this workgroup walks
-    f32x4 G1[6], G2[8], G3 = {0.f, 0.f, 0.f, 0.f}, GB1 = G3, GB2 = G3, GB3 = G3;
-#pragma unroll
-    for (int t = 0; t < 6; t++) G1[t] = G3;
-#pragma unroll
-    for (int t = 0; t < 8; t++) G2[t] = G3;
-    // DQ image columns 4..15 stay zero
-    for (int k = threadIdx.x; k < B_ * 16; k += 512) DQI[k] = (h16)0.0f;
-    Pref pf;
-    if ((int)blockIdx.x < a.NA) pref_issue(a, y_in, act_in, blockIdx.x, pos_of(a, blockIdx.x), pf);
-    int npos = pos_of(a, blockIdx.x + gridDim.x);  // the next agent's deque position, in flight
-    __syncthreads();
-
-    for (int agent = blockIdx.x; agent < a.NA; agent += gridDim.x) {
-        SH_STAMP(agent, 0, threadIdx.x);
-        // ---- R: rows 16w..16w+15 -- forward, dL/dQ, dZ2, dH1 -> dZ1 in registers
-        half8 bx[3], hb1[4], hb2[4];
-        x_frags(pf.x, bx);
-        const float yv = pf.y;
-        const int av = (int)pf.act;
-#if SH_PIPE_FWD
-        const f32x4 q = fwd_tile_pipe(on, bx, hb1, hb2);
-#else
-        const f32x4 q = fwd_tile<false>(on, bx, hb1, hb2);
-#endif
-        SH_STAMP(agent, 13, threadIdx.x);
-        float term = 0.0f, dq = 0.0f;
-        if (g == 0) {
-            const float qa = av == 0 ? q[0] : av == 1 ? q[1] : av == 2 ? q[2] : q[3];
-            row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
-            dq = r16(dq);  // dL/dQ in f16 (the gradient of the learn's tf.cast)
-            sdq[row] = dq;
-            sact[row] = av;
-            half4v d;
-#pragma unroll
-            for (int e = 0; e < 4; e++) d[e] = e == av ? (h16)dq : (h16)0.0f;
-            *reinterpret_cast<half4v *>(DQI + row * 16) = d;
-        }
-        dq = __shfl(dq, i);
-        // activations into the images (rows of this wave)
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            half4v v1, v2;
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                v1[e] = hb1[t >> 1][4 * (t & 1) + e];
-                v2[e] = hb2[t >> 1][4 * (t & 1) + e];
-            }
-            const int o = hsplit(i, 16 * (t & 1) + 4 * g, w, 0) + 256 * (t >> 1);
-            *reinterpret_cast<half4v *>(I1 + o) = v1;  // [row][16t + 4g]
-            *reinterpret_cast<half4v *>(I2 + o) = v2;
-        }
-        // dZ2 = h16(dq W3[k][a]) where H2 > 0 (operand order of hb2)
-        half8 dz2[4];
-#if SH_PIPE_BWD
-        half8 wb[4];  // dH1's first W2B tile, in flight behind the dZ2 epilogue
-#pragma unroll
-        for (int s = 0; s < 4; s++) wb[s] = w2b[s * 64 + l];
-#endif
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const half4v w3 = *reinterpret_cast<const half4v *>(w3r + av * H + 16 * t + 4 * g);
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const h16 hv = hb2[t >> 1][4 * (t & 1) + e];
-                dz2[t >> 1][4 * (t & 1) + e] = hv > (h16)0.0f ? (h16)(dq * (float)w3[e]) : (h16)0.0f;
-            }
-        }
-        SH_STAMP(agent, 14, threadIdx.x);
-        // dH1^T = W2 dZ2^T -> dZ1 = h16(dH1) where H1 > 0 (operand order of hb1)
-        half8 dz1[4];
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#if SH_PIPE_BWD
-            // MFMAs of tile t, then tile t + 1's fragments into the registers
-            // they consumed, then tile t's mask (fwd_tile_pipe's order)
-#pragma unroll
-            for (int s = 0; s < 4; s++) c = mfma(wb[s], dz2[s], c);
-            __builtin_amdgcn_sched_barrier(0);
-            if (t < 7)
-#pragma unroll
-                for (int s = 0; s < 4; s++) wb[s] = w2b[((t + 1) * 4 + s) * 64 + l];
-            __builtin_amdgcn_sched_barrier(0);
-#else
-#pragma unroll
-            for (int s = 0; s < 4; s++) c = mfma(w2b[(t * 4 + s) * 64 + l], dz2[s], c);
-#endif
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const h16 hv = hb1[t >> 1][4 * (t & 1) + e];
-                dz1[t >> 1][4 * (t & 1) + e] = hv > (h16)0.0f ? (h16)c[e] : (h16)0.0f;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        SH_STAMP(agent, 15, threadIdx.x);
-        // loss of the batch: per wave over its 16 rows, then 8 partials in order
-        {
-            float ls = term;
-            for (int off = 8; off > 0; off >>= 1) ls += __shfl_xor(ls, off);
-            if (l == 0) sloss[w] = ls;
-        }
-        if (QSTATS) {
-            float s1 = g == 0 ? (q[0] + q[1]) + (q[2] + q[3]) : 0.0f;
-            float s2 = g == 0 ? (q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]) : 0.0f;
-            for (int off = 32; off > 0; off >>= 1) {
-                s1 += __shfl_xor(s1, off);
-                s2 += __shfl_xor(s2, off);
-            }
-            if (l == 0) {
-                float *o = a.qstats + (size_t)agent * 6;
-                atomicAdd(o + 0, s1);
-                atomicAdd(o + 1, s2);
-            }
-            if (l < NACT) {
-                const float cnt = (float)__popcll(__ballot(g == 0 && av == l));
-                atomicAdd(a.qstats + (size_t)agent * 6 + 2 + l, cnt);
-            }
-        }
-        SH_STAMP(agent, 1, threadIdx.x);
-        __syncthreads();  // 1: H1, H2, DQ, dq / act of every row
-        SH_STAMP(agent, 2, threadIdx.x);
-        if (threadIdx.x == 0 && a.loss) {
-            float ls = 0.0f;
-            for (int k = 0; k < 8; k++) ls += sloss[k];
-            a.loss[agent] = ls / (float)B_;
-        }
-        // next agent's indices and rows in flight behind the reductions
-        const int nxt = agent + gridDim.x;
-        if (nxt < a.NA) pref_issue(a, y_in, act_in, nxt, npos, pf);
-        npos = pos_of(a, nxt + gridDim.x);
-        // ---- W1: wave w owns fan-out neurons 16w..16w+15 of layers 2 and 3
-        // dW3 (k-tile w) and db3 from H2 (before its slice turns into dZ2)
-#pragma unroll
-        for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 dqf = frag_tr(DQI, 16, b0, 0);
-            G3 = mfma(frag_tr_h(I2, b0, 16 * w), dqf, G3);
-            GB3 = mfma(ones, dqf, GB3);
-        }
-        // this wave's H2 columns -> dZ2 in place (the values dz2 holds above)
-#if SH_PIPE_BWD
-        {  // every read of the four chunks first, then the stores (one LDS round trip)
-            half8 hv[4], w3[4];
-            float dqb[4];
-            int ab[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int b = (l >> 1) + 32 * j;  // [b][16w + 8(l & 1)]
-                hv[j] = *reinterpret_cast<const half8 *>(
-                    I2 + hsplit((l >> 1) & 15, 16 * (w & 1) + 8 * (l & 1), l >> 5, w >> 1) + 16 * H * 2 * j);
-                dqb[j] = sdq[b];
-                ab[j] = sact[b];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                w3[j] = *reinterpret_cast<const half8 *>(w3r + ab[j] * H + 16 * w + 8 * (l & 1));
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                half8 o;
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                    o[e] = hv[j][e] > (h16)0.0f ? (h16)(dqb[j] * (float)w3[j][e]) : (h16)0.0f;
-                *reinterpret_cast<half8 *>(
-                    I2 + hsplit((l >> 1) & 15, 16 * (w & 1) + 8 * (l & 1), l >> 5, w >> 1) + 16 * H * 2 * j) = o;
-            }
-        }
-#else
-        for (int c = l; c < B_ * 2; c += 64) {
-            const int b = c >> 1, k0 = 16 * w + 8 * (c & 1);
-            half8 *p = reinterpret_cast<half8 *>(I2 + hoff(b, k0));
-            const half8 hv = *p;
-            const float dqb = sdq[b];
-            const half8 w3 = *reinterpret_cast<const half8 *>(w3r + sact[b] * H + k0);
-            half8 o;
-#pragma unroll
-            for (int e = 0; e < 8; e++) o[e] = hv[e] > (h16)0.0f ? (h16)(dqb * (float)w3[e]) : (h16)0.0f;
-            *p = o;
-        }
-#endif
-        // dW2 (all fan-in tiles, fan-out slice w) and db2
-        {
-            half8 bq[4];
-#pragma unroll
-            for (int q4 = 0; q4 < 4; q4++) {
-                bq[q4] = frag_tr_h(I2, 32 * q4, 16 * w);
-                GB2 = mfma(ones, bq[q4], GB2);
-            }
-#if SH_PIPE_BWD
-            half8 af[4];  // fan-in tile t's H1 fragments, one tile ahead
-#pragma unroll
-            for (int q4 = 0; q4 < 4; q4++) af[q4] = frag_tr_h(I1, 32 * q4, 0);
-#pragma unroll
-            for (int t = 0; t < 8; t++) {
-                half8 an[4];
-                if (t < 7)
-#pragma unroll
-                    for (int q4 = 0; q4 < 4; q4++) an[q4] = frag_tr_h(I1, 32 * q4, 16 * (t + 1));
-#pragma unroll
-                for (int q4 = 0; q4 < 4; q4++) G2[t] = mfma(af[q4], bq[q4], G2[t]);
-                if (t < 7)
-#pragma unroll
-                    for (int q4 = 0; q4 < 4; q4++) af[q4] = an[q4];
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#else
-#pragma unroll
-            for (int t = 0; t < 8; t++) {
-#pragma unroll
-                for (int q4 = 0; q4 < 4; q4++) G2[t] = mfma(frag_tr_h(I1, 32 * q4, 16 * t), bq[q4], G2[t]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#endif
-        }
-        SH_STAMP(agent, 3, threadIdx.x);
-        __syncthreads();  // 2: H1 and dZ2 consumed
-        SH_STAMP(agent, 4, threadIdx.x);
-        // ---- R2: dZ1 -> I1, X(S) -> I2 (rows of this wave)
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            half4v v;
-#pragma unroll
-            for (int e = 0; e < 4; e++) v[e] = dz1[t >> 1][4 * (t & 1) + e];
-            *reinterpret_cast<half4v *>(
-                I1 + hsplit(i, 16 * (t & 1) + 4 * g, w, 0) + 256 * (t >> 1)) = v;
-        }
-#pragma unroll
-        for (int s = 0; s < 3; s++)  // [row][32s + 8g]
-            *reinterpret_cast<half8 *>(I2 + hsplit<DP>(i, 8 * g, w, 0) + 256 * s) = bx[s];
-        SH_STAMP(agent, 5, threadIdx.x);
-        __syncthreads();  // 3
-        SH_STAMP(agent, 6, threadIdx.x);
-        // ---- W2: wave w owns layer-1 neurons 16w..16w+15: dW1 and db1
-#if SH_PIPE_BWD
-        {
-            half8 bv = frag_tr_h(I1, 0, 16 * w), xa[6];  // batch rows 0..31, then one step ahead
-#pragma unroll
-            for (int t = 0; t < 6; t++) xa[t] = frag_tr_h<DP>(I2, 0, 16 * t);
-#pragma unroll
-            for (int b0 = 0; b0 < B_; b0 += 32) {
-                half8 bn, xn[6];
-                if (b0 + 32 < B_) {
-                    bn = frag_tr_h(I1, b0 + 32, 16 * w);
-#pragma unroll
-                    for (int t = 0; t < 6; t++) xn[t] = frag_tr_h<DP>(I2, b0 + 32, 16 * t);
-                }
-                GB1 = mfma(ones, bv, GB1);
-#pragma unroll
-                for (int t = 0; t < 6; t++) G1[t] = mfma(xa[t], bv, G1[t]);
-                if (b0 + 32 < B_) {
-                    bv = bn;
-#pragma unroll
-                    for (int t = 0; t < 6; t++) xa[t] = xn[t];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-#else
-#pragma unroll
-        for (int b0 = 0; b0 < B_; b0 += 32) {
-            const half8 bv = frag_tr_h(I1, b0, 16 * w);
-            GB1 = mfma(ones, bv, GB1);
-#pragma unroll
-            for (int t = 0; t < 6; t++) G1[t] = mfma(frag_tr_h<DP>(I2, b0, 16 * t), bv, G1[t]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#endif
-        SH_STAMP(agent, 7, threadIdx.x);
-        __syncthreads();  // 4: the images are rewritten by the next agent
-        SH_STAMP(agent, 8, threadIdx.x);
-    }
-    // partial sums of this workgroup, kernel layout (every index written once)
-    float *G = slab + (size_t)blockIdx.x * L::P;
-    if (i < NACT) {
-        *reinterpret_cast<float4 *>(G + L::oW3T + i * H + 16 * w + 4 * g) =
-            make_float4(G3[0], G3[1], G3[2], G3[3]);
-        if (w == 0 && g == 0) G[L::ob3 + i] = GB3[0];
-    }
-#pragma unroll
-    for (int t = 0; t < 8; t++)  // G2[t]: fan-in j = 16t + 4g + e, fan-out k = 16w + i
-        *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(16 * w + i, 16 * t + 4 * g, H)) =
-            make_float4(G2[t][0], G2[t][1], G2[t][2], G2[t][3]);
-    if (g == 0) G[L::ob2 + 16 * w + i] = GB2[0];
-#pragma unroll
-    for (int t = 0; t < 6; t++)
-        if (t < 5 || g < 2)  // tile 5: features 80..87 (89..95 do not exist)
-            *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(16 * w + i, 16 * t + 4 * g)) =
-                make_float4(G1[t][0], G1[t][1], G1[t][2], G1[t][3]);
-    if (g == 0) G[L::ob1 + 16 * w + i] = GB1[0];
-    if (g == 2) G[L::oW1X + 16 * w + i] = G1[5][0];  // feature 88
 }
 
 // ---------------------------------------------------------------- pass 2, v3: neuron-owning
@@ -1486,21 +973,9 @@ int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *s
     const int next_blocks = next_wg < n_slabs ? next_wg : n_slabs;
     hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(64 * NEXT_WAVES), 0, s, *a, y, act);
     DMDQN_LAUNCH_CHECK("k_shared_next");
-    const char *gv = getenv("DMDQN_SHARED_GRAD");  // A/B: "2" = the row-owning pass
-    if (gv && gv[0] == '2') {
-        if (a->qstats)
-            hipLaunchKernelGGL(k_shared_grad<true>, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
-        else
-            hipLaunchKernelGGL(k_shared_grad<false>, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
-        DMDQN_LAUNCH_CHECK("k_shared_grad");
-    } else {
-        // neuron tiles per wave: 2 (4 waves, 512 VGPRs) or 1 (8 waves)
-        const bool nt1 = !(gv && gv[0] == '4');
-        auto k = a->qstats ? (nt1 ? g3::k_shared_grad3<true, 1> : g3::k_shared_grad3<true, 2>)
-                           : (nt1 ? g3::k_shared_grad3<false, 1> : g3::k_shared_grad3<false, 2>);
-        hipLaunchKernelGGL(k, dim3(n_slabs), dim3(nt1 ? 512 : 256), 0, s, *a, y, act, slab);
-        DMDQN_LAUNCH_CHECK("k_shared_grad3");
-    }
+    auto k = a->qstats ? g3::k_shared_grad3<true, 1> : g3::k_shared_grad3<false, 1>;
+    hipLaunchKernelGGL(k, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
+    DMDQN_LAUNCH_CHECK("k_shared_grad3");
     return DMDQN_OK;
 }
 

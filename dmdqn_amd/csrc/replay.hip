@@ -89,7 +89,12 @@ __global__ void k_replay_gather_f32(const float *rows_s, const float *rows_n, co
     const int grp = (int)(t - rowi * G);
     if (rowi >= (size_t)NA * batch) return;
     const int agent = (int)(rowi / batch);
-    int s = start + idx[rowi];
+    int pos = idx[rowi];
+    DMDQN_DBG(pos >= 0 && pos < cap, DBG_LEARN_IDX);  // as the int8 learn's gather
+#ifdef DMDQN_DEBUG_BOUNDS
+    if (pos < 0 || pos >= cap) pos = 0;
+#endif
+    int s = start + pos;
     if (s >= cap) s -= cap;
     const size_t src = ((size_t)agent * cap + s) * DMDQN_ROW_FLOATS;
     reinterpret_cast<float4 *>(xs + rowi * DMDQN_ROW_FLOATS)[grp] =
@@ -97,6 +102,8 @@ __global__ void k_replay_gather_f32(const float *rows_s, const float *rows_n, co
     reinterpret_cast<float4 *>(xn + rowi * DMDQN_ROW_FLOATS)[grp] =
         reinterpret_cast<const float4 *>(rows_n + src)[grp];
 }
+
+DMDQN_DBG_READER(dbg_flags_replay)
 
 }  // namespace dmdqn
 

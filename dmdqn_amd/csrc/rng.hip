@@ -124,24 +124,21 @@ __device__ __forceinline__ uint32_t py_randbelow(MTWave &w, uint32_t n) {
 //   set branch: for i < k: j = randbelow(n), redrawn while j in selected.
 // randbelow(m) = getrandbits(bit_length(m)), redrawn while >= m.
 //
-// One wave per env consumes the env's stream 64 tempered words at a time
-// ("chunk", lane l <-> word mti + l) and decides every word of the chunk at
-// once instead of one dependent LDS round trip per draw:
-//  * pool branch, phase 1: whether a word is accepted depends only on the
-//    word and on m = n - i, never on the pool.  Lane l is accepted iff
-//    getrandbits(bit_length(m - c_l)) < m - c_l, where c_l counts the accepted
-//    lanes below l.  That recurrence is solved by iterating
-//    c <- exclusive popcount(ballot(accepted(c))) from c = 0: each pass makes
-//    at least one more lane exact (lane 0 always is), and a fixed point is the
-//    sequential answer.  Accepted positions j go to LDS, per agent.
-//    Phase 2: every agent's k pool swaps run in parallel, lane = agent, each
-//    on its own u16 pool in LDS (only the swap chain is sequential).
-//  * set branch: out-of-range words and words already selected (LDS bitmap)
-//    are rejected in parallel; a repeat within the chunk is rejected when an
-//    earlier lane holds the same value (LDS first-lane table); positions in
-//    the sample come from the popcount prefix.
-// In both branches the agent whose k-th pick falls inside a chunk consumes
-// the chunk only up to that lane; the next agent starts at the lane after.
+// Pool branch (k_sample): one wave per env consumes the env's stream 64
+// tempered words at a time ("chunk", lane l <-> word mti + l) and decides every
+// word of the chunk at once instead of one dependent LDS round trip per draw.
+// Phase 1: whether a word is accepted depends only on the word and on
+// m = n - i, never on the pool.  Lane l is accepted iff
+// getrandbits(bit_length(m - c_l)) < m - c_l, where c_l counts the accepted
+// lanes below l.  That recurrence is solved by iterating
+// c <- exclusive popcount(ballot(accepted(c))) from c = 0: each pass makes at
+// least one more lane exact (lane 0 always is), and a fixed point is the
+// sequential answer.  Accepted positions j go to LDS, per agent.  Phase 2:
+// every agent's k pool swaps run in parallel, lane = agent, each on its own
+// u16 pool in LDS (only the swap chain is sequential).
+// The set branch is k_sample_set below.  In both, the agent whose k-th pick
+// falls inside a chunk consumes the chunk only up to that word; the next agent
+// starts at the word after.
 __device__ __forceinline__ uint32_t bitlen(uint32_t m) { return 32u - (uint32_t)__clz(m); }
 __device__ __forceinline__ uint32_t getbits(uint32_t u, uint32_t kb) {
     return u >> (32u - kb);  // kb in 1..32
@@ -152,14 +149,14 @@ __device__ __forceinline__ uint64_t lanes_below() {
 }
 
 __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32_t n, int k,
-                                               uint32_t setsize, int tlog, int32_t *idx) {
+                                               int32_t *idx) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *mt = smem, *tmp = smem + MT_N, *aux = smem + 2 * MT_N;
     MTWave w{mt, tmp, 0};
     const int e = blockIdx.x, l = threadIdx.x;
     uint32_t *g = py_state + (size_t)e * DMDQN_MT_WORDS;
     w.load(g);
-    if (n <= setsize) {
+    {
         uint16_t *sel = reinterpret_cast<uint16_t *>(aux);           // [A][k]
         uint16_t *pool = sel + (((size_t)A * k + 1) & ~(size_t)1);  // [min(A,64)][n]
         // ---- phase 1: the stream -> accepted j per (agent, i)
@@ -213,103 +210,6 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
                     o[q] = (int32_t)v;
                     P[x] = last;
                 }
-            }
-            __syncthreads();
-        }
-    } else {
-        uint32_t *bm = aux;  // selected bitmap, n bits
-        const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
-        // first[r & (T-1)]: (r >> tlog) << 7 | lowest word of the current chunk
-        // that drew r (all ones between chunks): the in-chunk repeat test in 3
-        // LDS operations instead of 63 dependent lane shuffles.  T = 2^tlog
-        // entries (<= 32 KB for C3's n = 10000: four sampler blocks per CU, the
-        // 1024 env waves in one round); values r that share a slot resolve in
-        // turn -- the smallest r >> tlog first -- in a wave-uniform loop that
-        // almost always runs once.
-        uint32_t *first = bm + words;
-        const uint32_t tmask = (1u << tlog) - 1u;
-        for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
-        for (uint32_t t = l; t <= tmask + 1u; t += 64) first[t] = 0xffffffffu;
-        __syncthreads();
-        // Two words per lane per iteration (a 128-word chunk, word q = 64h + l):
-        // half the dependent rounds of LDS traffic per drawn index.  Every LDS
-        // access is issued unconditionally (lanes with nothing to do address
-        // the dummy table entry first[T] or OR 0 into bm[0]): one wave's LDS
-        // operations complete in issue order, so each group of reads costs one
-        // wait and no exec-mask branches.
-        constexpr int HW = 2;
-        const uint32_t dummy = tmask + 1u;
-        int j = 0, i = 0;
-        int32_t *out = idx + (size_t)e * A * k;  // agent j's i-th pick
-        while (j < A) {
-            if (w.mti >= MT_N) w.refill();
-            const int cnt = min(64 * HW, MT_N - w.mti);
-            uint32_t r[HW], slot[HW], key[HW], bw[HW];
-            bool inr[HW], cand[HW], dup[HW], pend[HW];
-#pragma unroll
-            for (int h = 0; h < HW; h++) {
-                const int q = 64 * h + l;
-                r[h] = getbits(tmp[w.mti + (q < cnt ? q : 0)], kb);
-                inr[h] = q < cnt && r[h] < n;
-            }
-#pragma unroll
-            for (int h = 0; h < HW; h++) bw[h] = bm[inr[h] ? r[h] >> 5 : 0u];
-#pragma unroll
-            for (int h = 0; h < HW; h++) {
-                cand[h] = inr[h] && !((bw[h] >> (r[h] & 31)) & 1u);
-                slot[h] = cand[h] ? (r[h] & tmask) : dummy;
-                key[h] = cand[h] ? (((r[h] >> tlog) << 7) | (uint32_t)(64 * h + l)) : 0xffffffffu;
-                dup[h] = false;
-                pend[h] = cand[h];
-            }
-            // a repeat of an earlier candidate word in the same chunk is rejected:
-            // the reads see every word's min, the resets follow every read
-            while (__ballot(pend[0] || pend[1])) {
-                uint32_t win[HW], sl[HW];
-#pragma unroll
-                for (int h = 0; h < HW; h++) {
-                    sl[h] = pend[h] ? slot[h] : dummy;
-                    atomicMin(&first[sl[h]], pend[h] ? key[h] : 0xffffffffu);
-                }
-#pragma unroll
-                for (int h = 0; h < HW; h++) win[h] = first[sl[h]];
-#pragma unroll
-                for (int h = 0; h < HW; h++) first[sl[h]] = 0xffffffffu;
-#pragma unroll
-                for (int h = 0; h < HW; h++) {
-                    const bool mine = pend[h] && (win[h] >> 7) == (key[h] >> 7);  // same r
-                    if (mine) dup[h] = win[h] != key[h];
-                    pend[h] = pend[h] && !mine;
-                }
-            }
-            const bool a0 = cand[0] && !dup[0], a1 = cand[1] && !dup[1];
-            const uint64_t acc0 = __ballot(a0), acc1 = __ballot(a1);
-            const int p0 = __popcll(acc0);
-            const int c0 = __popcll(acc0 & lanes_below()), c1 = p0 + __popcll(acc1 & lanes_below());
-            const int total = p0 + __popcll(acc1), need = k - i;
-            int taken = total, consumed = cnt;
-            if (total >= need) {
-                taken = need;
-                if (need <= p0) {
-                    consumed = __ffsll((unsigned long long)__ballot(a0 && c0 == need - 1));
-                } else {
-                    consumed = 64 + __ffsll((unsigned long long)__ballot(a1 && c1 == need - 1));
-                }
-            }
-            const bool t0 = a0 && c0 < taken, t1 = a1 && c1 < taken;
-            DMDQN_DBG(!t0 || r[0] < n, DBG_SAMPLE);
-            DMDQN_DBG(!t1 || r[1] < n, DBG_SAMPLE);
-            if (t0) out[i + c0] = (int32_t)r[0];
-            if (t1) out[i + c1] = (int32_t)r[1];
-            atomicOr(&bm[t0 ? r[0] >> 5 : 0u], t0 ? 1u << (r[0] & 31) : 0u);
-            atomicOr(&bm[t1 ? r[1] >> 5 : 0u], t1 ? 1u << (r[1] & 31) : 0u);
-            w.mti += consumed;
-            i += taken;
-            if (i == k) {
-                j++;
-                i = 0;
-                out += k;
-                for (uint32_t t = l; t < words; t += 64) bm[t] = 0u;
             }
             __syncthreads();
         }
@@ -510,29 +410,26 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
     size_t lds = 2 * MT_N * sizeof(uint32_t) + aux_bytes;
     // set branch: the first-lane table, 2^tlog u32 entries: no more than n
     // needs, within 39 KB per block in all (four blocks per CU) when that
-    // leaves at least 4 KB for it, else up to 32 KB; DMDQN_SAMPLE_TLOG caps it
-    // (tests: collisions in every chunk)
+    // leaves at least 4 KB for it, else up to 32 KB; DMDQN_OPT_SAMPLE_TLOG caps
+    // it (tests: collisions in every chunk)
     int tlog = 0;
     if (!pool) {
         const size_t quad = 39 * 1024;
         const size_t room = (quad >= lds + 4096 + 4) ? quad - lds - 4 : 32 * 1024;
         while (tlog < 20 && ((size_t)4 << (tlog + 1)) <= room && (1u << tlog) < (uint32_t)n) tlog++;
-        const char *cap = getenv("DMDQN_SAMPLE_TLOG");
-        if (cap && atoi(cap) >= 0 && atoi(cap) < tlog) tlog = atoi(cap);
+        const int cap = option(DMDQN_OPT_SAMPLE_TLOG);
+        if (cap < tlog) tlog = cap;
         lds += ((size_t)4 << tlog) + 4;  // + the dummy entry first[T]
     }
     DMDQN_REQUIRE(lds <= 160 * 1024, "dmdqn_replay_sample: n=%d too large for LDS", n);
-    // set branch: four waves per stream (k_sample_set); DMDQN_SAMPLE_WAVES=1
-    // keeps the one-wave kernel (A/B)
-    const char *sw = getenv("DMDQN_SAMPLE_WAVES");
-    if (!pool && !(sw && atoi(sw) == 1)) {
+    if (!pool) {  // set branch: four waves per stream
         hipLaunchKernelGGL(k_sample_set<4>, dim3(E), dim3(256), lds, as_stream(stream), py_state, A,
                            (uint32_t)n, k, tlog, idx);
         DMDQN_LAUNCH_CHECK("k_sample_set");
         return DMDQN_OK;
     }
     hipLaunchKernelGGL(k_sample, dim3(E), dim3(64), lds, as_stream(stream), py_state, A,
-                       (uint32_t)n, k, setsize, tlog, idx);
+                       (uint32_t)n, k, idx);
     DMDQN_LAUNCH_CHECK("k_sample");
     return DMDQN_OK;
 }

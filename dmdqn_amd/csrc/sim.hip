@@ -1549,14 +1549,14 @@ static int launch_sim(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t 
     // four per CU), else the register path when a block can own every lane
     // (8x8: 0.22 ms vs 0.45 ms on global memory; its 139 KB image would run one
     // block per CU), else the LDS image if it fits at all, else global memory.
-    // DMDQN_SIM_PATH=reg|lds|global forces one (A/B, tests).
-    const char *force = getenv("DMDQN_SIM_PATH");
+    // DMDQN_OPT_SIM_PATH (1 reg, 2 lds, 3 global) forces one (A/B, tests).
+    const int force = option(DMDQN_OPT_SIM_PATH);
     const bool reg_ok = NL <= 1024 && sim->cap_lane <= RCAP;
     bool use_reg = !lds_2cu && reg_ok;
     bool use_lds = fits_lds && !use_reg;
-    if (force && !strcmp(force, "reg")) { use_reg = reg_ok; use_lds = !reg_ok && fits_lds; }
-    if (force && !strcmp(force, "lds")) { use_reg = false; use_lds = fits_lds; }
-    if (force && !strcmp(force, "global")) { use_reg = false; use_lds = false; }
+    if (force == 1) { use_reg = reg_ok; use_lds = !reg_ok && fits_lds; }
+    if (force == 2) { use_reg = false; use_lds = fits_lds; }
+    if (force == 3) { use_reg = false; use_lds = false; }
     const dmdqn_env_fuse f = F ? *F : dmdqn_env_fuse{};
     if (use_reg) {
         const int nt = NL <= 256 ? 256 : NL <= 512 ? 512 : 1024;

@@ -6,7 +6,14 @@ global env id, and runs with NO data-path collectives.  Collectives appear only
 (a) outside timed regions (barrier, max-over-ranks timing) and (b) in the
 shared-parameter DQN configuration (C5), where the flat f32 gradient is
 all-reduced and averaged (`allreduce_mean_`).
+
+Every collective call here is bounded: init_process_group gets a timeout (the
+rendezvous and the backend's own operations), and barrier / max_over_ranks
+wait on their work with a timeout.  A failure raises DistError naming the rank
+and the call, so a first-time RCCL problem ends the run with a cause instead of
+hanging to an outer limit.  DMDQN_DIST_TIMEOUT_S overrides the default.
 """
+import datetime
 import os
 
 import numpy as np
@@ -20,15 +27,44 @@ def world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend=None, device=None):
+DEFAULT_TIMEOUT_S = float(os.environ.get("DMDQN_DIST_TIMEOUT_S", "180"))
+
+
+class DistError(RuntimeError):
+    """A collective failed or timed out (the message names rank and call)."""
+
+
+def _td(timeout_s):
+    return datetime.timedelta(seconds=DEFAULT_TIMEOUT_S if timeout_s is None else timeout_s)
+
+
+def _fail(call, exc):
+    raise DistError(f"rank {world()[0]} of {world()[1]}: {call} failed: "
+                    f"{type(exc).__name__}: {exc}") from exc
+
+
+def init(backend=None, device=None, timeout_s=None):
+    """init_process_group from the torch.distributed.run environment, with a
+    timeout (rendezvous and the backend's operations); raises DistError."""
     rank, ws, local = world()
     if ws > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
-        dist.init_process_group(backend, **kw)
+        try:
+            dist.init_process_group(backend, timeout=_td(timeout_s), **kw)
+        except Exception as e:  # noqa: BLE001 -- any failure is reported with its cause
+            _fail(f"init_process_group({backend}, MASTER_ADDR="
+                  f"{os.environ.get('MASTER_ADDR')}, MASTER_PORT={os.environ.get('MASTER_PORT')})", e)
     return rank, ws, local
+
+
+def _wait(work, call, timeout_s):
+    try:
+        work.wait(timeout=_td(timeout_s))
+    except Exception as e:  # noqa: BLE001
+        _fail(call, e)
 
 
 def shard(rank, envs_per_rank, base_seed=0):
@@ -38,19 +74,28 @@ def shard(rank, envs_per_rank, base_seed=0):
     return offset, ids + base_seed
 
 
-def barrier():
+def barrier(timeout_s=None):
+    """All ranks meet, within the timeout (DistError otherwise)."""
     if dist.is_initialized():
-        dist.barrier()
+        try:
+            work = dist.barrier(async_op=True)
+        except Exception as e:  # noqa: BLE001
+            _fail("barrier", e)
+        _wait(work, "barrier", timeout_s)
 
 
-def max_over_ranks(x: float, device="cpu"):
+def max_over_ranks(x: float, device="cpu", timeout_s=None):
     """Slowest rank's value (the job's wall time)."""
     if not dist.is_initialized():
         return float(x)
     if dist.get_backend() == "gloo":
         device = "cpu"
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    try:
+        work = dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True)
+    except Exception as e:  # noqa: BLE001
+        _fail("all_reduce(MAX) of the timed region", e)
+    _wait(work, "all_reduce(MAX) of the timed region", timeout_s)
     return float(t.item())
 
 

@@ -88,8 +88,14 @@ class EnvConfig:
 class TrafficEnv:
     """E replicas of the grid on one device.  All state lives in device memory."""
 
-    def __init__(self, cfg: EnvConfig = None, device="cuda"):
+    def __init__(self, cfg: EnvConfig = None, device="cuda", auto_restart=True):
+        """auto_restart (only matters when the demand drains before
+        max_sim_time): step() restarts each replica whose episode ended (the
+        Trainer's loop); False leaves an ended replica as it ended until the
+        caller's reset() (the single-replica SumoTrafficEnvironment surface,
+        sumo_env.py:420-489, whose caller reloads)."""
         self.cfg = cfg = cfg or EnvConfig()
+        self.auto_restart = auto_restart
         if cfg.signal_features not in SIGNAL_MODES:
             raise ValueError(f"signal_features must be one of {list(SIGNAL_MODES)}")
         self._ops = load_ops()
@@ -179,20 +185,29 @@ class TrafficEnv:
         self._local0, self._obs0 = self.local[0].clone(), self.obs[0].clone()
         return self.obs
 
+    def _t0(self):
+        """The t0 argument of the sim launches.  Every launch passes t_env, so
+        the kernel runs each replica from its own clock and ignores t0; the host
+        clock self.t is the shared clock of the lockstep mode only (it stays 0
+        when replicas restart on their own, so it cannot outgrow int32)."""
+        return 0 if self.drains_early else self.t
+
     def advance(self):
         """K substeps for every replica with the signals running their program
         (no setPhase, no observation): the sim launch alone.  Diagnostics only
         (bench.py times k_sim_step with it); a training loop calls step()."""
         cfg = self.cfg
         self._ops.sim_step(self._sim_state, self._sim_tables, self._sim_dims, self._idm, None,
-                           cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time,
+                           cfg.action_stride, self._t0(), cfg.step_duration, cfg.max_sim_time,
                            self.halt, self.phase, self.tspent, self.done_u8)
-        self.t += cfg.step_duration
+        if not self.drains_early:
+            self.t += cfg.step_duration
 
-    def step(self, actions):
+    def step(self, actions, restart=None):
         """One RL step for all replicas (train.py:225-270).
         actions int32 [E,A] on the device.  Returns (obs', reward, done, info):
-        reward [E,A] f64 is computed from the PRE-step local state (A-3)."""
+        reward [E,A] f64 is computed from the PRE-step local state (A-3).
+        restart: overrides auto_restart for this step."""
         if self.local is None:
             raise RuntimeError("call reset() first")
         if actions.dtype != torch.int32 or tuple(actions.shape) != (self.E, self.A):
@@ -201,14 +216,14 @@ class TrafficEnv:
         if self.sim_hook:
             self.sim_hook(True)
         self._ops.sim_step(self._sim_state, self._sim_tables, self._sim_dims, self._idm, actions,
-                           cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time,
+                           cfg.action_stride, self._t0(), cfg.step_duration, cfg.max_sim_time,
                            self.halt, self.phase, self.tspent, self.done_u8)
         if self.sim_hook:
             self.sim_hook(False)
         prev = self.local
         local, obs, reward = K.observe(self.R, self.C, self.halt, self.phase, self.tspent,
                                        self.mode, prev_local=prev)
-        return self._finish_step(local, obs, reward)
+        return self._finish_step(local, obs, reward, restart)
 
     def step_fused(self, np_state, eps, greedy, actions, ring, obs_s, n_actions=4):
         """act + step + remember of one loop iteration in ONE launch per replica
@@ -230,7 +245,7 @@ class TrafficEnv:
         if self.sim_hook:
             self.sim_hook(True)
         self._ops.env_step(self._sim_state, self._sim_tables, self._sim_dims, self._idm,
-                           cfg.action_stride, self.t, cfg.step_duration, cfg.max_sim_time,
+                           cfg.action_stride, self._t0(), cfg.step_duration, cfg.max_sim_time,
                            self.halt, self.phase, self.tspent, self.done_u8, np_state, greedy,
                            actions, float(eps), int(n_actions), self.mode, local, obs, self.local,
                            reward, obs_s, ring.total % ring.cap, ring.s, ring.n, ring.a, ring.r,
@@ -239,41 +254,58 @@ class TrafficEnv:
             self.sim_hook(False)
         return self._finish_step(local, obs, reward)
 
-    def _finish_step(self, local, obs, reward):
+    def _finish_step(self, local, obs, reward, restart=None):
         cfg = self.cfg
-        self.t += cfg.step_duration
+        restart = self.auto_restart if restart is None else restart
         self.local, self.obs = local, obs
-        info = {"simulation_time": float(self.t), "done_flags": self.done_u8}
         if self.drains_early:
             # the reference rule per replica (done_u8, from the last substep):
-            # the transition of replica e carries its own flag, and a replica
-            # whose episode ended restarts now, alone (train.py:188-207);
+            # the transition of replica e carries its own flag, and (restart) a
+            # replica whose episode ended restarts now, alone (train.py:188-207);
             # info["obs_next"] is what the next act sees (the restart state for
             # those replicas).  `done` is True when every replica ended at this
-            # step -- for E = 1, train.py's `while not done` exactly.
-            flags = self.done_u8.cpu().numpy().astype(bool)
-            info["done"] = self.done_u8.clone()
+            # step -- for E = 1, train.py's `while not done` exactly.  One sync
+            # reads the flags and the replicas' clocks together.
+            both = torch.cat([self.done_u8.to(torch.int32), self.t_env]).cpu().numpy()
+            flags, clock = both[:self.E].astype(bool), both[self.E:]
+            info = {"simulation_time": float(clock.max()), "t_env": clock,
+                    "done_flags": self.done_u8, "done": self.done_u8.clone()}
             self.env_steps += 1
             done = bool(flags.all())
             obs_next = self.obs
+            restarted = flags if restart else np.zeros_like(flags)
             if flags.any():
+                # the ended episodes' counters [E,4] (inserted, arrived, running,
+                # pending) before any restart clears them
+                info["final_stats"] = self.t_stats.clone()
+                self.env_episodes[flags] += 1
+            if restarted.any():
                 self._ops.sim_reset(self._sim_state, self._sim_tables, self._sim_dims,
                                     info["done"])
                 m = info["done"].bool().view(self.E, 1, 1)
                 self.local = torch.where(m, self._local0, self.local)
                 obs_next = torch.where(m, self._obs0, self.obs)
-                self.env_episodes[flags] += 1
                 self.env_steps[flags] = 0
             info["obs_next"] = obs_next
-            info["restarted"] = flags
+            info["restarted"] = restarted
         else:
             # shared clock and demand horizon: `done` is uniform and known on
             # the host without a device sync
-            done = info["done"] = self.t >= cfg.max_sim_time
+            self.t += cfg.step_duration
+            done = self.t >= cfg.max_sim_time
+            info = {"simulation_time": float(self.t), "done_flags": self.done_u8, "done": done}
             self.env_steps += 1
             if done:
                 self.env_episodes += 1
         return self.obs, reward, done, info
+
+    def termination_reason(self, e=0):
+        """sumo_env.py:483-487 for replica e after a step that ended its
+        episode: "sumo_halted" when no vehicle is running or pending
+        (_is_episode_done_sumo, :681-692; checked first, as there), else
+        "max_time_reached".  Reads the replica's counters (syncs)."""
+        st = self.t_stats[e].cpu().numpy()
+        return "sumo_halted" if int(st[2]) + int(st[3]) == 0 else "max_time_reached"
 
     def stats(self):
         """[E,4] inserted, arrived, running, pending (syncs)."""
@@ -293,21 +325,25 @@ class TrafficEnv:
         pass
 
     def reset_dict(self):
-        """SumoTrafficEnvironment.reset (sumo_env.py:420) for E = 1."""
+        """SumoTrafficEnvironment.reset (sumo_env.py:420) for E = 1: {id: obs}."""
+        if self.E != 1:
+            raise ValueError("reset_dict is the single-replica API (num_envs == 1)")
         obs = self.reset()[0].cpu().numpy()
         return {j: obs[a] for a, j in enumerate(self.grid.junction_ids)}
 
     def step_dict(self, actions):
-        """SumoTrafficEnvironment.step (sumo_env.py:434) for E = 1, train.py semantics."""
+        """SumoTrafficEnvironment.step (sumo_env.py:434-489) for E = 1 with
+        train.py's semantics: {id: action} -> ({id: obs}, {id: reward}, done,
+        info).  An ended episode stays ended (no restart) until reset_dict();
+        info["termination_reason"] as the reference sets it."""
         if self.E != 1:
             raise ValueError("step_dict is the single-replica API (num_envs == 1)")
-        a = torch.tensor([[int(actions[j]) for j in self.grid.junction_ids]], dtype=torch.int32,
-                         device=self.device)
-        obs, rew, done, info = self.step(a)
-        obs, rew = obs[0].cpu().numpy(), rew[0].cpu().numpy()
         ids = self.grid.junction_ids
-        info = {"simulation_time": float(self.t)}
+        a = torch.tensor([[int(actions[j]) for j in ids]], dtype=torch.int32, device=self.device)
+        obs, rew, done, info = self.step(a, restart=False)
+        obs, rew = obs[0].cpu().numpy(), rew[0].cpu().numpy()
+        out = {"simulation_time": info["simulation_time"]}
         if done:
-            info["termination_reason"] = "max_time_reached"
+            out["termination_reason"] = self.termination_reason(0)
         return ({j: obs[a] for a, j in enumerate(ids)}, {j: float(rew[a]) for a, j in enumerate(ids)},
-                bool(done), info)
+                bool(done), out)

@@ -187,6 +187,7 @@ class ReplayRing:
         if self._err_events is None:
             self._err_events = torch.cuda.Event()
             self._err_live = False
+        stream = torch.cuda.current_stream(self.device)  # the ring's device, not the current one
         ev = self._err_events
         if self._err_live:
             t0 = time.perf_counter()
@@ -194,7 +195,7 @@ class ReplayRing:
             POLL_WAIT_S[0] += time.perf_counter() - t0
             if int(self.err[0]) != 0:
                 raise _lib.DmdqnError(_RANGE_MSG)
-        ev.record()
+        ev.record(stream)
         self._err_live = True
 
 

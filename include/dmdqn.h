@@ -64,6 +64,24 @@ int dmdqn_version(void);
 int dmdqn_debug_status(void);
 int dmdqn_debug_build(void);
 
+/* Run-time options: the test / A-B hooks of the launchers.  Each is read from
+ * the environment ONCE, when the library loads, and changes afterwards only
+ * through dmdqn_set_option (no launch reads the environment):
+ *   DMDQN_OPT_SIM_PATH (env DMDQN_SIM_PATH = reg | lds | global): force the
+ *     simulator's kernel path; 0 = auto (the launcher's choice by grid size),
+ *     1 = register lanes, 2 = LDS image, 3 = global memory.
+ *   DMDQN_OPT_SAMPLE_TLOG (env DMDQN_SAMPLE_TLOG = n): cap the replay
+ *     sampler's first-lane table at 2^n entries, 0 <= n <= 20 (forces
+ *     collisions); 32 = no cap (default).
+ * dmdqn_set_option returns 0 or DMDQN_EINVAL (unknown option or value);
+ * dmdqn_get_option returns the current value (DMDQN_EINVAL for an unknown
+ * option).  Neither is synchronised with launches issued by other host
+ * threads. */
+#define DMDQN_OPT_SIM_PATH 0
+#define DMDQN_OPT_SAMPLE_TLOG 1
+int dmdqn_set_option(int option, int value);
+int dmdqn_get_option(int option);
+
 /* A HIP stream (returned in *stream as hipStream_t) whose kernels run only on
  * the CUs set in mask[n_words] (CU i = bit i % 32 of word i / 32).  The
  * trainer's optional split schedule runs the next step's act / sim / observe /
@@ -382,8 +400,7 @@ int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, int pr
  * (one workgroup per CU: n_slabs = 256 on MI355X).  precision must be 1.
  * work: device scratch of dmdqn_learn_shared_work_bytes(NA) bytes (each batch
  * row's TD target and action between the kernel's two passes: the S' pass
- * with both nets resident in LDS, then the gradient pass); NULL runs the
- * older one-pass kernel (one agent at a time per workgroup). */
+ * with both nets resident in LDS, then the gradient pass); required. */
 int dmdqn_learn_shared_grad(const dmdqn_learn_args *args, float *slab, int n_slabs, float *grad,
                             float scale, void *work, void *stream);
 size_t dmdqn_learn_shared_work_bytes(int NA);

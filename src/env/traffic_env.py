@@ -8,8 +8,10 @@ on the GPU; see dmdqn_amd/env.py for the implementation.
 
 Surfaces:
   TrafficEnv(cfg).reset() / .step(actions[E,A])        batched device tensors
-  TrafficEnv(cfg).reset_dict() / .step_dict({id: a})   SumoTrafficEnvironment-style
+  TrafficEnv(cfg).reset_dict() / .step_dict({id: a})   the same, one replica, dicts
   get_controlled_intersection_ids / get_state_size / get_action_size / close_sumo
+The reference's class surface under its own name and constructor is
+src/agents/sumo_env.py:SumoTrafficEnvironment.
 """
 import yaml
 

@@ -43,7 +43,8 @@ def test_python_bindings_cover_header(lib):
     from dmdqn_amd import _lib, agent, env, ops  # noqa: F401  (agent registers its signatures)
     declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version", "dmdqn_debug_status",
                                    "dmdqn_debug_build", "dmdqn_learn_shared_work_bytes"}
-    host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy"}
+    host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy", "dmdqn_set_option",
+                 "dmdqn_get_option"}
     assert declared - host_only <= set(ops.ENTRY_POINTS), sorted(declared - host_only -
                                                                  set(ops.ENTRY_POINTS))
     ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_reset_envs", "dmdqn_sim_step",
@@ -130,3 +131,23 @@ def test_learn_args_layout_matches_header(tmp_path):
                                           check=True).stdout.split()]
     assert got[0] == ctypes.sizeof(CLearn)
     assert got[1:] == [getattr(CLearn, f).offset for f in fields]
+
+
+def test_options_read_once_not_per_launch(lib):
+    """The launchers' test / A-B hooks (DMDQN_OPT_*) are read from the
+    environment once at load (capi.cpp) and set through dmdqn_set_option: no
+    other source calls getenv, so a stray variable cannot switch a launch."""
+    csrc = os.path.join(ROOT, "dmdqn_amd", "csrc")
+    for f in os.listdir(csrc):
+        txt = open(os.path.join(csrc, f)).read()
+        if f != "capi.cpp":
+            assert "getenv" not in txt, f
+    from dmdqn_amd import _lib
+    with _lib.option("sim_path", "reg"):
+        assert lib.dmdqn_get_option(0) == 1
+        with _lib.option("sample_tlog", 3):
+            assert lib.dmdqn_get_option(1) == 3
+        assert lib.dmdqn_get_option(1) == 32
+    assert lib.dmdqn_get_option(0) == 0
+    assert lib.dmdqn_set_option(0, 7) == -1 and lib.dmdqn_set_option(5, 0) == -1
+    assert lib.dmdqn_set_option(1, 21) == -1 and lib.dmdqn_get_option(1) == 32

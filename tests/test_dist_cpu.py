@@ -110,3 +110,64 @@ def test_shared_param_gradient_allreduce_two_ranks():
         assert np.allclose(seen["grad"], expect)       # identical on every rank
         assert np.isclose(seen["gscale"], 1 / ws)      # mean over ranks in Adam
         assert seen["sync"] == 1
+
+
+def _lonely_rank(port, q):
+    """Rank 0 of a world of 2 whose rank 1 never starts."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                      WORLD_SIZE="2", LOCAL_RANK="0")
+    from dmdqn_amd import dist as D
+    t0 = time.time()
+    try:
+        D.init(backend="gloo", timeout_s=4)
+        q.put(("joined", time.time() - t0))
+    except D.DistError as e:
+        q.put((str(e), time.time() - t0))
+
+
+def _stalled_peer(rank, port, q):
+    """Both ranks join; rank 1 then never reaches the barrier."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE="2", LOCAL_RANK=str(rank))
+    from dmdqn_amd import dist as D
+    D.init(backend="gloo", timeout_s=4)
+    if rank == 1:
+        time.sleep(30)
+        return
+    t0 = time.time()
+    try:
+        D.barrier(timeout_s=4)
+        q.put(("passed", time.time() - t0))
+    except D.DistError as e:
+        q.put((str(e), time.time() - t0))
+
+
+def test_missing_rank_fails_fast_with_its_cause():
+    """A rank that never joins: init_process_group raises DistError naming
+    the rank and the call within its timeout (the driver's multi-GPU run
+    then exits non-zero instead of hanging to the driver's limit)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_lonely_rank, args=(_free_port(), q))
+    p.start()
+    msg, dt = q.get(timeout=90)
+    p.join(timeout=30)
+    assert msg.startswith("rank 0 of 2: init_process_group(gloo"), msg
+    assert dt < 60, dt
+
+
+def test_stalled_barrier_fails_fast_with_its_cause():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_stalled_peer, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    msg, dt = q.get(timeout=90)
+    for p in ps:  # rank 1 is still asleep
+        p.kill()
+        p.join(timeout=30)
+    assert msg.startswith("rank 0 of 2: barrier failed"), msg
+    assert dt < 30, dt

@@ -148,8 +148,8 @@ def test_fixed_and_dqn_modes_and_cli(tmp_path):
 
 def test_resume_refuses_a_different_configuration(tmp_path):
     """checkpoint.load validates every config field that fixes the state's
-    layout or meaning (ADVICE r1): precision, replay size, loss, grid, seeds,
-    actuated mode ... and refuses a replay-less checkpoint of a filled ring."""
+    layout or meaning (ADVICE r1, r3): precision, replay size, loss, grid, seeds,
+    actuated mode, replay row format ... and refuses a replay-less checkpoint of a filled ring."""
     tr = _trainer("fp16")
     _run(tr, 130)
     path = os.path.join(str(tmp_path), "ck.pt")
@@ -165,6 +165,8 @@ def test_resume_refuses_a_different_configuration(tmp_path):
         (EnvConfig(rows=2, cols=2, num_envs=4, seed=6), dict(precision="fp16"), "seed"),
         (EnvConfig(rows=2, cols=2, num_envs=4, seed=5, actuated=True), dict(precision="fp16"),
          "actuated"),
+        (EnvConfig(rows=2, cols=2, num_envs=4, seed=5), dict(precision="fp16", replay_rows="f32"),
+         "replay_rows"),
     ]
     for env_cfg, agent_kw, field in bad:
         kw = dict(replay_buffer_size=300, target_update_frequency=7, seed=3)

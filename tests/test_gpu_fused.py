@@ -66,8 +66,8 @@ def _compare(ref, fus, a, b):
 
 @pytest.mark.parametrize("path", ["lds", "reg", "global"])
 @pytest.mark.parametrize("rows,cols", [(1, 1), (2, 2), (3, 3)])
-def test_fused_step_matches_four_launches(monkeypatch, path, rows, cols):
-    monkeypatch.setenv("DMDQN_SIM_PATH", path)
+def test_fused_step_matches_four_launches(lib_option, path, rows, cols):
+    lib_option("sim_path", path)
     ref, fus = _trainer(False, rows, cols), _trainer(True, rows, cols)
     a, b = _run(ref, 140), _run(fus, 140)  # episodes of 40 steps; learns from step 128
     _compare(ref, fus, a, b)

@@ -85,10 +85,10 @@ def test_replay_sample_shapes(A, n, k):
 
 
 @pytest.mark.parametrize("tlog", [0, 3, 6, 10])
-def test_replay_sample_table_collisions(tlog, monkeypatch):
+def test_replay_sample_table_collisions(tlog, lib_option):
     """Set branch with the first-lane table capped at 2^tlog entries: values
     sharing a slot (r = r' mod 2^tlog) in almost every chunk resolve in turn."""
-    monkeypatch.setenv("DMDQN_SAMPLE_TLOG", str(tlog))
+    lib_option("sample_tlog", tlog)
     seeds = [8, 9]
     st = K.seed_streams(seeds, "py")
     refs = [O.py_stream(s) for s in seeds]

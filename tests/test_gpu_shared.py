@@ -26,17 +26,24 @@ from test_gpu_learn import _fill, _host_batch, _mixed_emulation  # noqa: E402
 DEV = "cuda"
 
 
-def _shared(E, A, freq=500, seed=7):
-    cfg = AgentConfig(replay_buffer_size=300, target_update_frequency=freq, seed=seed,
+def _shared(E, A, freq=500, seed=7, cap=300):
+    cfg = AgentConfig(replay_buffer_size=cap, target_update_frequency=freq, seed=seed,
                       precision="fp16", shared_params=True)
     return BatchedDQN(E, A, cfg)
 
 
-def test_shared_gradient_is_mean_of_agent_gradients():
-    ag = _shared(3, 4)
+@pytest.mark.parametrize("cap,fill", [(300, 200), (300, 330), (1100, 1160)])
+def test_shared_gradient_is_mean_of_agent_gradients(cap, fill):
+    """(300, 200): a partly filled ring (start 0, the sampler's pool branch);
+    (300, 330): a wrapped ring, deque position 0 at slot 30 (the ring-slot
+    arithmetic of both shared passes, learn_shared.hip ring_slot / xrows_issue);
+    (1100, 1160): wrapped at n = 1100 > 1045, the sampler's set branch -- the
+    regime every steady-state C5 step runs in (dqn_agent.py:29, 59-85)."""
+    ag = _shared(3, 4, cap=cap)
     assert ag.params.shape[0] == 1 and ag.NA == 12
     rng = np.random.RandomState(4)
-    _fill(ag, 200, rng)
+    _fill(ag, fill, rng)
+    assert ag.ring.start == max(0, fill - cap) and len(ag.ring) == min(fill, cap)
     p0 = ag.keras_params("params")[0].copy()
     t0 = ag.keras_params("target")[0].copy()
     loss = ag.learn().cpu().numpy()

@@ -7,6 +7,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import oracle as O  # noqa: E402
+from dmdqn_amd import _lib  # noqa: E402
 from dmdqn_amd.env import EnvConfig, TrafficEnv  # noqa: E402
 
 
@@ -14,8 +15,8 @@ def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_a
          scenario=None, actuated=False, action_fn=None, path_at=None, period_ms=None):
     """Step E replicas through the HIP sim and the oracle side by side.
     action_fn(step, rng) -> [E, A] actions (default: uniform random);
-    path_at {step: "reg" | "lds" | "global"} switches DMDQN_SIM_PATH before
-    that step (the kernel reads it per launch)."""
+    path_at {step: "reg" | "lds" | "global"} forces the sim path
+    (_lib.set_option "sim_path") before that step."""
     import os
     max_cnt = 0
     cfg = EnvConfig(rows=R, cols=C, num_envs=E, seed=seed, signal_features=mode,
@@ -38,7 +39,7 @@ def _run(R, C, E, steps, mode="reference", seed=100, check_every=1, full_state_a
     t = 0
     for step in range(steps):
         if path_at and step in path_at:
-            os.environ["DMDQN_SIM_PATH"] = path_at[step]
+            _lib.set_option("sim_path", path_at[step])
         acts = (action_fn(step, rng) if action_fn else
                 rng.randint(0, 4, size=(E, A))).astype(np.int32)
         obs, rew, done, info = env.step(torch.from_numpy(acts).cuda())
@@ -146,14 +147,14 @@ def test_sim_actuated_shipped_scenario():
          scenario=os.path.join(GOLDEN, "grid_3x3_p06_scenario.npz"))
 
 
-def test_lds_image_long_queues_and_path_switches(monkeypatch):
+def test_lds_image_long_queues_and_path_switches(lib_option):
     """The LDS image keeps each lane's first 12 positions in LDS and the rest
     in HBM, lanes compacted.  Heavy demand with the signals held (phase 0 only:
     the E-W approaches queue to capacity) drives lanes past 12 vehicles; the
     path changes mid-episode (global rings with a rotated head -> LDS image,
     which compacts them -> register lanes -> LDS image), bit-exact vs the
     oracle throughout."""
-    monkeypatch.setenv("DMDQN_SIM_PATH", "global")
+    lib_option("sim_path", "global")  # restored after the test (path_at switches it)
     hold = lambda step, rng: np.zeros((3, 16))  # noqa: E731
     env = _run(4, 4, E=3, steps=90, check_every=5, full_state_at=(29, 30, 59, 60),
                action_fn=hold, period_ms=150,
@@ -163,11 +164,11 @@ def test_lds_image_long_queues_and_path_switches(monkeypatch):
 
 @pytest.mark.parametrize("path", ["reg", "lds", "global"])
 @pytest.mark.parametrize("grid", [(3, 3), (4, 4)])
-def test_every_sim_path_matches_oracle(grid, path, monkeypatch):
+def test_every_sim_path_matches_oracle(grid, path, lib_option):
     """All three kernel paths (register lanes, LDS image, global memory; the
-    launcher picks one by grid size, DMDQN_SIM_PATH forces it) are bit-exact,
+    launcher picks one by grid size, the sim_path option forces it) are bit-exact,
     actuated mode included."""
-    monkeypatch.setenv("DMDQN_SIM_PATH", path)
+    lib_option("sim_path", path)
     _run(*grid, E=3, steps=100, check_every=9, full_state_at=(50,), actuated=(path != "lds"))
 
 

@@ -13,6 +13,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dmdqn_amd.build import source_digest  # noqa: E402
+
 
 def per_kernel(path, counter, substr):
     vals = []
@@ -49,6 +52,9 @@ def main():
               "correction": "fetch x2 (gfx950 FETCH_SIZE reads 1/2 of wide streams), write x1"}
     if source:
         d[key]["source"] = source
+    # the kernel sources the passes measured (bench.py: traffic_stale when HEAD's differ)
+    kind = "sim" if key.endswith("_sim") else "learn"
+    d[key]["sources_digest"] = {"kind": kind, "sha256_16": source_digest(kind)}
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d[key]))

@@ -17,9 +17,12 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 for CFG in "$@"; do
     case $CFG in
-        c2) ARGS="--rows 2 --cols 2 --envs 256 --precision bf16"; KEY=2x2x256_bf16; LK=k_learn_bf16 ;;
-        c3) ARGS="--rows 4 --cols 4 --envs 1024 --precision fp16"; KEY=4x4x1024_fp16; LK=k_learn_f16 ;;
-        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK=k_shared_next,k_shared_grad,k_reduce_slabs,k_adam ;;
+        c2) ARGS="--rows 2 --cols 2 --envs 256 --precision bf16"; KEY=2x2x256_bf16; LK=k_learn_bf16
+            SIMK="k_sim_step<true, false, false>"; ENVK="k_sim_step<true, false, true>" ;;
+        c3) ARGS="--rows 4 --cols 4 --envs 1024 --precision fp16"; KEY=4x4x1024_fp16; LK=k_learn_f16
+            SIMK="k_sim_step<true, false, false>"; ENVK="k_sim_step<true, false, true>" ;;
+        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK=k_shared_next,k_shared_grad,k_reduce_slabs,k_adam
+            SIMK="k_sim_step_reg<1024, false>"; ENVK="k_sim_step_reg<1024, true>" ;;
         *) echo "unknown config $CFG"; exit 2 ;;
     esac
     O=$R/gpurun_out/$TAG/$CFG
@@ -40,8 +43,11 @@ for CFG in "$@"; do
     F=$(find $O/pmcF -name '*counter_collection.csv' | head -n 1)
     W=$(find $O/pmcW -name '*counter_collection.csv' | head -n 1)
     M=$(find $O/pmcM -name '*counter_collection.csv' | head -n 1)
+    # the sim key: the bench's sim probe (k_sim_step alone, the launches
+    # sim_roofline times); the envstep key: the fused env step of the loop
     (cd $R && python3 tools/pmc_learn.py "$F" "$W" "$KEY" "$LK" "profiles/$TAG/$CFG" &&
-         python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_sim" k_sim_step "profiles/$TAG/$CFG" &&
+         python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_sim" "$SIMK" "profiles/$TAG/$CFG" &&
+         python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_envstep" "$ENVK" "profiles/$TAG/$CFG" &&
          for K1 in ${LK//,/ }; do python3 tools/pmc_mfma.py "$M" "$K1" > $O/mfma_busy_$K1.json; done)
     cp "$(find $O/stats -name '*kernel_stats.csv' | head -n 1)" $O/kernel_stats.csv
     gzip -c "$F" > $O/fetch_size_counter_collection.csv.gz
