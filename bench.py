@@ -212,10 +212,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=60,
                     help="timed RL steps per replica of the CPU baseline")
-    ap.add_argument("--overlap", default="none", choices=["none", "sample", "full"],
+    ap.add_argument("--overlap", default="none", choices=["none", "sample", "full", "env"],
                     help="stream schedule (dmdqn_amd/trainer.py; all bit-identical): none = one "
                          "stream; sample = replay draws on a side stream beside act/sim/observe/"
-                         "store; full = step t+1's act/sim/observe/sample beside learn t")
+                         "store; full = step t+1's act/sim/observe/sample beside learn t; env = "
+                         "step t+1's fused env step (store in the ring's spare slot) + draws "
+                         "beside learn t")
     ap.add_argument("--split-learn", action="store_true",
                     help="independent learn as two launches (gradient, Adam; bit-identical; "
                          "trainer.py split_learn)")
@@ -396,7 +398,9 @@ def main():
                 "precision": args.precision,
                 "schedule": {"none": "one stream",
                              "sample": "replay draws on a side stream beside act/sim/observe/store",
-                             "full": "act/sim/observe/sample of step t+1 beside learn t"}[args.overlap]
+                             "full": "act/sim/observe/sample of step t+1 beside learn t",
+                             "env": "the fused env step + replay draws of step t+1 beside learn t"
+                             }[args.overlap]
                             + ("; act + sim + observe + store fused in one launch per env"
                                if tr.fused else ""),
             },

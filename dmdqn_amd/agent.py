@@ -394,7 +394,7 @@ class BatchedDQN:
 
     def remembered(self):
         """The bookkeeping of remember() after a fused env step stored the
-        transition into ring slot ring.total % ring.cap."""
+        transition into ring slot ring.next_slot."""
         self.ring.advance()
         self.ring.poll()
         if self.cfg.count_env_steps:
@@ -470,7 +470,7 @@ class BatchedDQN:
         call the C ABI directly; the tensors it points at belong to self."""
         alpha, c1, c2, eps, sync, qstats = self._last_learn
         cfg = self.cfg
-        return CLearn(self.NA, self.ring.cap, self.ring.start, cfg.batch_size, self.H,
+        return CLearn(self.NA, self.ring.slots, self.ring.start, cfg.batch_size, self.H,
                       PRECISIONS[cfg.precision], int(sync), self.P,
                       *[None if t is None else t.data_ptr()
                         for t in [self.ring.s, self.ring.n, self.ring.a, self.ring.d, self.ring.r,

@@ -26,9 +26,10 @@ import os
 import numpy as np
 import torch
 
+# 7: replay rings of cap + 1 slots (kernels.ReplayRing), the written slots saved;
 # 6: + per-replica clocks and episode counters; 5: + the actuated-mode detector
 # times; 4: 128-B replay rows, unpadded W1T
-FORMAT = "dmdqn-ckpt-6"
+FORMAT = "dmdqn-ckpt-7"
 
 _ENV_TENSORS = ["t_x", "t_v", "t_dst", "t_head", "t_cnt", "t_phase_state", "t_ts", "t_qptr",
                 "t_stats", "t_last_det", "t_env", "halt", "phase", "tspent", "done_u8"]
@@ -45,6 +46,13 @@ _ENV_FIXED = ["rows", "cols", "num_envs", "env_offset", "seed", "signal_features
               "actuated"]
 # fields added after format 4 was introduced
 _DEFAULTS = {"loss": "mse", "actuated": False, "replay_rows": "int8"}
+
+
+def _written(total, ring):
+    """Ring slots that hold transitions after `total` stores: 0 .. n-1 (once
+    the ring has wrapped, every slot; the spare one holds the evicted
+    transition, saved with the rest)."""
+    return min(int(total), ring.slots)
 
 
 def _check_cfg(saved, cur, fields, what):
@@ -84,7 +92,7 @@ def trainer_state(tr, include_replay=True):
     st["env"]["local"] = env.local.cpu()
     st["obs"] = tr.obs.cpu()
     if include_replay:
-        n = len(ag.ring)
+        n = _written(ag.ring.total, ag.ring)
         st["replay"] = {k: getattr(ag.ring, k)[:, :n].cpu() for k in ["s", "n", "a", "r", "d"]}
     return st
 
@@ -134,9 +142,9 @@ def load(path, tr):
     c = st["counters"]
     if "replay" in st:
         n = st["replay"]["s"].shape[1]
-        if n != min(int(c["ring_total"]), ag.ring.cap):
+        if n != _written(int(c["ring_total"]), ag.ring):
             raise ValueError(f"checkpoint replay holds {n} slots, its counter says "
-                             f"{min(int(c['ring_total']), ag.ring.cap)}")
+                             f"{_written(int(c['ring_total']), ag.ring)}")
         for k, v in st["replay"].items():
             plan("replay", getattr(ag.ring, k)[:, :n], v, k)
     for dst, v in copies:

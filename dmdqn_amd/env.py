@@ -231,7 +231,7 @@ class TrafficEnv:
         draws from np_state (eps; greedy [E,A] when eps < 1) into actions
         [E,A], setPhase + K substeps, the observation / reward, and the
         transition (obs_s, action, reward, obs', the replica's done flag) into
-        ring slot ring.total % ring.cap (int8 rows; the caller advances the
+        ring slot ring.next_slot (int8 rows; the caller advances the
         ring).  Bit-identical to act -> step -> ReplayRing.store; returns what
         step() returns."""
         if self.local is None:
@@ -248,7 +248,7 @@ class TrafficEnv:
                            cfg.action_stride, self._t0(), cfg.step_duration, cfg.max_sim_time,
                            self.halt, self.phase, self.tspent, self.done_u8, np_state, greedy,
                            actions, float(eps), int(n_actions), self.mode, local, obs, self.local,
-                           reward, obs_s, ring.total % ring.cap, ring.s, ring.n, ring.a, ring.r,
+                           reward, obs_s, ring.next_slot, ring.s, ring.n, ring.a, ring.r,
                            ring.d, ring.err)
         if self.sim_hook:
             self.sim_hook(False)

@@ -86,9 +86,12 @@ def observe(R, C, halt, phase, tspent, mode, prev_local=None, want_obs=True):
 class ReplayRing:
     """Device replay rings for NA agents (ReplayBuffer, dqn_agent.py:27-89).
 
-    Each agent keeps the last `cap` transitions; deque position p (0 = oldest)
-    lives in ring slot (start + p) % cap.  All agents add in lockstep, so one
-    host-side counter describes every ring.
+    Each agent keeps the last `cap` transitions (the deque's maxlen) in
+    `slots` = cap + 1 physical ring slots: deque position p (0 = oldest) lives
+    in slot (start + p) % slots and the next store goes to the one slot no
+    position maps to, total % slots -- so the store of step t+1 never touches
+    a slot the learn of step t may read (trainer overlap "env").  All agents
+    add in lockstep, so one host-side counter describes every ring.
 
     row_format "int8" (the batched path): 128-byte int8 rows, exact for this
     environment's integer features, anything else raises.  "f32" (the
@@ -99,16 +102,17 @@ class ReplayRing:
         if row_format not in ("int8", "f32"):
             raise ValueError("row_format must be 'int8' or 'f32'")
         self.NA, self.cap, self.row_format = NA, cap, row_format
+        self.slots = S = cap + 1
         z = dict(device=device)
         if row_format == "f32":
-            self.s = torch.zeros((NA, cap, ROW_FLOATS), dtype=torch.float32, **z)
-            self.n = torch.zeros((NA, cap, ROW_FLOATS), dtype=torch.float32, **z)
+            self.s = torch.zeros((NA, S, ROW_FLOATS), dtype=torch.float32, **z)
+            self.n = torch.zeros((NA, S, ROW_FLOATS), dtype=torch.float32, **z)
         else:
-            self.s = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
-            self.n = torch.zeros((NA, cap, ROW_BYTES), dtype=torch.int8, **z)
-        self.a = torch.zeros((NA, cap), dtype=torch.uint8, **z)
-        self.r = torch.zeros((NA, cap), dtype=torch.float64, **z)
-        self.d = torch.zeros((NA, cap), dtype=torch.uint8, **z)
+            self.s = torch.zeros((NA, S, ROW_BYTES), dtype=torch.int8, **z)
+            self.n = torch.zeros((NA, S, ROW_BYTES), dtype=torch.int8, **z)
+        self.a = torch.zeros((NA, S), dtype=torch.uint8, **z)
+        self.r = torch.zeros((NA, S), dtype=torch.float64, **z)
+        self.d = torch.zeros((NA, S), dtype=torch.uint8, **z)
         # the range flag lives in pinned host memory, written by the store kernel
         # itself (zero-copy; only on an error): polling it needs no copy launch
         if torch.device(device).type == "cuda":
@@ -125,7 +129,17 @@ class ReplayRing:
 
     @property
     def start(self):
-        return 0 if self.total <= self.cap else self.total % self.cap
+        """Slot of deque position 0."""
+        return (self.total - len(self)) % self.slots
+
+    @property
+    def next_slot(self):
+        """The slot the next store writes."""
+        return self.total % self.slots
+
+    def slots_of(self, pos):
+        """Ring slots of deque positions pos (int or array)."""
+        return (self.start + pos) % self.slots
 
     def store(self, obs_s, obs_n, act, rew, done):
         NA = self.NA
@@ -134,7 +148,7 @@ class ReplayRing:
         _check(act, torch.int32, (NA,), "act")
         _check(rew, torch.float64, (NA,), "rew")
         _check(done, torch.uint8, (NA,), "done")
-        slot = self.total % self.cap
+        slot = self.next_slot
         if self.row_format == "f32":
             _ops().replay_store_f32(slot, obs_s, obs_n, act, rew, done, self.s, self.n, self.a,
                                     self.r, self.d)
@@ -144,8 +158,8 @@ class ReplayRing:
         self.advance()
 
     def advance(self):
-        """One transition per agent was written at slot total % cap (store(),
-        or a fused env step, env.TrafficEnv.step_fused)."""
+        """One transition per agent was written at slot next_slot (store(), or
+        a fused env step, env.TrafficEnv.step_fused)."""
         self.total += 1
 
     def gather_f32(self, idx, xs, xn):

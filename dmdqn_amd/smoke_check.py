@@ -48,7 +48,7 @@ def run(TrafficEnv, EnvConfig, BatchedDQN, AgentConfig, K, O, np, torch):
         e = j // A  # agents of one env draw from that env's stream in junction order
         exp_idx = O.py_sample(pys[e], len(ring), 128)
         assert (idx[j] == exp_idx).all(), "replay indices vs CPython random.sample"
-        slots = (ring.start + idx[j]) % ring.cap
+        slots = ring.slots_of(idx[j])
         S = ring.s[j].cpu().numpy()[slots, :89].astype(np.float32)
         S2 = ring.n[j].cpu().numpy()[slots, :89].astype(np.float32)
         Aa = ring.a[j].cpu().numpy()[slots].astype(np.int32)

@@ -33,6 +33,18 @@ sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
             side work queued beside it mostly waits; split_learn=True makes the
             learn two launches whose Adam half leaves room beside it.
 
+  "env"     the fused env step of step t+1 (act, sim, observe, remember) and
+            the replay draws of learn t+1 run on a side stream beside learn t.
+            The ring has one spare slot (kernels.ReplayRing: cap + 1 slots for
+            a deque of maxlen cap), and the store of step t+1 goes to the one
+            slot learn t cannot sample; the store of step t+2 waits for learn
+            t (its slot is in learn t's window).  A greedy act (epsilon < 1)
+            waits for learn t's weights.
+              side:  [wait learn t-1] env_step_{t+1} sample_{t+1} (ev_env)
+              main:  [wait ev_env of t] learn_t
+            With a CU-masked side stream (bench --cu-split) the two split the
+            chip.
+
 What a step returns or exposes per step (obs, reward, loss, agent.actions,
 agent.idx) is fresh or double-buffered, so the caller may read it on its own
 stream between steps.  Persistent env/agent state (sim arrays, RNG streams) is
@@ -48,7 +60,7 @@ from .agent import AgentConfig, BatchedDQN
 from .env import EnvConfig, TrafficEnv
 
 
-SCHEDULES = ("none", "sample", "full")
+SCHEDULES = ("none", "sample", "full", "env")
 
 
 @dataclass
@@ -85,6 +97,9 @@ class Trainer:
         # fused: act + env step + remember as one launch (TrafficEnv.step_fused)
         # on the one-stream schedules; "full" splits them across its streams
         self.fused = bool(fused) and overlap != "full" and self.agent.ring.row_format == "int8"
+        if overlap == "env" and not self.fused:
+            raise ValueError('overlap "env" runs the fused env step (int8 replay rows, fused=True)')
+        self._ev_learn_prev = None  # overlap "env": the learn before the last one
         self.obs = self.env.reset()
         self.episode = 0
         self.step_count = 0
@@ -107,6 +122,8 @@ class Trainer:
     def _step(self, collect_stats):
         if self.overlap == "full":
             return self._step_overlap(collect_stats)
+        if self.overlap == "env":
+            return self._step_env_beside_learn(collect_stats)
         if self.overlap == "sample":
             return self._step_side_sample(collect_stats)
         env, agent = self.env, self.agent
@@ -179,6 +196,31 @@ class Trainer:
         self._ev_learn.record(main)
         self.last_loss, self.last_reward = loss, reward
         self.obs = self._after_step(done, next_obs, info, side=side, main=main)
+        return StepStats(loss is not None, done)
+
+    def _step_env_beside_learn(self, collect_stats):
+        env, agent, side = self.env, self.agent, self.side
+        main = torch.cuda.current_stream(env.device)
+        if self._join:  # first step, or the caller touched state on its stream
+            side.wait_stream(main)
+            self._join = False
+        if self._ev_learn_prev is not None:
+            # this store's slot is in the window of the learn two steps back
+            side.wait_event(self._ev_learn_prev)
+        if agent.current_epsilon() < 1.0 and self._ev_learn is not None:
+            side.wait_event(self._ev_learn)  # greedy act reads the updated weights
+        with torch.cuda.stream(side):
+            next_obs, reward, done, info = self._env_side()
+            agent.presample(len(agent.ring))
+            self.obs = self._after_step(done, next_obs, info)  # (an episode reset: on side)
+            ev_env = torch.cuda.Event()
+            ev_env.record(side)
+        main.wait_event(ev_env)  # the store learn t reads; what the caller reads after step()
+        loss = agent.learn(collect_stats=collect_stats)
+        self._ev_learn_prev = self._ev_learn
+        self._ev_learn = torch.cuda.Event()
+        self._ev_learn.record(main)
+        self.last_loss, self.last_reward = loss, reward
         return StepStats(loss is not None, done)
 
     def _after_step(self, done, next_obs, info, side=None, main=None):

@@ -73,7 +73,7 @@ class ReplayBuffer:
             return None
         _, py = _streams(self.device)
         idx = K.replay_sample(py, 1, n, batch_size)[0].long()
-        slots = (self.ring.start + idx) % self.ring.cap
+        slots = self.ring.slots_of(idx)
         # the z-score in float64 numpy on the host, exactly the reference's
         # expression (:66-69: np.mean / np.std use numpy's pairwise summation),
         # so the rewards are bit-identical; the fused learn kernel restates the

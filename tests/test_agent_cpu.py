@@ -68,3 +68,28 @@ def test_config_keys_match_reference_yaml():
     assert ref <= set(y)
     cfg = AgentConfig.from_dict(y)
     assert cfg.nn_layers == y["nn_layers"]
+
+
+def test_replay_ring_spare_slot_arithmetic():
+    """ReplayRing keeps a deque of maxlen cap in cap + 1 slots: deque position
+    p -> slot (start + p) % (cap + 1), the next store goes to the slot no
+    position maps to, so the store of step t+1 never touches the window of
+    learn t (trainer overlap "env"), while the store of step t+2 may (it
+    waits for learn t)."""
+    from dmdqn_amd.kernels import ReplayRing
+    cap = 5
+    r = ReplayRing(2, cap, device="cpu")
+    assert r.slots == cap + 1 and tuple(r.a.shape) == (2, cap + 1)
+    prev_window = None
+    for t in range(40):
+        window = {int(s) for s in r.slots_of(np.arange(len(r)))}
+        assert len(window) == len(r) and r.next_slot not in window
+        if prev_window is not None and len(prev_window) == cap:
+            # the window one learn back holds the next slot once the ring is full
+            assert r.next_slot in prev_window
+        prev_window = window
+        # deque semantics: position 0 is the oldest kept transition
+        if t >= cap:
+            assert int(r.slots_of(0)) == (t - cap) % (cap + 1)
+        r.advance()
+    assert len(r) == cap and r.start == (40 - cap) % (cap + 1)

@@ -81,7 +81,7 @@ def _check_shared_grad(tr, raw, pre, agents0, n_sub=64):
     g_sub = torch.empty(ag.P, dtype=torch.float32, device=DEV)
     work = torch.empty(n_sub * 128 * 5, dtype=torch.uint8, device=DEV)
     a = ag.c_learn_args()
-    j0, cap = agents0, ring.cap
+    j0, cap = agents0, ring.slots  # the physical row stride
     a.NA = n_sub
     for f, t, per in (("ring_s", ring.s, cap * 128), ("ring_n", ring.n, cap * 128),
                       ("ring_a", ring.a, cap), ("ring_d", ring.d, cap), ("ring_r", ring.r, cap * 8),
@@ -326,3 +326,28 @@ def test_c3_overlap_schedules_bit_identical_at_size():
     for sched in ("full", "sample"):
         for a, b in zip(res["none"], res[sched]):
             assert torch.equal(a, b), sched
+
+
+def test_c2_env_beside_learn_bit_identical_at_size():
+    """overlap "env" (the fused env step of t+1 beside learn t; the store in
+    the ring's spare slot) at C2 size (2x2 x 256, bf16), the ring wrapped
+    (replay 300, 420 steps): losses, weights, rings and observations
+    bit-identical to the one-stream order (train.py:207-292's order)."""
+    res = {}
+    for sched in ("none", "env"):
+        tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=256, seed=2),
+                     AgentConfig(precision="bf16", replay_buffer_size=300, seed=2),
+                     overlap=sched)
+        losses = []
+        for _ in range(420):
+            tr.step()
+            if tr.last_loss is not None:
+                losses.append(tr.last_loss.clone())
+        torch.cuda.synchronize()
+        assert tr.agent.ring.start != 0
+        res[sched] = (torch.stack(losses).cpu(), tr.agent.params.cpu(), tr.obs.cpu(),
+                      tr.agent.ring.s.cpu(), tr.agent.ring.n.cpu())
+        del tr
+        torch.cuda.empty_cache()
+    for a, b in zip(res["none"], res["env"]):
+        assert torch.equal(a, b)

@@ -36,7 +36,7 @@ def _fill(agent, T, rng):
 
 def _host_batch(agent, ag, idx):
     ring = agent.ring
-    slots = (ring.start + idx) % ring.cap
+    slots = ring.slots_of(idx)
     S = ring.s[ag].cpu().numpy()[slots, :89].astype(np.float32)
     S2 = ring.n[ag].cpu().numpy()[slots, :89].astype(np.float32)
     A = ring.a[ag].cpu().numpy()[slots].astype(np.int32)

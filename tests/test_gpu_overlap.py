@@ -14,9 +14,9 @@ from dmdqn_amd.env import EnvConfig  # noqa: E402
 from dmdqn_amd.trainer import Trainer  # noqa: E402
 
 
-def _trainer(overlap, precision, shared, greedy, side_stream=None):
+def _trainer(overlap, precision, shared, greedy, side_stream=None, cap=200):
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=8, seed=11, max_sim_time=500),
-                 AgentConfig(replay_buffer_size=200, target_update_frequency=9, seed=4,
+                 AgentConfig(replay_buffer_size=cap, target_update_frequency=9, seed=4,
                              precision=precision, shared_params=shared,
                              count_env_steps=greedy),
                  overlap=overlap, side_stream=side_stream)
@@ -35,7 +35,7 @@ def _run(tr, n):
     return out
 
 
-@pytest.mark.parametrize("mode", ["sample", "full"])
+@pytest.mark.parametrize("mode", ["sample", "full", "env"])
 @pytest.mark.parametrize("precision,shared,greedy", [
     ("fp16", False, False), ("fp32", False, False), ("bf16", False, False), ("fp16", True, False),
     ("fp16", False, True)])
@@ -60,6 +60,29 @@ def test_overlap_on_cu_masked_streams_matches_sequential():
         ovl = _trainer("full", "fp16", False, False, side_stream=side)
         assert ovl.side is side
         b = _run(ovl, 170)
+    _compare(ref, ovl, a, b)
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_env_beside_learn_on_a_wrapped_ring(masked):
+    """overlap "env": the fused env step of t+1 beside learn t, with the ring
+    wrapped (replay 120 < 170 steps), so every store lands in the spare slot
+    the running learn cannot sample (kernels.ReplayRing) -- bit-identical to
+    the one-stream order, also with the two streams CU-masked (bench
+    --cu-split)."""
+    from dmdqn_amd._lib import cu_masked_stream
+    ref = _trainer("none", "bf16", False, False, cap=120)
+    a = _run(ref, 170)
+    if masked:
+        n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+        main, side = cu_masked_stream(range(64, n_cu)), cu_masked_stream(range(64))
+        with torch.cuda.stream(main):
+            ovl = _trainer("env", "bf16", False, False, side_stream=side, cap=120)
+            b = _run(ovl, 170)
+    else:
+        ovl = _trainer("env", "bf16", False, False, cap=120)
+        b = _run(ovl, 170)
+    assert ovl.agent.ring.start != 0
     _compare(ref, ovl, a, b)
 
 

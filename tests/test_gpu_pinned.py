@@ -345,7 +345,7 @@ def test_device_zscore_bit_exact(precision):
         idx = ag.idx.cpu().numpy()
         rn = ag.rn_out.cpu().numpy()
         for j in range(ag.NA):
-            slots = (ag.ring.start + idx[j]) % ag.ring.cap
+            slots = ag.ring.slots_of(idx[j])
             r = ag.ring.r[j].cpu().numpy()[slots]
             np.testing.assert_array_equal(rn[j], O.zscore(r))
             # and numpy itself (the reference's expression)

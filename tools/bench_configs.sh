@@ -16,7 +16,6 @@ for CFG in "$@"; do
         c2) ARGS="--rows 2 --cols 2 --envs 256 --precision bf16 --no-cpu-baseline" ;;
         c2full) ARGS="--rows 2 --cols 2 --envs 256 --precision bf16 --overlap full --no-cpu-baseline" ;;
         c5) ARGS="--shared --rows 8 --cols 8 --envs 256 --no-cpu-baseline" ;;
-        c5v1) ARGS="--shared --rows 8 --cols 8 --envs 256 --no-cpu-baseline"; ENVV="DMDQN_SHARED_V1=1" ;;
         *) echo "unknown config $CFG"; exit 2 ;;
     esac
     env $ENVV timeout -k 10 300 python3 $R/bench.py $ARGS > $O/$CFG.json 2> $O/$CFG.err

@@ -22,7 +22,7 @@ for sched in sys.argv[2:] or ["none", "full"]:
     for t in range(STEPS):
         tr.step()
         a = tr.agent
-        slot = (a.ring.total - 1) % a.ring.cap
+        slot = (a.ring.total - 1) % a.ring.slots
         rec.append({"actions": a.actions.clone(), "obs": tr.obs.clone(),
                     "ring_s": a.ring.s[:, slot].clone(), "ring_n": a.ring.n[:, slot].clone(),
                     "ring_r": a.ring.r[:, slot].clone(),

@@ -37,10 +37,7 @@ lib = C.CDLL(sys.argv[1]) if len(sys.argv) > 1 else _lib.load()
 fn = lib.dmdqn_learn_shared_grad
 fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
 fn.restype = C.c_int
-V2 = os.environ.get("DMDQN_SHARED_GRAD", "") == "2"
-names_g = (["R (fwd, loss, dZ2, dH1)", "barrier 1", "W1 (dW3, dZ2 image, dW2)", "barrier 2",
-            "R2 (dZ1, X images)", "barrier 3", "W2 (dW1)", "barrier 4"] if V2 else
-           ["L1", "B1+L2+L3", "B2+loss+next X", "B3+dW3+dZ2", "B4+dH1", "dW2+dW1", "B5"])
+names_g = ["L1", "B1+L2+L3", "B2+loss+next X", "B3+dW3+dZ2", "B4+dH1", "dW2+dW1", "B5"]
 out = {}
 hashes = []
 for rep in range(3):
@@ -56,10 +53,6 @@ for rep in range(3):
     dg = np.diff(st[:, 0:len(names_g) + 1], axis=1)
     out = {"grad_" + n: round(float(np.median(dg[:, k])), 3) for k, n in enumerate(names_g)}
     last = len(names_g)
-    if V2:
-        for k, n in [(13, "R.fwd"), (14, "R.loss+images+dZ2"), (15, "R.dH1")]:
-            prev = 0 if k == 13 else k - 1
-            out["grad_" + n] = round(float(np.median(st[:, k] - st[:, prev])), 3)
     out["grad_per_agent_us"] = round(float(np.median(st[:, last] - st[:, 0])), 3)
     out["grad_span_ms"] = round(float(st[:, last].max() - st[:, 0].min()) / 1000, 4)
     out["next_zscore_us"] = round(float(np.median(st[:, 11] - st[:, 10])), 3)
@@ -72,5 +65,5 @@ tag = os.path.basename(sys.argv[1])[:-3] if len(sys.argv) > 1 else "product"
 os.makedirs("gpurun_out", exist_ok=True)
 np.save(f"gpurun_out/grad_{tag}.npy", ag.grad.cpu().numpy())
 out["lib"] = (os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else "product") + \
-    (" grad v2" if V2 else " grad v3")
+    " k_shared_grad3"
 print(json.dumps(out))
