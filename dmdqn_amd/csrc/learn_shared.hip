@@ -963,6 +963,323 @@ __global__ void __launch_bounds__(64 * (8 / NT), 1) k_shared_grad3(dmdqn_learn_a
 
 }  // namespace g3
 
+// ---------------------------------------------------------------- pass 2, v4
+// k_shared_grad3 with the output layer, the loss and dZ2 moved to ROW-owning
+// waves after the H2 image is complete: wave w takes batch rows 16w..16w+15,
+// reads their H2 rows once (the B operand of Q^T = W3^T H2^T, four MFMAs over
+// k = 0..127 from a W3^T LDS image), computes Q, the loss and dL/dQ on those
+// rows, then dZ2 = h16(dq W3[k][a]) masked by H2 > 0 for every k of the rows
+// straight from the same registers (the W3 row of the row's action from the
+// image), and writes the dZ2 image rows.  That replaces the per-wave partial
+// Q sums (8 waves' partials per row, summed by 16 lanes) and the separate
+// dZ2 phase: four barriers per agent instead of five.
+//   L1  Z1^T = W1^T X^T  (X image)          -> H1 image, own columns
+//   L2  Z2^T = W2^T H1^T (H1 image)         -> H2 image, own columns
+//   RQ  rows 16w..: Q, loss, dq ; dZ2 rows  -> DQ image, dZ2 image (rows)
+//   G   dW3 (H2 own^T, DQ) ; dH1 own (dZ2 image) -> dZ1 own (over H2 own) ;
+//       dW2 (H1^T, dZ2 own) ; dW1 (X^T, dZ1 own)
+// Same rounding points as k_shared_grad3 (Keras' mixed policy).
+namespace g4 {
+using g3::X_BYTES;
+using g3::IMG;
+constexpr int OFF_X = 0;                          // two X buffers
+constexpr int OFF_H1 = 2 * X_BYTES;
+constexpr int OFF_Z2 = OFF_H1 + IMG;              // dZ2 [128][128], written by rows
+constexpr int OFF_H2 = OFF_Z2 + IMG;              // H2 own columns, then dZ1 own columns
+constexpr int OFF_DQ = OFF_H2 + IMG;              // [128][16]
+constexpr int OFF_W3 = OFF_DQ + B_ * 16 * 2;      // W3^T [16][128] f16, rows 4..15 zero
+constexpr int OFF_SC = OFF_W3 + 16 * H * 2;       // sloss [8]
+constexpr int LDS = OFF_SC + 32;
+static_assert(LDS <= 160 * 1024, "k_shared_grad4 LDS");
+static_assert(OFF_W3 % 16 == 0, "aligned W3 image");
+
+struct WSlice4 {
+    half8 w1[3];   // lane (i, g): W1^T[16w + i][32s + 8g + e] (0 past feature 88)
+    half8 w2[4];   // W2^T[16w + i][32s + 8g + e]
+    half8 w2b[4];  // W2[16w + i][32s + 8g + e]  (= W2^T[k][j])
+    half4v b1, b2, b3;
+};
+
+__device__ __forceinline__ void load_slice4(const h16 *WH, int w, WSlice4 &S) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const int j = 16 * w + i;
+#pragma unroll
+    for (int s = 0; s < 3; s++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int f = 32 * s + 8 * g + e;
+            S.w1[s][e] = f < QN_D ? WH[L::oW1T + qn_w1<H>(j, f)] : (h16)0.0f;
+        }
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int c = 32 * s + 8 * g + e;
+            S.w2[s][e] = WH[L::oW2T + qn_wt(j, c, H)];
+            S.w2b[s][e] = WH[L::oW2T + qn_wt(c, j, H)];
+        }
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const int k = 16 * w + 4 * g + e;
+        S.b1[e] = WH[L::ob1 + k];
+        S.b2[e] = WH[L::ob1 + H + k];
+        S.b3[e] = WH[L::ob1 + 2 * H + e];
+    }
+}
+
+template <bool QSTATS>
+__global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, const float *y_in,
+                                                       const uint8_t *act_in, float *slab) {
+    constexpr int NTH = 512, RH = 4;
+    __shared__ __attribute__((aligned(16))) char smem[LDS];
+    h16 *H1I = reinterpret_cast<h16 *>(smem + OFF_H1), *Z2I = reinterpret_cast<h16 *>(smem + OFF_Z2);
+    h16 *H2I = reinterpret_cast<h16 *>(smem + OFF_H2), *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
+    h16 *W3I = reinterpret_cast<h16 *>(smem + OFF_W3);
+    float *sloss = reinterpret_cast<float *>(smem + OFF_SC);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
+    WSlice4 W;
+    load_slice4(WH, w, W);
+    // W3^T image [16][128]: rows a < 4 the output layer, rows 4..15 zero (the
+    // A operand of the Q MFMA is read straight from it)
+    for (int k = threadIdx.x; k < 16 * H; k += NTH)
+        W3I[k] = k < NACT * H ? WH[L::oW3T + k] : (h16)0.0f;
+    half8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
+    f32x4 G1[6], G2[8], G3, GB1, GB2, GB3;
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < 6; f++) G1[f] = z4;
+#pragma unroll
+    for (int j = 0; j < 8; j++) G2[j] = z4;
+    G3 = GB1 = GB2 = GB3 = z4;
+    for (int k = threadIdx.x; k < B_ * 16; k += NTH) DQI[k] = (h16)0.0f;
+    const int row = 16 * w + i;  // this lane's batch row in the RQ phase
+    int wv = w;
+    asm volatile("" : "+v"(wv));
+    const int bR = hoff(i, 8 * g), bX = hoff<DP>(i, 8 * g);
+    const int trH[2] = {hsplit(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
+                        hsplit(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
+    const int trX[2] = {hsplit<DP>(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
+                        hsplit<DP>(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
+    const int c0 = 16 * wv;  // own column block
+    const int bW = hoff(i, (c0 & 16) + 4 * g) + 256 * (c0 >> 5);
+    const int trO = hsplit(8 * (g & 1) + (i >> 2), (c0 & 16) + 4 * (i & 3), g >> 1, 0) + 256 * (c0 >> 5);
+    const bool stager = threadIdx.x < 256;
+    int agent = blockIdx.x;
+    if (agent < a.NA && stager) {
+        g3::XRows x0;
+        g3::xrows_issue<NTH>(a, agent, g3::pos3(a, agent, threadIdx.x), threadIdx.x, x0);
+        g3::xrows_commit(x0, reinterpret_cast<h16 *>(smem + OFF_X), threadIdx.x);
+    }
+    int npos = g3::pos3(a, agent + gridDim.x, threadIdx.x);
+    float yv = 0.0f;
+    int avl = 0;
+    if (agent < a.NA) {
+        yv = y_in[(size_t)agent * B_ + row];
+        avl = act_in[(size_t)agent * B_ + row];
+    }
+    __syncthreads();
+    int buf = 0;
+    for (; agent < a.NA; agent += gridDim.x, buf ^= 1) {
+        SH_STAMP(agent, 0, threadIdx.x);
+        const h16 *X = reinterpret_cast<const h16 *>(smem + OFF_X + buf * X_BYTES);
+        const int nxt = agent + gridDim.x;
+        g3::XRows xn;
+        float yn = 0.0f;
+        int an = 0;
+        if (nxt < a.NA && stager) g3::xrows_issue<NTH>(a, nxt, npos, threadIdx.x, xn);
+        if (nxt < a.NA) {
+            yn = y_in[(size_t)nxt * B_ + row];
+            an = act_in[(size_t)nxt * B_ + row];
+        }
+        npos = g3::pos3(a, nxt + gridDim.x, threadIdx.x);
+        // ---- L1: own neuron tile, row tiles in passes of RH -> H1 image
+#pragma unroll
+        for (int hf = 0; hf < 8 / RH; hf++) {
+            f32x4 c[RH];
+#pragma unroll
+            for (int r = 0; r < RH; r++) c[r] = z4;
+#pragma unroll
+            for (int s = 0; s < 3; s++) {
+                half8 xb[RH];
+#pragma unroll
+                for (int r = 0; r < RH; r++)
+                    xb[r] = *reinterpret_cast<const half8 *>(X + bX + 16 * DP * (RH * hf + r) + 256 * s);
+#pragma unroll
+                for (int r = 0; r < RH; r++) c[r] = mfma(W.w1[s], xb[r], c[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < RH; r++)
+                *reinterpret_cast<half4v *>(H1I + bW + 16 * H * (RH * hf + r)) = g3::relu4(c[r], W.b1);
+        }
+        SH_STAMP(agent, 1, threadIdx.x);
+        __syncthreads();  // B1: H1 image
+        // ---- L2: own tile -> H2 image
+#pragma unroll
+        for (int hf = 0; hf < 8 / RH; hf++) {
+            f32x4 c[RH];
+#pragma unroll
+            for (int r = 0; r < RH; r++) c[r] = z4;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                half8 hb[RH];
+#pragma unroll
+                for (int r = 0; r < RH; r++)
+                    hb[r] = *reinterpret_cast<const half8 *>(H1I + bR + 16 * H * (RH * hf + r) + 256 * s);
+#pragma unroll
+                for (int r = 0; r < RH; r++) c[r] = mfma(W.w2[s], hb[r], c[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < RH; r++)
+                *reinterpret_cast<half4v *>(H2I + bW + 16 * H * (RH * hf + r)) = g3::relu4(c[r], W.b2);
+        }
+        SH_STAMP(agent, 2, threadIdx.x);
+        __syncthreads();  // B2: H2 image
+        // ---- RQ: rows 16w + i.  Q^T = W3^T H2^T (K = k in four steps of 32)
+        half8 h2r[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+            h2r[s] = *reinterpret_cast<const half8 *>(H2I + bR + 16 * H * wv + 256 * s);
+        f32x4 cq = z4;
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+            cq = mfma(*reinterpret_cast<const half8 *>(W3I + i * H + 32 * s + 8 * g), h2r[s], cq);
+        float term = 0.0f, dq = 0.0f;
+        if (g == 0) {  // lane (i, 0): Q[row][0..3]
+            float q[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) q[e] = r16(r16(cq[e]) + (float)W.b3[e]);
+            const float qa = g3::pickf4(q[0], q[1], q[2], q[3], avl);
+            row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
+            dq = r16(dq);  // dL/dQ in f16 (the gradient of the learn's tf.cast)
+            half4v d;
+#pragma unroll
+            for (int e = 0; e < 4; e++) d[e] = e == avl ? (h16)dq : (h16)0.0f;
+            *reinterpret_cast<half4v *>(DQI + row * 16) = d;
+            if (QSTATS) {
+                float s1 = (q[0] + q[1]) + (q[2] + q[3]);
+                float s2 = (q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]);
+                for (int off = 8; off > 0; off >>= 1) {
+                    s1 += __shfl_xor(s1, off);
+                    s2 += __shfl_xor(s2, off);
+                }
+                if (l == 0) {
+                    atomicAdd(a.qstats + (size_t)agent * 6 + 0, s1);
+                    atomicAdd(a.qstats + (size_t)agent * 6 + 1, s2);
+                }
+            }
+        }
+        if (QSTATS)
+#pragma unroll
+            for (int e = 0; e < NACT; e++) {  // every lane takes part in the ballot
+                const float cnt = (float)__popcll(__ballot(g == 0 && avl == e));
+                if (l == 0) atomicAdd(a.qstats + (size_t)agent * 6 + 2 + e, cnt);
+            }
+        for (int off = 8; off > 0; off >>= 1) term += __shfl_xor(term, off);
+        if (l == 0) sloss[w] = term;
+        // dZ2 of the row for k = 32s + 8g + e: h16(dq W3[k][a]) where H2 > 0
+        dq = __shfl(dq, i);
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const half8 w3 = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * s + 8 * g);
+            half8 o;
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+                o[e] = h2r[s][e] > (h16)0.0f ? (h16)(dq * (float)w3[e]) : (h16)0.0f;
+            *reinterpret_cast<half8 *>(Z2I + bR + 16 * H * wv + 256 * s) = o;
+        }
+        // the next agent's X into the other buffer (last read two agents ago)
+        if (nxt < a.NA && stager)
+            g3::xrows_commit(xn, reinterpret_cast<h16 *>(smem + OFF_X + (buf ^ 1) * X_BYTES),
+                             threadIdx.x);
+        SH_STAMP(agent, 3, threadIdx.x);
+        __syncthreads();  // B3: DQ, dZ2 image, loss partials, next X
+        if (threadIdx.x == 0 && a.loss) {
+            float ls = sloss[0];
+            for (int v = 1; v < 8; v++) ls += sloss[v];
+            a.loss[agent] = ls / (float)B_;
+        }
+        // ---- dW3 (own k) and db3 (wave 0)
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const half8 dqf = frag_tr(DQI, 16, 32 * s, 0);
+            G3 = mfma(frag_tr_p(H2I + trO + 2 * 16 * H * s), dqf, G3);
+            if (w == 0) GB3 = mfma(ones, dqf, GB3);
+        }
+        SH_STAMP(agent, 4, threadIdx.x);
+        // ---- dH1 (own j) -> dZ1 own -> image (over this wave's H2 columns)
+#pragma unroll
+        for (int hf = 0; hf < 8 / RH; hf++) {
+            f32x4 c[RH];
+#pragma unroll
+            for (int r = 0; r < RH; r++) c[r] = z4;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                half8 zb[RH];
+#pragma unroll
+                for (int r = 0; r < RH; r++)
+                    zb[r] = *reinterpret_cast<const half8 *>(Z2I + bR + 16 * H * (RH * hf + r) + 256 * s);
+#pragma unroll
+                for (int r = 0; r < RH; r++) c[r] = mfma(W.w2b[s], zb[r], c[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < RH; r++) {
+                const int rt = RH * hf + r;
+                half4v o;
+                const half4v hv = *reinterpret_cast<const half4v *>(H1I + bW + 16 * H * rt);
+#pragma unroll
+                for (int e = 0; e < 4; e++) o[e] = hv[e] > (h16)0.0f ? (h16)c[r][e] : (h16)0.0f;
+                *reinterpret_cast<half4v *>(H2I + bW + 16 * H * rt) = o;
+            }
+        }
+        SH_STAMP(agent, 5, threadIdx.x);
+        // ---- dW2[j][k own] and db2 ; dW1[f][j own] and db1 (K = rows)
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const half8 bq = frag_tr_p(Z2I + trO + 2 * 16 * H * s);
+            const half8 bv = frag_tr_p(H2I + trO + 2 * 16 * H * s);
+            GB2 = mfma(ones, bq, GB2);
+            GB1 = mfma(ones, bv, GB1);
+#pragma unroll
+            for (int jt = 0; jt < 8; jt++)
+                G2[jt] = mfma(frag_tr_p(H1I + trH[jt & 1] + 256 * (jt >> 1) + 2 * 16 * H * s), bq, G2[jt]);
+#pragma unroll
+            for (int ft = 0; ft < 6; ft++)
+                G1[ft] = mfma(frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s), bv, G1[ft]);
+        }
+        yv = yn;
+        avl = an;
+        SH_STAMP(agent, 6, threadIdx.x);
+        __syncthreads();  // B4: the images are rewritten by the next agent
+        SH_STAMP(agent, 7, threadIdx.x);
+    }
+    // partial sums of this workgroup, kernel layout (every index written once)
+    float *G = slab + (size_t)blockIdx.x * L::P;
+    const int n0 = 16 * w, n = n0 + i;  // this lane's neuron (C-tile column)
+    if (i < NACT)  // G3: rows k = n0 + 4g + e, column a = i
+        *reinterpret_cast<float4 *>(G + L::oW3T + i * H + n0 + 4 * g) =
+            make_float4(G3[0], G3[1], G3[2], G3[3]);
+#pragma unroll
+    for (int jt = 0; jt < 8; jt++)  // G2[jt]: fan-in j = 16jt + 4g + e, fan-out k = n
+        *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(n, 16 * jt + 4 * g, H)) =
+            make_float4(G2[jt][0], G2[jt][1], G2[jt][2], G2[jt][3]);
+    if (g == 0) {
+        G[L::ob2 + n] = GB2[0];
+        G[L::ob1 + n] = GB1[0];
+    }
+#pragma unroll
+    for (int ft = 0; ft < 6; ft++)  // G1[ft]: features 16ft + 4g + e, neuron n
+        if (ft < 5 || g < 2)
+            *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(n, 16 * ft + 4 * g)) =
+                make_float4(G1[ft][0], G1[ft][1], G1[ft][2], G1[ft][3]);
+    if (g == 2) G[L::oW1X + n] = G1[5][0];  // feature 88
+    if (w == 0 && g == 0 && i < NACT) G[L::ob3 + i] = GB3[0];
+}
+
+}  // namespace g4
+
 }  // namespace shk
 
 // Launch of the two passes (called by dmdqn_learn_shared_grad, learn_f16.hip).
@@ -973,9 +1290,16 @@ int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *s
     const int next_blocks = next_wg < n_slabs ? next_wg : n_slabs;
     hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(64 * NEXT_WAVES), 0, s, *a, y, act);
     DMDQN_LAUNCH_CHECK("k_shared_next");
+#ifndef SH_GRAD
+#define SH_GRAD 4  // 3: k_shared_grad3 (A/B builds, tools/build_exp.py -DSH_GRAD=3)
+#endif
+#if SH_GRAD == 3
     auto k = a->qstats ? g3::k_shared_grad3<true, 1> : g3::k_shared_grad3<false, 1>;
+#else
+    auto k = a->qstats ? g4::k_shared_grad4<true> : g4::k_shared_grad4<false>;
+#endif
     hipLaunchKernelGGL(k, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
-    DMDQN_LAUNCH_CHECK("k_shared_grad3");
+    DMDQN_LAUNCH_CHECK("k_shared_grad");
     return DMDQN_OK;
 }
 

@@ -37,7 +37,9 @@ lib = C.CDLL(sys.argv[1]) if len(sys.argv) > 1 else _lib.load()
 fn = lib.dmdqn_learn_shared_grad
 fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
 fn.restype = C.c_int
-names_g = ["L1", "B1+L2+L3", "B2+loss+next X", "B3+dW3+dZ2", "B4+dH1", "dW2+dW1", "B5"]
+GRAD3 = "grad3" in (sys.argv[1] if len(sys.argv) > 1 else "")
+names_g = (["L1", "B1+L2+L3", "B2+loss+next X", "B3+dW3+dZ2", "B4+dH1", "dW2+dW1", "B5"] if GRAD3
+           else ["L1", "B1+L2", "B2+RQ (Q, loss, dZ2 rows)+next X", "B3+dW3", "dH1", "dW2+dW1", "B4"])
 out = {}
 hashes = []
 for rep in range(3):
@@ -65,5 +67,5 @@ tag = os.path.basename(sys.argv[1])[:-3] if len(sys.argv) > 1 else "product"
 os.makedirs("gpurun_out", exist_ok=True)
 np.save(f"gpurun_out/grad_{tag}.npy", ag.grad.cpu().numpy())
 out["lib"] = (os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else "product") + \
-    " k_shared_grad3"
+    (" k_shared_grad3" if GRAD3 else " k_shared_grad4")
 print(json.dumps(out))
