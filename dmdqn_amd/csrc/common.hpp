@@ -289,14 +289,27 @@ __device__ inline void learn_qstats(float *qstats, int agent, const float *z3, c
 //                     |d| <= 1 ? d^2 / 2 : |d| - 1/2,  clip(d, -1, 1) / B
 // The loss is the mean of the terms.  kind is uniform over the block, so the
 // select costs two VALU ops per row.
+// An f32 product the compiler may not fuse into an fma with the add that
+// consumes it, whatever the file's -ffp-contract (clang's "fast", which the
+// learn files use for their MFMA epilogues, fuses across statements and
+// disregards `#pragma clang fp contract(off)`): the empty asm makes the
+// rounded product opaque.  For the arithmetic that must round every op as
+// TF's separate elementwise kernels do -- Keras-3 Adam, the TD target, the
+// squared error.
+__device__ __forceinline__ float mul_rn(float a, float b) {
+    float p = a * b;
+    asm("" : "+v"(p));
+    return p;
+}
+
 __device__ __forceinline__ void loss_term(int kind, float diff, float inv_b, float &term,
                                           float &dq) {
     if (kind == DMDQN_LOSS_HUBER) {
         const float ae = fabsf(diff);
-        term = ae <= 1.0f ? 0.5f * diff * diff : ae - 0.5f;
+        term = ae <= 1.0f ? mul_rn(0.5f * diff, diff) : ae - 0.5f;
         dq = (ae <= 1.0f ? diff : copysignf(1.0f, diff)) * inv_b;
     } else {
-        term = diff * diff;
+        term = mul_rn(diff, diff);
         dq = 2.0f * diff * inv_b;
     }
 }

@@ -129,10 +129,11 @@ struct AdamK {
 // Keras-3 Adam (keras/src/optimizers/adam.py update_step) for one element.
 __device__ __forceinline__ void adam_el(float *w, float *m, float *v, float *tgt, size_t i,
                                         float g, const AdamK &K, bool sync) {
-#pragma clang fp contract(off)  // each op rounded as TF's separate kernels
+    // each op rounded as TF's separate kernels (mul_rn: this file is built with
+    // -ffp-contract=fast, which ignores the contract pragma)
     float mi = m[i], vi = v[i], wi = w[i];
-    mi = mi + (g - mi) * K.c1;
-    vi = vi + (g * g - vi) * K.c2;
+    mi = mi + mul_rn(g - mi, K.c1);
+    vi = vi + mul_rn(mul_rn(g, g) - vi, K.c2);
     wi = wi - (mi * K.alpha) / (sqrtf(vi) + K.eps);
     m[i] = mi;
     v[i] = vi;
@@ -252,14 +253,14 @@ __global__ void __launch_bounds__(512) k_learn_f32(dmdqn_learn_args a) {
     // online forward on S': layer 3 reads H2 only, so its Q goes to the H1 region
     forward<H>(Wp, X, H1, H2, H1);
     if (tid < B_) {
-#pragma clang fp contract(off)  // y = r + (gamma (1 - d)) q_t, each op rounded as TF's
+        // y = r + (gamma (1 - d)) q_t, each op rounded as TF's (mul_rn: no fma)
         const float *qo = H1 + tid * NACT;
         int best = 0;
         for (int k = 1; k < NACT; k++)
             if (qo[k] > qo[best]) best = k;  // tf.argmax: first max
         float tq = S.z3[tid * NACT + best];
         float gd = a.gamma * (1.0f - S.dn[tid]);
-        S.y[tid] = S.rn[tid] + gd * tq;
+        S.y[tid] = S.rn[tid] + mul_rn(gd, tq);
     }
     __syncthreads();
     // ---- P4/P5: gather S, online forward keeping H1, H2; q, loss, dq

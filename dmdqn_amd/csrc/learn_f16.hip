@@ -50,13 +50,14 @@ __global__ void __launch_bounds__(256) k_adam(float *W, float *M, float *V, floa
                                               _Float16 *TH, _Float16 *WH, const float *G, int n,
                                               float gscale,
                                               float alpha, float c1, float c2, float eps, int sync) {
-#pragma clang fp contract(off)  // each op rounded as TF's separate kernels
+    // each op rounded as TF's separate kernels (mul_rn: this file is built
+    // with -ffp-contract=fast, which ignores the contract pragma)
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const float g = G[i] * gscale;
+    const float g = mul_rn(G[i], gscale);
     float m = M[i], v = V[i], w = W[i];
-    m = m + (g - m) * c1;
-    v = v + (g * g - v) * c2;
+    m = m + mul_rn(g - m, c1);
+    v = v + mul_rn(mul_rn(g, g) - v, c2);
     w = w - (m * alpha) / (sqrtf(v) + eps);
     M[i] = m;
     V[i] = v;

@@ -415,13 +415,13 @@ __device__ __forceinline__ float gval(const f32x4 &g, int e) { return r16(g[e]);
 
 // Keras-3 Adam (keras/src/optimizers/adam.py update_step) on one parameter,
 // every op rounded on its own as TF's separate elementwise kernels do: no fma
-// contraction (this file is built with -ffp-contract=fast for the MFMA
-// epilogues), correctly rounded sqrt and divide (HIP's default).
+// contraction (mul_rn: this file is built with -ffp-contract=fast for the
+// MFMA epilogues, which ignores the contract pragma), correctly rounded sqrt
+// and divide (HIP's default).
 __device__ __forceinline__ void adam_el(float &w, float &m, float &v, float g, float alpha,
                                         float c1, float c2, float eps) {
-#pragma clang fp contract(off)
-    m = m + (g - m) * c1;
-    v = v + (g * g - v) * c2;
+    m = m + mul_rn(g - m, c1);
+    v = v + mul_rn(mul_rn(g, g) - v, c2);
     w = w - (m * alpha) / (sqrtf(v) + eps);
 }
 
@@ -808,7 +808,7 @@ __device__ __forceinline__ void ddqn_target(const dmdqn_learn_args &a, const flo
                                             const Scratch &S) {
     const int tid = threadIdx.x;
     if (tid < B_) {
-#pragma clang fp contract(off)  // y = r + (gamma (1 - d)) q_t, each op rounded as TF's
+        // y = r + (gamma (1 - d)) q_t, each op rounded as TF's (mul_rn: no fma)
         const float4 q = *reinterpret_cast<const float4 *>(qo + tid * NACT);
         int best = 0;
         float bq = q.x;
@@ -817,7 +817,7 @@ __device__ __forceinline__ void ddqn_target(const dmdqn_learn_args &a, const flo
         if (q.w > bq) { best = 3; }
         float tq = S.z3[tid * NACT + best];
         float gd = a.gamma * (1.0f - S.dn[tid]);
-        S.y[tid] = S.rn[tid] + gd * tq;
+        S.y[tid] = S.rn[tid] + mul_rn(gd, tq);
     }
     __syncthreads();
 }

@@ -76,3 +76,29 @@ def test_c2_full_schedule_with_split_learn_bit_identical():
         torch.cuda.empty_cache()
     for a, b in zip(res["none"], res["full"]):
         np.testing.assert_array_equal(a.numpy(), b.numpy())
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_adam_is_keras3_adam_bit_exact_on_the_kernel_gradient(precision):
+    """Keras-3 Adam (keras/src/optimizers/adam.py update_step) rounds every op
+    as TF's separate elementwise kernels: given the gradient the kernel used
+    (the split learn exports it), params / m / v after the learn equal the
+    f32 numpy update bit for bit -- no fma contraction (common.hpp mul_rn)."""
+    import oracle as O
+    cfg = AgentConfig(precision=precision, seed=5, replay_buffer_size=300)
+    ag = BatchedDQN(8, 4, cfg)
+    ag.set_split_learn(True)
+    _fill(ag, 160, 2)
+    for _ in range(3):  # non-zero Adam slots
+        ag.learn()
+    p0, m0, v0 = (getattr(ag, n).cpu().numpy().copy() for n in ("params", "adam_m", "adam_v"))
+    ag.learn()
+    g = ag._split_grad.cpu().numpy()
+    alpha, c1, c2, eps = O.keras_adam_consts(ag.learn_step_counter)
+    m1 = m0 + (g - m0) * c1
+    v1 = v0 + (g * g - v0) * c2
+    p1 = p0 - (m1 * alpha) / (np.sqrt(v1) + eps)
+    for name, want in (("adam_m", m1), ("adam_v", v1), ("params", p1)):
+        got = getattr(ag, name).cpu().numpy()
+        assert np.array_equal(got.view(np.int32), want.view(np.int32)), (
+            name, int((got != want).sum()))
