@@ -1,16 +1,9 @@
 #!/bin/bash
-# Round-4 first GPU call: the -m gpu suite + smoke, then the C5 shared-learn
-# A/B (k_shared_grad4 product vs k_shared_grad3 experiment build: stamps and
-# event timing) and the C2 schedule A/B (one stream vs the fused env step
-# beside the learn, with and without CU masks).
+# Round-4 GPU call: the -m gpu suite + smoke, then the C2 schedule A/B (one
+# stream vs the fused env step beside the learn, with and without CU masks).
 set -e
 O=gpurun_out/r04a
 mkdir -p $O
-for rep in 1 2; do
-  timeout -k 10 120 python tools/stamp_shared.py > $O/stamp_grad4_$rep.json
-  timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_grad3.so > $O/stamp_grad3_$rep.json
-done
-cat $O/stamp_grad4_2.json $O/stamp_grad3_2.json
 bash tools/gpu_tests.sh r04a
 for rep in 1 2; do
   for v in "none" "env" "env --cu-split 32" "env --cu-split 64"; do
