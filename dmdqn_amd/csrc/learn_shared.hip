@@ -987,11 +987,22 @@ constexpr int OFF_H1 = 2 * X_BYTES;
 constexpr int OFF_Z2 = OFF_H1 + IMG;              // dZ2 [128][128], written by rows
 constexpr int OFF_H2 = OFF_Z2 + IMG;              // H2 own columns, then dZ1 own columns
 constexpr int OFF_DQ = OFF_H2 + IMG;              // [128][16]
-constexpr int OFF_W3 = OFF_DQ + B_ * 16 * 2;      // W3^T [16][128] f16, rows 4..15 zero
+constexpr int OFF_W3 = OFF_DQ + B_ * 16 * 2;      // W3^T [16][128] f16, row m = W3^T[m & 3]
 constexpr int OFF_SC = OFF_W3 + 16 * H * 2;       // sloss [8]
 constexpr int LDS = OFF_SC + 32;
 static_assert(LDS <= 160 * 1024, "k_shared_grad4 LDS");
 static_assert(OFF_W3 % 16 == 0, "aligned W3 image");
+
+// Sum over the 16 lanes of each DPP row (quad xor 1, xor 2, half-row mirror,
+// row mirror): every lane of the row ends with the row's sum, in registers
+// (no LDS round trip of a ds_bpermute shuffle).
+__device__ __forceinline__ float row16_sum(float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false));
+    return x;
+}
 
 struct WSlice4 {
     half8 w1[3];   // lane (i, g): W1^T[16w + i][32s + 8g + e] (0 past feature 88)
@@ -1040,10 +1051,9 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
     const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
     WSlice4 W;
     load_slice4(WH, w, W);
-    // W3^T image [16][128]: rows a < 4 the output layer, rows 4..15 zero (the
-    // A operand of the Q MFMA is read straight from it)
-    for (int k = threadIdx.x; k < 16 * H; k += NTH)
-        W3I[k] = k < NACT * H ? WH[L::oW3T + k] : (h16)0.0f;
+    // W3^T image [16][128], row m = W3^T[m & 3]: the A operand of the Q MFMA,
+    // read straight from it, puts row i's four Q values on every lane (i, g)
+    for (int k = threadIdx.x; k < 16 * H; k += NTH) W3I[k] = WH[L::oW3T + (k & (NACT * H - 1))];
     half8 ones;
 #pragma unroll
     for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
@@ -1146,48 +1156,47 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
 #pragma unroll
         for (int s = 0; s < 4; s++)
             cq = mfma(*reinterpret_cast<const half8 *>(W3I + i * H + 32 * s + 8 * g), h2r[s], cq);
-        float term = 0.0f, dq = 0.0f;
-        if (g == 0) {  // lane (i, 0): Q[row][0..3]
-            float q[4];
+        // every lane (i, g) holds Q[row][0..3] (the W3 image repeats its 4 rows):
+        // the loss and dL/dQ of the row on every lane, stored by lanes g = 0
+        float q[4];
 #pragma unroll
-            for (int e = 0; e < 4; e++) q[e] = r16(r16(cq[e]) + (float)W.b3[e]);
-            const float qa = g3::pickf4(q[0], q[1], q[2], q[3], avl);
-            row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
-            dq = r16(dq);  // dL/dQ in f16 (the gradient of the learn's tf.cast)
+        for (int e = 0; e < 4; e++) q[e] = r16(r16(cq[e]) + (float)W.b3[e]);
+        const float qa = g3::pickf4(q[0], q[1], q[2], q[3], avl);
+        float term, dq;
+        row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
+        dq = r16(dq);  // dL/dQ in f16 (the gradient of the learn's tf.cast)
+        if (g == 0) {
             half4v d;
 #pragma unroll
             for (int e = 0; e < 4; e++) d[e] = e == avl ? (h16)dq : (h16)0.0f;
             *reinterpret_cast<half4v *>(DQI + row * 16) = d;
-            if (QSTATS) {
-                float s1 = (q[0] + q[1]) + (q[2] + q[3]);
-                float s2 = (q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]);
-                for (int off = 8; off > 0; off >>= 1) {
-                    s1 += __shfl_xor(s1, off);
-                    s2 += __shfl_xor(s2, off);
-                }
-                if (l == 0) {
-                    atomicAdd(a.qstats + (size_t)agent * 6 + 0, s1);
-                    atomicAdd(a.qstats + (size_t)agent * 6 + 1, s2);
-                }
-            }
         }
-        if (QSTATS)
+        if (QSTATS) {
+            const float s1 = row16_sum((q[0] + q[1]) + (q[2] + q[3]));
+            const float s2 = row16_sum((q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]));
+            if (l == 0) {
+                atomicAdd(a.qstats + (size_t)agent * 6 + 0, s1);
+                atomicAdd(a.qstats + (size_t)agent * 6 + 1, s2);
+            }
 #pragma unroll
             for (int e = 0; e < NACT; e++) {  // every lane takes part in the ballot
                 const float cnt = (float)__popcll(__ballot(g == 0 && avl == e));
                 if (l == 0) atomicAdd(a.qstats + (size_t)agent * 6 + 2 + e, cnt);
             }
-        for (int off = 8; off > 0; off >>= 1) term += __shfl_xor(term, off);
+        }
+        term = row16_sum(term);
         if (l == 0) sloss[w] = term;
         // dZ2 of the row for k = 32s + 8g + e: h16(dq W3[k][a]) where H2 > 0
-        dq = __shfl(dq, i);
+        // (the W3 row of the action read first, then the stores)
+        half8 w3[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) w3[s] = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * s + 8 * g);
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            const half8 w3 = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * s + 8 * g);
             half8 o;
 #pragma unroll
             for (int e = 0; e < 8; e++)
-                o[e] = h2r[s][e] > (h16)0.0f ? (h16)(dq * (float)w3[e]) : (h16)0.0f;
+                o[e] = h2r[s][e] > (h16)0.0f ? (h16)(dq * (float)w3[s][e]) : (h16)0.0f;
             *reinterpret_cast<half8 *>(Z2I + bR + 16 * H * wv + 256 * s) = o;
         }
         // the next agent's X into the other buffer (last read two agents ago)
