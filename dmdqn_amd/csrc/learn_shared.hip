@@ -223,42 +223,43 @@ __device__ __forceinline__ void x_frags(const XTile &x, half8 bx[3]) {
         }
 }
 
-// relu(h16(h16(acc) + b)) of output tile t into the next layer's operand
-// slot: tile t -> K-step t >> 1, elements 4 (t & 1) .. +3.
-__device__ __forceinline__ void dense_out(f32x4 c, const h16 *bias, int t, half8 *ops) {
-    const int g = (threadIdx.x & 63) >> 4;
-    const half4v b = *reinterpret_cast<const half4v *>(bias + 16 * t + 4 * g);
+// relu(h16(h16(acc) + b)) of output tile t (bias b: the tile's 4 values of
+// this lane) into the next layer's operand slot: tile t -> K-step t >> 1,
+// elements 4 (t & 1) .. +3.
+__device__ __forceinline__ void dense_out(f32x4 c, half4v b, int t, half8 *ops) {
     const half4v z = __builtin_convertvector(c, half4v) + b;
 #pragma unroll
     for (int e = 0; e < 4; e++) ops[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
 }
 
+__device__ __forceinline__ half4v bias4(const h16 *bias, int t) {
+    return *reinterpret_cast<const half4v *>(bias + 16 * t + 4 * ((threadIdx.x & 63) >> 4));
+}
+
 // Forward of NT 16-row tiles through a net, every weight fragment read once
 // from LDS and used for the NT tiles: hb1 / hb2 = the layer-1 / layer-2
 // activations as next-layer operands (permuted K order); q = Q on the lanes
-// g = 0 (Q[row i][0..3]; other lanes hold zeros).  DB: each output tile's
-// weight fragments are read from LDS one tile ahead (double-buffered, order
+// g = 0 (Q[row i][0..3]; other lanes hold zeros).  Each output tile's weight
+// fragments and bias are read from LDS one tile ahead (double-buffered, order
 // pinned by scheduling barriers: the LDS latency hides behind the previous
-// tile's MFMAs without the scheduler hoisting every read at once); !DB reads
-// them with the tile (28 fewer VGPRs: the gradient pass, whose accumulators
-// live across the whole launch, would spill).
-template <int NT, bool DB>
+// tile's MFMAs without the scheduler hoisting every read at once, and the
+// epilogue never waits on a bias read).
+template <int NT>
 __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3], half8 (&hb1)[NT][4],
                                           half8 (&hb2)[NT][4], f32x4 (&q)[NT]) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
     {
         half8 cur[3], nxt[3];
-        if (DB)
+        half4v bc = bias4(N.b1, 0), bn = bc;
 #pragma unroll
-            for (int s = 0; s < 3; s++) cur[s] = N.w1[s * 64 + l];
+        for (int s = 0; s < 3; s++) cur[s] = N.w1[s * 64 + l];
 #pragma unroll
         for (int t = 0; t < 8; t++) {
-            if (!DB)
-#pragma unroll
-                for (int s = 0; s < 3; s++) cur[s] = N.w1[(t * 3 + s) * 64 + l];
-            if (DB && t < 7)
+            if (t < 7) {
 #pragma unroll
                 for (int s = 0; s < 3; s++) nxt[s] = N.w1[((t + 1) * 3 + s) * 64 + l];
+                bn = bias4(N.b1, t + 1);
+            }
             f32x4 c[NT];
 #pragma unroll
             for (int n = 0; n < NT; n++) c[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -267,28 +268,27 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
 #pragma unroll
                 for (int n = 0; n < NT; n++) c[n] = mfma(cur[s], bx[n][s], c[n]);
 #pragma unroll
-            for (int n = 0; n < NT; n++) dense_out(c[n], N.b1, t, hb1[n]);
-            if (DB)
+            for (int n = 0; n < NT; n++) dense_out(c[n], bc, t, hb1[n]);
 #pragma unroll
-                for (int s = 0; s < 3; s++) cur[s] = nxt[s];
+            for (int s = 0; s < 3; s++) cur[s] = nxt[s];
+            bc = bn;
             __builtin_amdgcn_sched_barrier(0);
         }
     }
     half8 cur[4], nxt[4];
-    if (DB)
+    half4v bc = bias4(N.b2, 0), bn = bc;
 #pragma unroll
-        for (int s = 0; s < 4; s++) cur[s] = N.w2[s * 64 + l];
+    for (int s = 0; s < 4; s++) cur[s] = N.w2[s * 64 + l];
 #pragma unroll
     for (int t = 0; t < 8; t++) {
-        if (!DB)
-#pragma unroll
-            for (int s = 0; s < 4; s++) cur[s] = N.w2[(t * 4 + s) * 64 + l];
-        if (DB && t < 7)
+        if (t < 7) {
 #pragma unroll
             for (int s = 0; s < 4; s++) nxt[s] = N.w2[((t + 1) * 4 + s) * 64 + l];
-        else if (DB)
+            bn = bias4(N.b2, t + 1);
+        } else {
 #pragma unroll
             for (int s = 0; s < 4; s++) nxt[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
+        }
         f32x4 c[NT];
 #pragma unroll
         for (int n = 0; n < NT; n++) c[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -297,15 +297,12 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
 #pragma unroll
             for (int n = 0; n < NT; n++) c[n] = mfma(cur[s], hb1[n][s], c[n]);
 #pragma unroll
-        for (int n = 0; n < NT; n++) dense_out(c[n], N.b2, t, hb2[n]);
-        if (DB)
+        for (int n = 0; n < NT; n++) dense_out(c[n], bc, t, hb2[n]);
 #pragma unroll
-            for (int s = 0; s < 4; s++) cur[s] = nxt[s];
+        for (int s = 0; s < 4; s++) cur[s] = nxt[s];
+        bc = bn;
         __builtin_amdgcn_sched_barrier(0);
     }
-    if (!DB)
-#pragma unroll
-        for (int s = 0; s < 4; s++) cur[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
     f32x4 c[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) c[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -435,8 +432,8 @@ __global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_
                 for (int n = 0; n < NEXT_NT; n++)
                     x_issue(base + (size_t)slots[RT * (rp + 1) + 16 * n + i] * DMDQN_ROW_BYTES, xt[n]);
             f32x4 qt[NEXT_NT], qo[NEXT_NT];
-            fwd_tiles<NEXT_NT, true>(tg, bx, hb1, hb2, qt);
-            fwd_tiles<NEXT_NT, true>(on, bx, hb1, hb2, qo);
+            fwd_tiles<NEXT_NT>(tg, bx, hb1, hb2, qt);
+            fwd_tiles<NEXT_NT>(on, bx, hb1, hb2, qo);
             if (g == 0) {
 #pragma unroll
                 for (int n = 0; n < NEXT_NT; n++) {

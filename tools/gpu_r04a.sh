@@ -1,9 +1,15 @@
 #!/bin/bash
-# Round-4 GPU call: the -m gpu suite + smoke, then the C2 schedule A/B (one
-# stream vs the fused env step beside the learn, with and without CU masks).
+# Round-4 GPU call: C5 shared-learn A/B (stamps), the -m gpu suite + smoke,
+# then the C2 schedule A/B and the C5 bench line.
 set -e
 O=gpurun_out/r04a
 mkdir -p $O
+for rep in 1 2; do
+  timeout -k 10 120 python tools/stamp_shared.py > $O/stamp_grad4_$rep.json
+  timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_nextprev.so > $O/stamp_nextprev_$rep.json
+  timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_grad3.so > $O/stamp_grad3_$rep.json
+done
+cat $O/stamp_grad4_2.json $O/stamp_nextprev_2.json $O/stamp_grad3_2.json
 bash tools/gpu_tests.sh r04a
 for rep in 1 2; do
   for v in "none" "env" "env --cu-split 32" "env --cu-split 64"; do
@@ -13,3 +19,5 @@ for rep in 1 2; do
     echo "$v $rep $(python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])" $f)"
   done
 done
+timeout -k 10 300 python bench.py --shared --rows 8 --cols 8 --envs 256 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err
+tail -1 $O/bench_c5.json | cut -c1-300
