@@ -8,8 +8,9 @@ for rep in 1 2; do
   timeout -k 10 120 python tools/stamp_shared.py > $O/stamp_grad4_$rep.json
   timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_nextprev.so > $O/stamp_nextprev_$rep.json
   timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_grad3.so > $O/stamp_grad3_$rep.json
+  timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_grad5.so > $O/stamp_grad5_$rep.json
 done
-cat $O/stamp_grad4_2.json $O/stamp_nextprev_2.json $O/stamp_grad3_2.json
+cat $O/stamp_grad4_2.json $O/stamp_nextprev_2.json $O/stamp_grad3_2.json $O/stamp_grad5_2.json
 bash tools/gpu_tests.sh r04a
 for rep in 1 2; do
   for v in "none" "env" "env --cu-split 32" "env --cu-split 64"; do

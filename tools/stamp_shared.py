@@ -67,5 +67,5 @@ tag = os.path.basename(sys.argv[1])[:-3] if len(sys.argv) > 1 else "product"
 os.makedirs("gpurun_out", exist_ok=True)
 np.save(f"gpurun_out/grad_{tag}.npy", ag.grad.cpu().numpy())
 out["lib"] = (os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else "product") + \
-    (" k_shared_grad3" if GRAD3 else " k_shared_grad4")
+    (" k_shared_grad3" if GRAD3 else " k_shared_grad5" if "grad5" in (sys.argv[1] if len(sys.argv) > 1 else "") else " k_shared_grad4")
 print(json.dumps(out))
