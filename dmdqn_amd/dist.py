@@ -43,11 +43,12 @@ def _fail(call, exc):
                     f"{type(exc).__name__}: {exc}") from exc
 
 
-def init(backend=None, device=None, timeout_s=None):
+def init(backend=None, device=None, timeout_s=None, force=False):
     """init_process_group from the torch.distributed.run environment, with a
-    timeout (rendezvous and the backend's operations); raises DistError."""
+    timeout (rendezvous and the backend's operations); raises DistError.
+    force: also for a world of one (tests: the RCCL path on a one-GPU box)."""
     rank, ws, local = world()
-    if ws > 1 and not dist.is_initialized():
+    if (ws > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"

@@ -157,3 +157,51 @@ def test_c5_allreduce_beside_next_step_bit_identical():
     for r in range(2):
         for k in ("params", "target", "loss", "idx", "obs"):
             np.testing.assert_array_equal(ovl[r][k], seq[r][k], err_msg=f"rank {r} {k}")
+
+
+_NCCL_ONE_RANK = r"""
+import os, sys, json, torch
+sys.path.insert(0, sys.argv[1])
+import torch.distributed as dist
+from dmdqn_amd import dist as D
+from dmdqn_amd.agent import AgentConfig, BatchedDQN
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+D.init(backend="nccl", device=dev, timeout_s=60, force=True)
+assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+D.barrier(30)
+m = D.max_over_ranks(1.25, device=dev, timeout_s=30)
+ag = BatchedDQN(2, 4, AgentConfig(precision="fp16", shared_params=True, replay_buffer_size=200))
+g = torch.Generator(device="cuda").manual_seed(0)
+for t in range(130):
+    s = torch.randint(-1, 24, (2, 4, 89), device=dev, generator=g).float()
+    a = torch.randint(0, 4, (2, 4), device=dev, generator=g, dtype=torch.int32)
+    r = -torch.rand((2, 4), device=dev, generator=g, dtype=torch.float64) * 100
+    ag.remember(s, a, r, s, False)
+ag.learn()
+g0 = ag.grad.clone()
+dist.all_reduce(ag.grad, op=dist.ReduceOp.SUM)  # RCCL, one rank: the identity
+torch.cuda.synchronize()
+print(json.dumps({"max": m, "same": bool(torch.equal(g0, ag.grad)),
+                  "finite": bool(torch.isfinite(g0).all())}))
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_one_rank_group_on_this_gpu():
+    """The nccl (= RCCL) branch of dmdqn_amd.dist on the real device: a
+    one-rank process group with device_id and timeouts, the timed barrier,
+    the max-over-ranks all-reduce and an all-reduce of a C5 gradient on the
+    learn's buffer (the identity for one rank).  The driver's multi-GPU run
+    takes this code path first; a failure here names the call."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+               WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", _NCCL_ONE_RANK, root], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert out == {"max": 1.25, "same": True, "finite": True}
