@@ -1286,322 +1286,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
 
 }  // namespace g4
 
-// ---------------------------------------------------------------- pass 2, v5
-// k_shared_grad4 with the forward layers L1 / L2 on TWO neuron tiles per
-// wave: wave w = (ng, rh) = (w & 3, w >> 2) computes neurons 32 ng .. 32 ng +
-// 31 for the 64 batch rows 64 rh .., so every activation fragment it reads
-// from LDS feeds two MFMAs (half the image reads of one tile per wave).  From
-// the loss on, every phase is k_shared_grad4's with the wave's own tile
-// tw = 2 ng + rh (one of its two forward tiles), over all 128 rows.
-namespace g5 {
-using g4::OFF_X; using g4::OFF_H1; using g4::OFF_Z2; using g4::OFF_H2; using g4::OFF_DQ;
-using g4::OFF_W3; using g4::OFF_SC; using g4::LDS; using g3::X_BYTES;
-
-struct WSlice5 {
-    half8 w1[2][3];  // forward tile t (neurons 32ng + 16t + i): W1^T[.][32s + 8g + e]
-    half8 w2[2][4];  // W2^T[32ng + 16t + i][32s + 8g + e]
-    half8 w2b[4];    // W2[16tw + i][32s + 8g + e]  (= W2^T[k][j], the dH1 tile)
-    half4v b1[2], b2[2], b3;
-};
-
-__device__ __forceinline__ void load_slice5(const h16 *WH, int ng, int tw, WSlice5 &S) {
-    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-        const int j = 32 * ng + 16 * t + i;
-#pragma unroll
-        for (int s = 0; s < 3; s++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const int f = 32 * s + 8 * g + e;
-                S.w1[t][s][e] = f < QN_D ? WH[L::oW1T + qn_w1<H>(j, f)] : (h16)0.0f;
-            }
-#pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) S.w2[t][s][e] = WH[L::oW2T + qn_wt(j, 32 * s + 8 * g + e, H)];
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int k = 32 * ng + 16 * t + 4 * g + e;
-            S.b1[t][e] = WH[L::ob1 + k];
-            S.b2[t][e] = WH[L::ob1 + H + k];
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < 4; s++)
-#pragma unroll
-        for (int e = 0; e < 8; e++) S.w2b[s][e] = WH[L::oW2T + qn_wt(32 * s + 8 * g + e, 16 * tw + i, H)];
-#pragma unroll
-    for (int e = 0; e < 4; e++) S.b3[e] = WH[L::ob1 + 2 * H + e];
-}
-
-template <bool QSTATS>
-__global__ void __launch_bounds__(512, 1) k_shared_grad5(dmdqn_learn_args a, const float *y_in,
-                                                       const uint8_t *act_in, float *slab) {
-    constexpr int NTH = 512;
-    __shared__ __attribute__((aligned(16))) char smem[LDS];
-    h16 *H1I = reinterpret_cast<h16 *>(smem + OFF_H1), *Z2I = reinterpret_cast<h16 *>(smem + OFF_Z2);
-    h16 *H2I = reinterpret_cast<h16 *>(smem + OFF_H2), *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
-    h16 *W3I = reinterpret_cast<h16 *>(smem + OFF_W3);
-    float *sloss = reinterpret_cast<float *>(smem + OFF_SC);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    const int ng = w & 3, tw = 2 * ng + (w >> 2);
-    const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
-    WSlice5 W;
-    load_slice5(WH, ng, tw, W);
-    for (int k = threadIdx.x; k < 16 * H; k += NTH) W3I[k] = WH[L::oW3T + (k & (NACT * H - 1))];
-    half8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
-    f32x4 G1[6], G2[8], G3, GB1, GB2, GB3;
-    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < 6; f++) G1[f] = z4;
-#pragma unroll
-    for (int j = 0; j < 8; j++) G2[j] = z4;
-    G3 = GB1 = GB2 = GB3 = z4;
-    for (int k = threadIdx.x; k < B_ * 16; k += NTH) DQI[k] = (h16)0.0f;
-    const int row = 16 * w + i;  // this lane's batch row in the RQ phase
-    int wv = w;
-    asm volatile("" : "+v"(wv));
-    const int rbase = 4 * (wv >> 2);  // first own row tile of the forward layers
-    const int bR = hoff(i, 8 * g), bX = hoff<DP>(i, 8 * g);
-    const int trH[2] = {hsplit(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    const int trX[2] = {hsplit<DP>(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit<DP>(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    // forward tiles 2ng, 2ng + 1: C-layout write bases (neurons 32 ng .. 32 ng + 31)
-    const int c2 = 32 * (wv & 3);
-    const int bWf[2] = {hoff(i, 4 * g) + 256 * (c2 >> 5), hoff(i, 16 + 4 * g) + 256 * (c2 >> 5)};
-    // the reduction phases' own tile tw
-    const int twv = 2 * (wv & 3) + (wv >> 2), c0 = 16 * twv;
-    const int bW = hoff(i, (c0 & 16) + 4 * g) + 256 * (c0 >> 5);
-    const int trO = hsplit(8 * (g & 1) + (i >> 2), (c0 & 16) + 4 * (i & 3), g >> 1, 0) + 256 * (c0 >> 5);
-    const bool stager = threadIdx.x < 256;
-    int agent = blockIdx.x;
-    if (agent < a.NA && stager) {
-        g3::XRows x0;
-        g3::xrows_issue<NTH>(a, agent, g3::pos3(a, agent, threadIdx.x), threadIdx.x, x0);
-        g3::xrows_commit(x0, reinterpret_cast<h16 *>(smem + OFF_X), threadIdx.x);
-    }
-    int npos = g3::pos3(a, agent + gridDim.x, threadIdx.x);
-    float yv = 0.0f;
-    int avl = 0;
-    if (agent < a.NA) {
-        yv = y_in[(size_t)agent * B_ + row];
-        avl = act_in[(size_t)agent * B_ + row];
-    }
-    __syncthreads();
-    int buf = 0;
-    for (; agent < a.NA; agent += gridDim.x, buf ^= 1) {
-        SH_STAMP(agent, 0, threadIdx.x);
-        const h16 *X = reinterpret_cast<const h16 *>(smem + OFF_X + buf * X_BYTES);
-        const int nxt = agent + gridDim.x;
-        g3::XRows xn;
-        float yn = 0.0f;
-        int an = 0;
-        if (nxt < a.NA && stager) g3::xrows_issue<NTH>(a, nxt, npos, threadIdx.x, xn);
-        if (nxt < a.NA) {
-            yn = y_in[(size_t)nxt * B_ + row];
-            an = act_in[(size_t)nxt * B_ + row];
-        }
-        npos = g3::pos3(a, nxt + gridDim.x, threadIdx.x);
-        // ---- L1: tiles 2ng, 2ng + 1 x rows 64rh .. (two row tiles per pass)
-#pragma unroll
-        for (int hf = 0; hf < 2; hf++) {
-            f32x4 c[2][2];
-#pragma unroll
-            for (int r = 0; r < 2; r++)
-#pragma unroll
-                for (int t = 0; t < 2; t++) c[r][t] = z4;
-#pragma unroll
-            for (int s = 0; s < 3; s++) {
-                half8 xb[2];
-#pragma unroll
-                for (int r = 0; r < 2; r++)
-                    xb[r] = *reinterpret_cast<const half8 *>(X + bX + 16 * DP * (rbase + 2 * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < 2; r++)
-#pragma unroll
-                    for (int t = 0; t < 2; t++) c[r][t] = mfma(W.w1[t][s], xb[r], c[r][t]);
-            }
-#pragma unroll
-            for (int r = 0; r < 2; r++)
-#pragma unroll
-                for (int t = 0; t < 2; t++)
-                    *reinterpret_cast<half4v *>(H1I + bWf[t] + 16 * H * (rbase + 2 * hf + r)) =
-                        g3::relu4(c[r][t], W.b1[t]);
-        }
-        SH_STAMP(agent, 1, threadIdx.x);
-        __syncthreads();  // B1: H1 image
-        // ---- L2: the same tiles and rows -> H2 image
-#pragma unroll
-        for (int hf = 0; hf < 2; hf++) {
-            f32x4 c[2][2];
-#pragma unroll
-            for (int r = 0; r < 2; r++)
-#pragma unroll
-                for (int t = 0; t < 2; t++) c[r][t] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 hb[2];
-#pragma unroll
-                for (int r = 0; r < 2; r++)
-                    hb[r] = *reinterpret_cast<const half8 *>(H1I + bR + 16 * H * (rbase + 2 * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < 2; r++)
-#pragma unroll
-                    for (int t = 0; t < 2; t++) c[r][t] = mfma(W.w2[t][s], hb[r], c[r][t]);
-            }
-#pragma unroll
-            for (int r = 0; r < 2; r++)
-#pragma unroll
-                for (int t = 0; t < 2; t++)
-                    *reinterpret_cast<half4v *>(H2I + bWf[t] + 16 * H * (rbase + 2 * hf + r)) =
-                        g3::relu4(c[r][t], W.b2[t]);
-        }
-        SH_STAMP(agent, 2, threadIdx.x);
-        __syncthreads();  // B2: H2 image
-        // ---- RQ: rows 16w + i (as k_shared_grad4)
-        {
-            half8 h2r[4];
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                h2r[s] = *reinterpret_cast<const half8 *>(H2I + bR + 16 * H * wv + 256 * s);
-            f32x4 cq = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                cq = mfma(*reinterpret_cast<const half8 *>(W3I + i * H + 32 * s + 8 * g), h2r[s], cq);
-            float q[4];
-#pragma unroll
-            for (int e = 0; e < 4; e++) q[e] = r16(r16(cq[e]) + (float)W.b3[e]);
-            const float qa = g3::pickf4(q[0], q[1], q[2], q[3], avl);
-            float term, dq;
-            row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
-            dq = r16(dq);  // dL/dQ in f16 (the gradient of the learn's tf.cast)
-            if (g == 0) {
-                half4v d;
-#pragma unroll
-                for (int e = 0; e < 4; e++) d[e] = e == avl ? (h16)dq : (h16)0.0f;
-                *reinterpret_cast<half4v *>(DQI + row * 16) = d;
-            }
-            if (QSTATS) {
-                const float s1 = g4::row16_sum((q[0] + q[1]) + (q[2] + q[3]));
-                const float s2 = g4::row16_sum((q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]));
-                if (l == 0) {
-                    atomicAdd(a.qstats + (size_t)agent * 6 + 0, s1);
-                    atomicAdd(a.qstats + (size_t)agent * 6 + 1, s2);
-                }
-#pragma unroll
-                for (int e = 0; e < NACT; e++) {  // every lane takes part in the ballot
-                    const float cnt = (float)__popcll(__ballot(g == 0 && avl == e));
-                    if (l == 0) atomicAdd(a.qstats + (size_t)agent * 6 + 2 + e, cnt);
-                }
-            }
-            term = g4::row16_sum(term);
-            if (l == 0) sloss[w] = term;
-#pragma unroll
-            for (int sp = 0; sp < 4; sp += 2) {  // two W3 row chunks read, then their stores
-                half8 w3[2];
-#pragma unroll
-                for (int s = 0; s < 2; s++)
-                    w3[s] = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * (sp + s) + 8 * g);
-#pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    half8 o;
-#pragma unroll
-                    for (int e = 0; e < 8; e++)
-                        o[e] = h2r[sp + s][e] > (h16)0.0f ? (h16)(dq * (float)w3[s][e]) : (h16)0.0f;
-                    *reinterpret_cast<half8 *>(Z2I + bR + 16 * H * wv + 256 * (sp + s)) = o;
-                }
-            }
-        }
-        if (nxt < a.NA && stager)  // the next agent's X into the other buffer
-            g3::xrows_commit(xn, reinterpret_cast<h16 *>(smem + OFF_X + (buf ^ 1) * X_BYTES),
-                             threadIdx.x);
-        SH_STAMP(agent, 3, threadIdx.x);
-        __syncthreads();  // B3: DQ, dZ2 image, loss partials, next X
-        if (threadIdx.x == 0 && a.loss) {
-            float ls = sloss[0];
-            for (int v = 1; v < 8; v++) ls += sloss[v];
-            a.loss[agent] = ls / (float)B_;
-        }
-        // ---- from here on k_shared_grad4 with the own tile tw
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const half8 dqf = frag_tr(DQI, 16, 32 * s, 0);
-            G3 = mfma(frag_tr_p(H2I + trO + 2 * 16 * H * s), dqf, G3);
-            if (w == 0) GB3 = mfma(ones, dqf, GB3);
-        }
-        SH_STAMP(agent, 4, threadIdx.x);
-#pragma unroll
-        for (int hf = 0; hf < 4; hf++) {  // two row tiles per pass
-            f32x4 c[2];
-#pragma unroll
-            for (int r = 0; r < 2; r++) c[r] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 zb[2];
-#pragma unroll
-                for (int r = 0; r < 2; r++)
-                    zb[r] = *reinterpret_cast<const half8 *>(Z2I + bR + 16 * H * (2 * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < 2; r++) c[r] = mfma(W.w2b[s], zb[r], c[r]);
-            }
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const int rt = 2 * hf + r;
-                half4v o;
-                const half4v hv = *reinterpret_cast<const half4v *>(H1I + bW + 16 * H * rt);
-#pragma unroll
-                for (int e = 0; e < 4; e++) o[e] = hv[e] > (h16)0.0f ? (h16)c[r][e] : (h16)0.0f;
-                *reinterpret_cast<half4v *>(H2I + bW + 16 * H * rt) = o;
-            }
-        }
-        SH_STAMP(agent, 5, threadIdx.x);
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const half8 bq = frag_tr_p(Z2I + trO + 2 * 16 * H * s);
-            const half8 bv = frag_tr_p(H2I + trO + 2 * 16 * H * s);
-            GB2 = mfma(ones, bq, GB2);
-            GB1 = mfma(ones, bv, GB1);
-#pragma unroll
-            for (int jt = 0; jt < 8; jt++)
-                G2[jt] = mfma(frag_tr_p(H1I + trH[jt & 1] + 256 * (jt >> 1) + 2 * 16 * H * s), bq, G2[jt]);
-#pragma unroll
-            for (int ft = 0; ft < 6; ft++)
-                G1[ft] = mfma(frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s), bv, G1[ft]);
-        }
-        yv = yn;
-        avl = an;
-        SH_STAMP(agent, 6, threadIdx.x);
-        __syncthreads();  // B4: the images are rewritten by the next agent
-        SH_STAMP(agent, 7, threadIdx.x);
-    }
-    // partial sums of this workgroup, kernel layout (every index written once)
-    float *G = slab + (size_t)blockIdx.x * L::P;
-    const int n0 = 16 * tw, n = n0 + i;  // this lane's neuron (C-tile column)
-    if (i < NACT)  // G3: rows k = n0 + 4g + e, column a = i
-        *reinterpret_cast<float4 *>(G + L::oW3T + i * H + n0 + 4 * g) =
-            make_float4(G3[0], G3[1], G3[2], G3[3]);
-#pragma unroll
-    for (int jt = 0; jt < 8; jt++)  // G2[jt]: fan-in j = 16jt + 4g + e, fan-out k = n
-        *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(n, 16 * jt + 4 * g, H)) =
-            make_float4(G2[jt][0], G2[jt][1], G2[jt][2], G2[jt][3]);
-    if (g == 0) {
-        G[L::ob2 + n] = GB2[0];
-        G[L::ob1 + n] = GB1[0];
-    }
-#pragma unroll
-    for (int ft = 0; ft < 6; ft++)  // G1[ft]: features 16ft + 4g + e, neuron n
-        if (ft < 5 || g < 2)
-            *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(n, 16 * ft + 4 * g)) =
-                make_float4(G1[ft][0], G1[ft][1], G1[ft][2], G1[ft][3]);
-    if (g == 2) G[L::oW1X + n] = G1[5][0];  // feature 88
-    if (w == 0 && g == 0 && i < NACT) G[L::ob3 + i] = GB3[0];
-}
-
-}  // namespace g5
 
 
 }  // namespace shk
@@ -1619,8 +1303,6 @@ int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *s
 #endif
 #if SH_GRAD == 3
     auto k = a->qstats ? g3::k_shared_grad3<true, 1> : g3::k_shared_grad3<false, 1>;
-#elif SH_GRAD == 5
-    auto k = a->qstats ? g5::k_shared_grad5<true> : g5::k_shared_grad5<false>;
 #else
     auto k = a->qstats ? g4::k_shared_grad4<true> : g4::k_shared_grad4<false>;
 #endif

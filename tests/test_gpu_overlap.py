@@ -66,23 +66,23 @@ def test_overlap_on_cu_masked_streams_matches_sequential():
 @pytest.mark.parametrize("masked", [False, True])
 def test_env_beside_learn_on_a_wrapped_ring(masked):
     """overlap "env": the fused env step of t+1 beside learn t, with the ring
-    wrapped (replay 120 < 170 steps), so every store lands in the spare slot
+    wrapped (replay 150 < 170 steps, learns from step 128), so every store lands in the spare slot
     the running learn cannot sample (kernels.ReplayRing) -- bit-identical to
     the one-stream order, also with the two streams CU-masked (bench
     --cu-split)."""
     from dmdqn_amd._lib import cu_masked_stream
-    ref = _trainer("none", "bf16", False, False, cap=120)
+    ref = _trainer("none", "bf16", False, False, cap=150)
     a = _run(ref, 170)
     if masked:
         n_cu = torch.cuda.get_device_properties(0).multi_processor_count
         main, side = cu_masked_stream(range(64, n_cu)), cu_masked_stream(range(64))
         with torch.cuda.stream(main):
-            ovl = _trainer("env", "bf16", False, False, side_stream=side, cap=120)
+            ovl = _trainer("env", "bf16", False, False, side_stream=side, cap=150)
             b = _run(ovl, 170)
     else:
-        ovl = _trainer("env", "bf16", False, False, cap=120)
+        ovl = _trainer("env", "bf16", False, False, cap=150)
         b = _run(ovl, 170)
-    assert ovl.agent.ring.start != 0
+    assert ovl.agent.ring.start != 0 and ovl.agent.learn_launches == 170 - 127
     _compare(ref, ovl, a, b)
 
 

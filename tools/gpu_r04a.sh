@@ -1,16 +1,9 @@
 #!/bin/bash
-# Round-4 GPU call: C5 shared-learn A/B (stamps), the -m gpu suite + smoke,
-# then the C2 schedule A/B and the C5 bench line.
+# Round-4 GPU call: the -m gpu suite + smoke, then the C2 schedule A/B and the
+# C5 bench line (the C5 shared-learn stamp A/B: tools/stamp_shared.py [lib]).
 set -e
 O=gpurun_out/r04a
 mkdir -p $O
-for rep in 1 2; do
-  timeout -k 10 120 python tools/stamp_shared.py > $O/stamp_grad4_$rep.json
-  timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_nextprev.so > $O/stamp_nextprev_$rep.json
-  timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_grad3.so > $O/stamp_grad3_$rep.json
-  timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_grad5.so > $O/stamp_grad5_$rep.json
-done
-cat $O/stamp_grad4_2.json $O/stamp_nextprev_2.json $O/stamp_grad3_2.json $O/stamp_grad5_2.json
 bash tools/gpu_tests.sh r04a
 for rep in 1 2; do
   for v in "none" "env" "env --cu-split 32" "env --cu-split 64"; do
