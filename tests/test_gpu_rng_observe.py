@@ -134,11 +134,13 @@ def test_replay_store_roundtrip_and_range_check():
         ring.store(s.to(DEV), n.to(DEV), a.to(DEV), r.to(DEV), d.to(DEV))
         rows.append((s, n, a, r, d))
     ring.check()
-    assert len(ring) == cap and ring.start == 10 % cap
+    # a deque of maxlen cap in cap + 1 slots: position p -> slot (start + p) % (cap + 1)
+    assert len(ring) == cap and ring.slots == cap + 1 and ring.start == (10 - cap) % (cap + 1)
     S = ring.s.cpu().numpy()
-    for p in range(cap):  # deque position p -> ring slot (start + p) % cap
+    for p in range(cap):
         t = 10 - cap + p
-        slot = (ring.start + p) % cap
+        slot = int(ring.slots_of(p))
+        assert slot == t % (cap + 1)
         s, n, a, r, d = rows[t]
         np.testing.assert_array_equal(S[:, slot, :89].astype(np.float32), s.numpy())
         np.testing.assert_array_equal(S[:, slot, 89:], 0)
