@@ -97,11 +97,12 @@ def test_synthetic_drain_and_max_time_reasons():
 
 def test_int_sumo_seed_reseeds_the_synthetic_demand():
     env = SumoTrafficEnvironment(None, None, [{"id": j} for j in _ids(2, 2)], step_duration=10,
-                                 max_simulation_time=2400,
+                                 max_simulation_time=100,
                                  env_config=EnvConfig(rows=2, cols=2, seed=1))
     env.reset(sumo_seed=7)
     ref = O.OracleEnv(2, 2, 7)
-    _drive(env, ref, 2, 2, 100, 10, seed=2)  # reset(sumo_seed="random") keeps seed 7
+    steps, info, _ = _drive(env, ref, 2, 2, 100, 10, seed=2)  # reset("random") keeps seed 7
+    assert steps == 10 and info["termination_reason"] == "max_time_reached"
 
 
 def test_action_phases_strings_and_one_second_steps():
