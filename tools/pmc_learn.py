@@ -4,8 +4,8 @@ the learn kernel, with the gfx950 corrections of MI355X_MICROARCH.md (HBM):
   * WRITE_SIZE (KB) is exact for 16-byte stores
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (TCC slots).
 Usage: python tools/pmc_learn.py <fetch_csv> <write_csv> <workload_key> [kernel_substr] [source]
-(kernel_substr: one name, or a comma list of the kernels one learn launches --
-their per-dispatch means are summed; source: where the passes were run, e.g.
+(kernel_substr: one name, or a '|' list of the kernels one learn launches --
+their per-dispatch means are summed (template names hold commas); source: where the passes were run, e.g.
 "profiles/r03/c3 @ <commit>").
 Writes/updates profiles/learn_pmc.json."""
 import csv
@@ -32,7 +32,7 @@ def main():
     source = sys.argv[5] if len(sys.argv) > 5 else None
     fetch_kb = write_kb = 0.0
     counts = []
-    for name in substr.split(","):
+    for name in substr.split("|"):
         fv = per_kernel(fetch_csv, "FETCH_SIZE", name)
         wv = per_kernel(write_csv, "WRITE_SIZE", name)
         if not fv or not wv:
@@ -53,7 +53,7 @@ def main():
     if source:
         d[key]["source"] = source
     # the kernel sources the passes measured (bench.py: traffic_stale when HEAD's differ)
-    kind = "sim" if key.endswith("_sim") else "learn"
+    kind = "sim" if key.endswith("_sim") or key.endswith("_envstep") else "learn"
     d[key]["sources_digest"] = {"kind": kind, "sha256_16": source_digest(kind)}
     with open(out, "w") as f:
         json.dump(d, f, indent=1)

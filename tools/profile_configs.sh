@@ -21,7 +21,7 @@ for CFG in "$@"; do
             SIMK="k_sim_step<true, false, false>"; ENVK="k_sim_step<true, false, true>" ;;
         c3) ARGS="--rows 4 --cols 4 --envs 1024 --precision fp16"; KEY=4x4x1024_fp16; LK=k_learn_f16
             SIMK="k_sim_step<true, false, false>"; ENVK="k_sim_step<true, false, true>" ;;
-        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK=k_shared_next,k_shared_grad,k_reduce_slabs,k_adam
+        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK="k_shared_next|k_shared_grad|k_reduce_slabs|k_adam"
             SIMK="k_sim_step_reg<1024, false>"; ENVK="k_sim_step_reg<1024, true>" ;;
         *) echo "unknown config $CFG"; exit 2 ;;
     esac
@@ -48,7 +48,7 @@ for CFG in "$@"; do
     (cd $R && python3 tools/pmc_learn.py "$F" "$W" "$KEY" "$LK" "profiles/$TAG/$CFG" &&
          python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_sim" "$SIMK" "profiles/$TAG/$CFG" &&
          python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_envstep" "$ENVK" "profiles/$TAG/$CFG" &&
-         for K1 in ${LK//,/ }; do python3 tools/pmc_mfma.py "$M" "$K1" > $O/mfma_busy_$K1.json; done)
+         for K1 in ${LK//|/ }; do python3 tools/pmc_mfma.py "$M" "$K1" > $O/mfma_busy_$K1.json; done)
     cp "$(find $O/stats -name '*kernel_stats.csv' | head -n 1)" $O/kernel_stats.csv
     gzip -c "$F" > $O/fetch_size_counter_collection.csv.gz
     gzip -c "$W" > $O/write_size_counter_collection.csv.gz
