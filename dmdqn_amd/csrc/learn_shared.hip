@@ -976,6 +976,12 @@ __global__ void __launch_bounds__(64 * (8 / NT), 1) k_shared_grad3(dmdqn_learn_a
 //   G   dW3 (H2 own^T, DQ) ; dH1 own (dZ2 image) -> dZ1 own (over H2 own) ;
 //       dW2 (H1^T, dZ2 own) ; dW1 (X^T, dZ1 own)
 // Same rounding points as k_shared_grad3 (Keras' mixed policy).
+#ifndef SH_G4_ORDER
+#define SH_G4_ORDER 0  // 1: dH1 interleaved with dW2 (tools/build_exp.py A/B)
+#endif
+#ifndef SH_G4_RH
+#define SH_G4_RH 4
+#endif
 namespace g4 {
 using g3::X_BYTES;
 using g3::IMG;
@@ -1038,7 +1044,7 @@ __device__ __forceinline__ void load_slice4(const h16 *WH, int w, WSlice4 &S) {
 template <bool QSTATS>
 __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, const float *y_in,
                                                        const uint8_t *act_in, float *slab) {
-    constexpr int NTH = 512, RH = 4;
+    constexpr int NTH = 512, RH = SH_G4_RH;  // row tiles per pass of L1 / L2 / dH1
     __shared__ __attribute__((aligned(16))) char smem[LDS];
     h16 *H1I = reinterpret_cast<h16 *>(smem + OFF_H1), *Z2I = reinterpret_cast<h16 *>(smem + OFF_Z2);
     h16 *H2I = reinterpret_cast<h16 *>(smem + OFF_H2), *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
@@ -1149,6 +1155,12 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
 #pragma unroll
         for (int s = 0; s < 4; s++)
             h2r[s] = *reinterpret_cast<const half8 *>(H2I + bR + 16 * H * wv + 256 * s);
+#if SH_G4_ORDER
+        // the W3 row of the row's action (dZ2 below), read with the H2 rows
+        half8 w3[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) w3[s] = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * s + 8 * g);
+#endif
         f32x4 cq = z4;
 #pragma unroll
         for (int s = 0; s < 4; s++)
@@ -1185,9 +1197,11 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         if (l == 0) sloss[w] = term;
         // dZ2 of the row for k = 32s + 8g + e: h16(dq W3[k][a]) where H2 > 0
         // (the W3 row of the action read first, then the stores)
+#if !SH_G4_ORDER
         half8 w3[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) w3[s] = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * s + 8 * g);
+#endif
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             half8 o;
@@ -1215,6 +1229,56 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             if (w == 0) GB3 = mfma(ones, dqf, GB3);
         }
         SH_STAMP(agent, 4, threadIdx.x);
+#if SH_G4_ORDER
+        // ---- dH1 (own j, all rows) interleaved with dW2[j][k own] / db2 (K =
+        // rows): both read only the dZ2 and H1 images, so their MFMAs fill each
+        // other's LDS latency; then dZ1 own -> image (over this wave's H2
+        // columns), then dW1[f][j own] / db1 from it.  Same sums in the same
+        // order as the sequential form below: bit-identical.
+        {
+            f32x4 c[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) c[r] = z4;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const half8 bq = frag_tr_p(Z2I + trO + 2 * 16 * H * s);
+                GB2 = mfma(ones, bq, GB2);
+#pragma unroll
+                for (int hf = 0; hf < 2; hf++) {
+                    half8 zb[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        zb[r] = *reinterpret_cast<const half8 *>(Z2I + bR + 16 * H * (4 * hf + r) + 256 * s);
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++) {
+                        const int jt = 4 * hf + jj;
+                        G2[jt] = mfma(frag_tr_p(H1I + trH[jt & 1] + 256 * (jt >> 1) + 2 * 16 * H * s), bq, G2[jt]);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; r++) c[4 * hf + r] = mfma(W.w2b[s], zb[r], c[4 * hf + r]);
+                }
+            }
+            SH_STAMP(agent, 5, threadIdx.x);
+            half4v hv[8];
+#pragma unroll
+            for (int rt = 0; rt < 8; rt++) hv[rt] = *reinterpret_cast<const half4v *>(H1I + bW + 16 * H * rt);
+#pragma unroll
+            for (int rt = 0; rt < 8; rt++) {
+                half4v o;
+#pragma unroll
+                for (int e = 0; e < 4; e++) o[e] = hv[rt][e] > (h16)0.0f ? (h16)c[rt][e] : (h16)0.0f;
+                *reinterpret_cast<half4v *>(H2I + bW + 16 * H * rt) = o;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const half8 bv = frag_tr_p(H2I + trO + 2 * 16 * H * s);
+            GB1 = mfma(ones, bv, GB1);
+#pragma unroll
+            for (int ft = 0; ft < 6; ft++)
+                G1[ft] = mfma(frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s), bv, G1[ft]);
+        }
+#else
         // ---- dH1 (own j) -> dZ1 own -> image (over this wave's H2 columns)
 #pragma unroll
         for (int hf = 0; hf < 8 / RH; hf++) {
@@ -1255,6 +1319,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             for (int ft = 0; ft < 6; ft++)
                 G1[ft] = mfma(frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s), bv, G1[ft]);
         }
+#endif
         yv = yn;
         avl = an;
         SH_STAMP(agent, 6, threadIdx.x);

@@ -1,0 +1,11 @@
+#!/bin/bash
+# C5 shared-learn variant A/B, unperturbed HIP-event timing (tools/stamp_shared.py --nostamp).
+set -e
+O=gpurun_out/r04d
+mkdir -p $O
+for rep in 1 2 3; do
+  for v in g4base g4order g4rh8 g4order_rh8 next12 next16nt1; do
+    timeout -k 10 120 python tools/stamp_shared.py exp/libdmdqn_hip_$v.so --nostamp >> $O/ab.jsonl
+  done
+done
+cat $O/ab.jsonl
