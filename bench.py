@@ -188,6 +188,14 @@ def _step_roofline(value, K, vbar, A, P, shared, NA):
             "parts": {"sim": round(b_sim, 1), "obs": 424, "store": 721, "learn": round(b_learn, 1)}}
 
 
+# --overlap auto: C2 (1,024 agents) runs 3.35 M steps/s on one
+# stream, 4.03 M with the env step of t+1 beside learn t, 4.21 M with that side
+# stream on 64 CUs (32: 3.92 M, 96: 3.79 M); C3 gains 1-3 % with a slower learn
+# kernel, so it and C5 stay on one stream (profiles/r04/c2_schedules, c3_schedules)
+AUTO_ENV_MAX_AGENTS = 4096
+AUTO_ENV_CU_SPLIT = 64
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,8 +220,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=60,
                     help="timed RL steps per replica of the CPU baseline")
-    ap.add_argument("--overlap", default="none", choices=["none", "sample", "full", "env"],
-                    help="stream schedule (dmdqn_amd/trainer.py; all bit-identical): none = one "
+    ap.add_argument("--overlap", default="auto", choices=["auto", "none", "sample", "full", "env"],
+                    help="stream schedule (dmdqn_amd/trainer.py; all bit-identical): auto = "
+                         "env with the side stream on 64 CUs for independent nets of at most "
+                         f"{AUTO_ENV_MAX_AGENTS} agents per GPU (C2: the learn's compute phase "
+                         "leaves most of the chip idle), else none; none = one "
                          "stream; sample = replay draws on a side stream beside act/sim/observe/"
                          "store; full = step t+1's act/sim/observe/sample beside learn t; env = "
                          "step t+1's fused env step (store in the ring's spare slot) + draws "
@@ -221,8 +232,8 @@ def main():
     ap.add_argument("--split-learn", action="store_true",
                     help="independent learn as two launches (gradient, Adam; bit-identical; "
                          "trainer.py split_learn)")
-    ap.add_argument("--cu-split", type=int, default=0,
-                    help="with --overlap full/sample: run the side stream on this many CUs "
+    ap.add_argument("--cu-split", type=int, default=None,
+                    help="with --overlap full/sample/env: run the side stream on this many CUs "
                          "and the learn stream on the rest (CU-masked HIP streams)")
     ap.add_argument("--cu-stride", action="store_true",
                     help="--cu-split picks every k-th CU instead of CUs 0..N-1")
@@ -255,6 +266,12 @@ def main():
 
     # all work on one dedicated stream: HIP events recorded on the legacy null
     # stream block the host and would inflate the timed region
+    if args.overlap == "auto":
+        small = (not args.shared and not args.no_fuse and not args.split_learn
+                 and args.rows * args.cols * args.envs <= AUTO_ENV_MAX_AGENTS)
+        args.overlap = "env" if small else "none"
+        if small and args.cu_split is None:
+            args.cu_split = AUTO_ENV_CU_SPLIT
     side = None
     if args.cu_split:
         from dmdqn_amd._lib import cu_masked_stream
@@ -402,22 +419,9 @@ def main():
                              "env": "the fused env step + replay draws of step t+1 beside learn t"
                              }[args.overlap]
                             + ("; act + sim + observe + store fused in one launch per env"
-                               if tr.fused else ""),
-            },
-            "roofline": {
-                "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared else
-                           "k_learn (fused gather + 3x fwd + bwd + Adam, MFMA)"),
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "traffic_stale": traffic_stale,
-                "bytes_per_launch": bpl,
-                "avg_launch_ms": round(avg_learn_s * 1e3, 4),
-                "learn_share_of_step": round(avg_learn_s / (el_max / args.steps), 3),
+                               if tr.fused else "")
+                            + (f"; side stream on {args.cu_split} CUs"
+                               + (" (strided)" if args.cu_stride else "") if args.cu_split else ""),
             },
             "cpu_baseline": cpu,
             # secondary figures SURVEY 8d asks for next to the headline roofline
@@ -428,17 +432,45 @@ def main():
             "sim_roofline": _sim_roofline(E, tr.env.cfg.step_duration, vbar, sim_ms,
                                           sim_traffic, sim_src, sim_stale,
                                           sim_state_fits_lds(args.rows, args.cols)),
-            "mfma": {
-                "kernel": ("k_shared_next + k_shared_grad" if args.shared else LEARN_KERNELS[args.precision]) +
-                          f" (Q-net forward/backward, {MFMA_OPS[args.precision]})",
-                "flop_per_launch": NA * LEARN_FLOP_PER_AGENT,
-                "achieved": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12, 2),
-                "peak": MFMA_PEAK_TFLOPS[args.precision],
-                "unit": "TFLOP/s",
-                "frac": round(NA * LEARN_FLOP_PER_AGENT / avg_learn_s / 1e12 /
-                              MFMA_PEAK_TFLOPS[args.precision], 4),
-            },
         }
+        timing = {"avg_launch_ms": round(avg_learn_s * 1e3, 4),
+                  "learn_share_of_step": round(avg_learn_s / (el_max / args.steps), 3)}
+        hbm_roof = {
+            "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared else
+                       "k_learn (fused gather + 3x fwd + bwd + Adam, MFMA)"),
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "traffic_stale": traffic_stale,
+            "bytes_per_launch": bpl,
+            **timing,
+        }
+        flop = NA * LEARN_FLOP_PER_AGENT
+        mfma_roof = {
+            "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared
+                       else LEARN_KERNELS[args.precision]) +
+                      f" (Q-net forward/backward, {MFMA_OPS[args.precision]})",
+            "bound": "mfma",
+            "flop_per_launch": flop,
+            "achieved": round(flop / avg_learn_s / 1e12, 2),
+            "peak": MFMA_PEAK_TFLOPS[args.precision],
+            "unit": "TFLOP/s",
+            "frac": round(flop / avg_learn_s / 1e12 / MFMA_PEAK_TFLOPS[args.precision], 4),
+        }
+        if args.shared:
+            # one net for NA batches: ~360 FLOP per algorithmic HBM byte, above
+            # the 2.5 PFLOP/s / 8 TB/s ridge (~310), so the shared learn is bound
+            # by the matrix cores and its HBM figure is the secondary one
+            out["roofline"] = {**mfma_roof, "traffic": traffic, "traffic_source": traffic_src,
+                               "traffic_stale": traffic_stale, **timing}
+            out["hbm"] = hbm_roof
+        else:
+            out["roofline"] = hbm_roof
+            out["mfma"] = mfma_roof
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
