@@ -574,14 +574,25 @@ __device__ __forceinline__ void xrows_issue(const dmdqn_learn_args &a, int agent
 
 __device__ __forceinline__ void xrows_commit(const XRows &x, h16 *X, int part) {
     const int row = part >> 1, c0 = 48 * (part & 1);
+    // int8 -> f16 exactly: byte b ^ 0x80 = x + 128 in the low byte of a half
+    // whose high byte is 0x64 is 1024 + x + 128; subtract 1152 (v_perm, one xor
+    // per 4 bytes, v_pk_add)
+    typedef h16 h2v __attribute__((ext_vector_type(2)));
+    const h2v bias = {(h16)-1152.0f, (h16)-1152.0f};
 #pragma unroll
-    for (int c = 0; c < 6; c++) {  // 6 chunks of 8 features
+    for (int c = 0; c < 6; c++) {
         half8 h;
-        const uint32_t w0 = (&x.v[c >> 1].x)[2 * (c & 1)], w1 = (&x.v[c >> 1].x)[2 * (c & 1) + 1];
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            h[e] = (h16)(float)(int8_t)(w0 >> (8 * e));
-            h[e + 4] = (h16)(float)(int8_t)(w1 >> (8 * e));
+        for (int q = 0; q < 2; q++) {
+            const uint32_t wv = (&x.v[c >> 1].x)[2 * (c & 1) + q] ^ 0x80808080u;
+            // bytes {b0, 0x64, b1, 0x64} and {b2, 0x64, b3, 0x64}
+            const uint32_t lo = __builtin_amdgcn_perm(0x64646464u, wv, 0x07010700u);
+            const uint32_t hi = __builtin_amdgcn_perm(0x64646464u, wv, 0x07030702u);
+            const h2v a0 = __builtin_bit_cast(h2v, lo) + bias, a1 = __builtin_bit_cast(h2v, hi) + bias;
+            h[4 * q + 0] = a0[0];
+            h[4 * q + 1] = a0[1];
+            h[4 * q + 2] = a1[0];
+            h[4 * q + 3] = a1[1];
         }
         *reinterpret_cast<half8 *>(X + hoff<DP>(row, c0 + 8 * c)) = h;
     }
@@ -608,10 +619,11 @@ __device__ __forceinline__ float pickf4(float q0, float q1, float q2, float q3, 
 
 __device__ __forceinline__ half4v relu4(f32x4 c, half4v b) {
     const half4v z = __builtin_convertvector(c, half4v) + b;
-    half4v r;
-#pragma unroll
-    for (int e = 0; e < 4; e++) r[e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
-    return r;
+    // z > 0 ? z : +0 as a signed 16-bit max with 0 (v_pk_max_i16): a set sign
+    // bit (negative, -0) is a negative integer; positive halves order as their
+    // bits.  Same result for every non-NaN z.
+    typedef short s4v __attribute__((ext_vector_type(4)));
+    return __builtin_bit_cast(half4v, __builtin_elementwise_max(__builtin_bit_cast(s4v, z), (s4v)(0)));
 }
 
 // NT neuron tiles per wave, NW = 8 / NT waves (NT = 2: one wave per SIMD,
@@ -976,12 +988,6 @@ __global__ void __launch_bounds__(64 * (8 / NT), 1) k_shared_grad3(dmdqn_learn_a
 //   G   dW3 (H2 own^T, DQ) ; dH1 own (dZ2 image) -> dZ1 own (over H2 own) ;
 //       dW2 (H1^T, dZ2 own) ; dW1 (X^T, dZ1 own)
 // Same rounding points as k_shared_grad3 (Keras' mixed policy).
-#ifndef SH_G4_ORDER
-#define SH_G4_ORDER 0  // 1: dH1 interleaved with dW2 (tools/build_exp.py A/B)
-#endif
-#ifndef SH_G4_RH
-#define SH_G4_RH 4
-#endif
 namespace g4 {
 using g3::X_BYTES;
 using g3::IMG;
@@ -1044,7 +1050,7 @@ __device__ __forceinline__ void load_slice4(const h16 *WH, int w, WSlice4 &S) {
 template <bool QSTATS>
 __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, const float *y_in,
                                                        const uint8_t *act_in, float *slab) {
-    constexpr int NTH = 512, RH = SH_G4_RH;  // row tiles per pass of L1 / L2 / dH1
+    constexpr int NTH = 512, RH = 4;  // row tiles per pass of L1 / L2 / dH1
     __shared__ __attribute__((aligned(16))) char smem[LDS];
     h16 *H1I = reinterpret_cast<h16 *>(smem + OFF_H1), *Z2I = reinterpret_cast<h16 *>(smem + OFF_Z2);
     h16 *H2I = reinterpret_cast<h16 *>(smem + OFF_H2), *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
@@ -1155,12 +1161,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
 #pragma unroll
         for (int s = 0; s < 4; s++)
             h2r[s] = *reinterpret_cast<const half8 *>(H2I + bR + 16 * H * wv + 256 * s);
-#if SH_G4_ORDER
-        // the W3 row of the row's action (dZ2 below), read with the H2 rows
-        half8 w3[4];
-#pragma unroll
-        for (int s = 0; s < 4; s++) w3[s] = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * s + 8 * g);
-#endif
         f32x4 cq = z4;
 #pragma unroll
         for (int s = 0; s < 4; s++)
@@ -1197,11 +1197,9 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         if (l == 0) sloss[w] = term;
         // dZ2 of the row for k = 32s + 8g + e: h16(dq W3[k][a]) where H2 > 0
         // (the W3 row of the action read first, then the stores)
-#if !SH_G4_ORDER
         half8 w3[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) w3[s] = *reinterpret_cast<const half8 *>(W3I + avl * H + 32 * s + 8 * g);
-#endif
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             half8 o;
@@ -1229,56 +1227,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             if (w == 0) GB3 = mfma(ones, dqf, GB3);
         }
         SH_STAMP(agent, 4, threadIdx.x);
-#if SH_G4_ORDER
-        // ---- dH1 (own j, all rows) interleaved with dW2[j][k own] / db2 (K =
-        // rows): both read only the dZ2 and H1 images, so their MFMAs fill each
-        // other's LDS latency; then dZ1 own -> image (over this wave's H2
-        // columns), then dW1[f][j own] / db1 from it.  Same sums in the same
-        // order as the sequential form below: bit-identical.
-        {
-            f32x4 c[8];
-#pragma unroll
-            for (int r = 0; r < 8; r++) c[r] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                const half8 bq = frag_tr_p(Z2I + trO + 2 * 16 * H * s);
-                GB2 = mfma(ones, bq, GB2);
-#pragma unroll
-                for (int hf = 0; hf < 2; hf++) {
-                    half8 zb[4];
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        zb[r] = *reinterpret_cast<const half8 *>(Z2I + bR + 16 * H * (4 * hf + r) + 256 * s);
-#pragma unroll
-                    for (int jj = 0; jj < 4; jj++) {
-                        const int jt = 4 * hf + jj;
-                        G2[jt] = mfma(frag_tr_p(H1I + trH[jt & 1] + 256 * (jt >> 1) + 2 * 16 * H * s), bq, G2[jt]);
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; r++) c[4 * hf + r] = mfma(W.w2b[s], zb[r], c[4 * hf + r]);
-                }
-            }
-            SH_STAMP(agent, 5, threadIdx.x);
-            half4v hv[8];
-#pragma unroll
-            for (int rt = 0; rt < 8; rt++) hv[rt] = *reinterpret_cast<const half4v *>(H1I + bW + 16 * H * rt);
-#pragma unroll
-            for (int rt = 0; rt < 8; rt++) {
-                half4v o;
-#pragma unroll
-                for (int e = 0; e < 4; e++) o[e] = hv[rt][e] > (h16)0.0f ? (h16)c[rt][e] : (h16)0.0f;
-                *reinterpret_cast<half4v *>(H2I + bW + 16 * H * rt) = o;
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const half8 bv = frag_tr_p(H2I + trO + 2 * 16 * H * s);
-            GB1 = mfma(ones, bv, GB1);
-#pragma unroll
-            for (int ft = 0; ft < 6; ft++)
-                G1[ft] = mfma(frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s), bv, G1[ft]);
-        }
-#else
         // ---- dH1 (own j) -> dZ1 own -> image (over this wave's H2 columns)
 #pragma unroll
         for (int hf = 0; hf < 8 / RH; hf++) {
@@ -1319,7 +1267,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             for (int ft = 0; ft < 6; ft++)
                 G1[ft] = mfma(frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s), bv, G1[ft]);
         }
-#endif
         yv = yn;
         avl = an;
         SH_STAMP(agent, 6, threadIdx.x);
