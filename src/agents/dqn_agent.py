@@ -15,6 +15,8 @@ Each DQNAgent is one agent slot run by the fused kernels (act, replay store,
 replay sample, learn).  For many agents / many env replicas use
 dmdqn_amd.agent.BatchedDQN, which runs all of them in one launch per stage.
 """
+import json
+import os
 import zlib
 
 import numpy as np
@@ -118,6 +120,16 @@ class DQNAgent:
         self.replay_buffer.device, self.replay_buffer.ring = self.device, self._core.ring
         self.global_step_count = 0
         self.learn_step_counter = 0
+        # the per-learn scalars the reference writes with tf.summary to
+        # logs/<agent_id> (:151, :361-370): kept as last_summary; with the
+        # additive config key "summary_dir", also appended as JSON lines to
+        # <summary_dir>/<agent_id>/summaries.jsonl (no TensorBoard here)
+        self.last_summary = None
+        self._summary_path = None
+        if config.get("summary_dir"):
+            d = os.path.join(config["summary_dir"], str(agent_id))
+            os.makedirs(d, exist_ok=True)
+            self._summary_path = os.path.join(d, "summaries.jsonl")
 
     def select_action(self, state_tensor):
         """epsilon-greedy on the global numpy stream (:246-274)."""
@@ -137,11 +149,19 @@ class DQNAgent:
 
     def learn(self):
         """One fused learn step; None while the buffer is underfilled (:333-335)."""
-        loss = self._core.learn()
+        loss = self._core.learn(collect_stats=True)
         if loss is None:
             return None
         self.learn_step_counter = self._core.learn_step_counter
-        return float(loss[0].item())
+        m = self._core.learn_metrics()
+        self.last_summary = {"step": self.learn_step_counter, "loss": float(loss[0].item()),
+                             "epsilon": float(self.epsilon),
+                             "q_values_mean": m["q_values_mean"], "q_values_std": m["q_values_std"],
+                             "action_distribution": m["action_distribution"]}
+        if self._summary_path:
+            with open(self._summary_path, "a") as f:
+                f.write(json.dumps(self.last_summary) + "\n")
+        return self.last_summary["loss"]
 
     def replay(self) -> float:
         loss = self.learn()

@@ -89,3 +89,36 @@ def test_train_batched_metrics_and_save(tmp_path):
     assert all(r["global_reward"] <= 0 for r in recs)
     assert (sdir / "checkpoint.pt").exists() and (sdir / "agent_J_1_1.weights.npz").exists()
     assert tr.episode == 1
+
+
+def test_dropin_learn_writes_the_reference_summaries(tmp_path):
+    """DQNAgent.learn records the scalars the reference logs per learn
+    (dqn_agent.py:361-370: loss, epsilon, Q mean / std of the batch's online Q
+    values, the sampled action histogram), in last_summary and, with
+    "summary_dir", as JSON lines under <dir>/<agent_id>/; the Q moments match
+    the host forward of the pre-learn weights on the sampled rows."""
+    import json
+    from src.agents import dqn_agent
+    dqn_agent.seed(7)
+    cfg = {"nn_layers": [128, 128], "batch_size": 128, "replay_buffer_size": 300,
+           "summary_dir": str(tmp_path)}
+    ag = dqn_agent.DQNAgent(89, 4, "J1", cfg)
+    rs = np.random.RandomState(5)
+    for _ in range(140):
+        s, n = rs.randint(-1, 20, 89).astype(np.float32), rs.randint(-1, 20, 89).astype(np.float32)
+        ag.remember(s, int(rs.randint(4)), float(-rs.rand() * 50), n, False)
+    assert ag.learn() is not None
+    p0 = ag._core.keras_params("params").copy()
+    loss = ag.learn()
+    rec = ag.last_summary
+    assert rec["step"] == 2 and rec["loss"] == loss and rec["epsilon"] == ag.epsilon
+    idx = ag._core.idx.cpu().numpy()[0]
+    slots = ag.replay_buffer.ring.slots_of(idx)
+    S = ag.replay_buffer.ring.s[0, slots, :89].cpu().numpy()
+    A = ag.replay_buffer.ring.a[0, slots].cpu().numpy()
+    assert rec["action_distribution"] == np.bincount(A, minlength=4).tolist()
+    q = O.qnet_forward(p0[0], S)
+    np.testing.assert_allclose(rec["q_values_mean"], q.mean(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(rec["q_values_std"], q.std(), rtol=1e-3)
+    lines = (tmp_path / "J1" / "summaries.jsonl").read_text().strip().splitlines()
+    assert [json.loads(x)["step"] for x in lines] == [1, 2]

@@ -251,7 +251,7 @@ def test_c2_steady_state_wrapped_rings():
 def test_c5_steady_state_wrapped_rings():
     """C5 (8x8 x 256, ONE shared fp16 network, replay 10,000), the regime
     bench.py's C5 line times: past 10,000 steps, wrapped rings (start != 0,
-    the wrap arithmetic of k_shared_next / k_shared_grad3) and the set-branch
+    the wrap arithmetic of k_shared_next / k_shared_grad4) and the set-branch
     sampler.  Sampled replicas vs OracleLoop as C2 / C3; at learns 3 and 5
     after the wrap the device z-score bit-exact and 8 agents' losses vs
     oracle.learn_mixed; at both, Adam exact on the all-agent gradient and the
