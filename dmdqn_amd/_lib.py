@@ -148,7 +148,7 @@ def stream_of(device=None):
 
 def cu_masked_stream(cus, device=None):
     """A torch ExternalStream whose kernels run only on the CU indices `cus`
-    (dmdqn_stream_create_cumask).  The stream lives for the process."""
+    (dmdqn_stream_create_cumask).  The stream lives until interpreter exit."""
     import torch
     cus = sorted(set(int(c) for c in cus))
     if not cus or cus[0] < 0:
@@ -159,4 +159,24 @@ def cu_masked_stream(cus, device=None):
         mask[c // 32] |= 1 << (c % 32)
     out = C.c_void_p()
     call("dmdqn_stream_create_cumask", words, mask, C.byref(out))
+    if not _CU_STREAMS:
+        import atexit
+        atexit.register(_destroy_cu_streams)
+    _CU_STREAMS.append(out.value)
     return torch.cuda.ExternalStream(out.value, device=device)
+
+
+_CU_STREAMS = []
+
+
+def _destroy_cu_streams():
+    """Destroy the CU-masked streams at interpreter exit, after their work,
+    before the HIP runtime's own teardown (left to it, the teardown crashed
+    under rocprofv3 once the tool had finalized)."""
+    import torch
+    try:
+        torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001 -- exiting anyway; still release the streams
+        pass
+    while _CU_STREAMS:
+        load().dmdqn_stream_destroy(C.c_void_p(_CU_STREAMS.pop()))

@@ -31,14 +31,14 @@ for CFG in "$@"; do
         -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline $ARGS > $O/bench_prof.json 2> $O/bench_prof.err
     echo "$CFG stats done"
     timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcF -o run \
-        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline $ARGS > $O/pmcF.log 2>&1
+        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline --overlap none $ARGS > $O/pmcF.log 2>&1
     echo "$CFG fetch done"
     timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcW -o run \
-        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline $ARGS > $O/pmcW.log 2>&1
+        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline --overlap none $ARGS > $O/pmcW.log 2>&1
     echo "$CFG write done"
     timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES \
         --output-format csv -d $O/pmcM -o run \
-        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline $ARGS > $O/pmcM.log 2>&1
+        -- python3 $R/bench.py --steps 4 --warmup 1 --prefill-steps 1100 --no-cpu-baseline --overlap none $ARGS > $O/pmcM.log 2>&1
     echo "$CFG mfma done"
     F=$(find $O/pmcF -name '*counter_collection.csv' | head -n 1)
     W=$(find $O/pmcW -name '*counter_collection.csv' | head -n 1)
