@@ -237,6 +237,9 @@ def main():
                          "and the learn stream on the rest (CU-masked HIP streams)")
     ap.add_argument("--cu-stride", action="store_true",
                     help="--cu-split picks every k-th CU instead of CUs 0..N-1")
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="bracket every k-th learn launch of the timed region with timing "
+                         "events (the roofline's average launch duration; 1 = every launch)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="act / sim / observe / store as four launches instead of the fused "
                          "env step (dmdqn_env_step; bit-identical, A/B)")
@@ -299,17 +302,28 @@ def main():
         tr.step()
     assert tr.agent.learn_launches > 0 or args.warmup == 0
 
-    # HIP events bracketing each learn launch, on the stream it runs on.
-    # Created (and recorded once) before the timed region: a torch Event
-    # creates its HIP event lazily at the first record.
-    pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+    # HIP events bracketing each learn launch, on the stream it runs on:
+    # timing events without the system-scope fence (_lib.TimingEvent) -- a
+    # default timing event's record writes caches back between the kernels
+    # and cost C2's two-stream step ~11 us per learn (tools/hook_cost.py).
+    # Created and recorded once before the timed region.
+    from dmdqn_amd._lib import TimingEvent
+    pool = [TimingEvent() for _ in range(2 * args.steps)]
     for ev in pool:
         ev.record(work)
     torch.cuda.synchronize(dev)
     pool_it = iter(pool)
     starts, ends = [], []
 
+    seen = [0]
+
     def hook(before):
+        # every args.time_every-th learn: each pair of records still costs the
+        # step a few us (two marker packets between dependent kernels)
+        if before:
+            seen[0] += 1
+        if (seen[0] - 1) % args.time_every:
+            return
         ev = next(pool_it)
         ev.record(torch.cuda.current_stream(dev))
         (starts if before else ends).append(ev)
@@ -434,6 +448,7 @@ def main():
                                           sim_state_fits_lds(args.rows, args.cols)),
         }
         timing = {"avg_launch_ms": round(avg_learn_s * 1e3, 4),
+                  "timed_launches": len(learn_ms),
                   "learn_share_of_step": round(avg_learn_s / (el_max / args.steps), 3)}
         hbm_roof = {
             "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared else

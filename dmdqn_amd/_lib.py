@@ -35,6 +35,11 @@ SIGNATURES = {
     "dmdqn_stream_destroy": [vp],
     "dmdqn_set_option": [i32, i32],
     "dmdqn_get_option": [i32],
+    "dmdqn_timing_event_create": [vp],
+    "dmdqn_event_record": [vp, vp],
+    "dmdqn_event_synchronize": [vp],
+    "dmdqn_event_elapsed_ms": [vp, vp, vp],
+    "dmdqn_event_destroy": [vp],
 }
 
 
@@ -180,3 +185,36 @@ def _destroy_cu_streams():
         pass
     while _CU_STREAMS:
         load().dmdqn_stream_destroy(C.c_void_p(_CU_STREAMS.pop()))
+
+
+class TimingEvent:
+    """A HIP timing event without the system-scope fence
+    (dmdqn_timing_event_create): recording it between two kernels costs no
+    cache write-back.  For timing only (bench.py's per-learn events), never
+    for ordering streams."""
+
+    def __init__(self):
+        out = C.c_void_p()
+        call("dmdqn_timing_event_create", C.byref(out))
+        self._ev = out.value
+        self._lib = load()
+
+    def record(self, stream):
+        call("dmdqn_event_record", C.c_void_p(self._ev), C.c_void_p(stream.cuda_stream))
+
+    def synchronize(self):
+        call("dmdqn_event_synchronize", C.c_void_p(self._ev))
+
+    def elapsed_time(self, end):
+        """ms from this event's record to end's (both complete)."""
+        ms = C.c_float()
+        call("dmdqn_event_elapsed_ms", C.c_void_p(self._ev), C.c_void_p(end._ev), C.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        ev, self._ev = getattr(self, "_ev", None), None
+        if ev:
+            try:
+                self._lib.dmdqn_event_destroy(C.c_void_p(ev))
+            except Exception:  # noqa: BLE001 -- interpreter shutdown
+                pass

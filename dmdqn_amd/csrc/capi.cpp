@@ -97,3 +97,44 @@ extern "C" int dmdqn_stream_destroy(void *stream) {
     DMDQN_REQUIRE(e == hipSuccess, "hipStreamDestroy: %s", hipGetErrorString(e));
     return DMDQN_OK;
 }
+
+// Timing events without the system-scope fence (include/dmdqn.h): bench.py
+// brackets every learn launch with two of them.
+extern "C" int dmdqn_timing_event_create(void **out) {
+    DMDQN_REQUIRE(out, "dmdqn_timing_event_create: null out");
+    hipEvent_t ev = nullptr;
+    const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableSystemFence);
+    DMDQN_REQUIRE(e == hipSuccess, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
+    *out = ev;
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_event_record(void *event, void *stream) {
+    DMDQN_REQUIRE(event, "dmdqn_event_record: null event");
+    const hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(event),
+                                        reinterpret_cast<hipStream_t>(stream));
+    DMDQN_REQUIRE(e == hipSuccess, "hipEventRecord: %s", hipGetErrorString(e));
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_event_synchronize(void *event) {
+    DMDQN_REQUIRE(event, "dmdqn_event_synchronize: null event");
+    const hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(event));
+    DMDQN_REQUIRE(e == hipSuccess, "hipEventSynchronize: %s", hipGetErrorString(e));
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_event_elapsed_ms(void *start, void *end, float *ms) {
+    DMDQN_REQUIRE(start && end && ms, "dmdqn_event_elapsed_ms: null argument");
+    const hipError_t e = hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(start),
+                                             reinterpret_cast<hipEvent_t>(end));
+    DMDQN_REQUIRE(e == hipSuccess, "hipEventElapsedTime: %s", hipGetErrorString(e));
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_event_destroy(void *event) {
+    DMDQN_REQUIRE(event, "dmdqn_event_destroy: null event");
+    const hipError_t e = hipEventDestroy(reinterpret_cast<hipEvent_t>(event));
+    DMDQN_REQUIRE(e == hipSuccess, "hipEventDestroy: %s", hipGetErrorString(e));
+    return DMDQN_OK;
+}

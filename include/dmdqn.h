@@ -90,6 +90,19 @@ int dmdqn_get_option(int option);
 int dmdqn_stream_create_cumask(uint32_t n_words, const uint32_t *mask, void **stream);
 int dmdqn_stream_destroy(void *stream);
 
+/* Timing events for bench.py's per-launch kernel timing: a HIP event (in
+ * *event, hipEvent_t) created with hipEventDisableSystemFence, so recording it
+ * between two kernels adds no cache write-back / invalidate (a default timing
+ * event's system-scope release cost C2's step ~11 us per learn).  Only for
+ * timing: not for ordering streams or for host visibility.  elapsed: the time
+ * between two recorded events in ms (both complete: synchronize first).  No
+ * reference counterpart. */
+int dmdqn_timing_event_create(void **event);
+int dmdqn_event_record(void *event, void *stream);
+int dmdqn_event_synchronize(void *event);
+int dmdqn_event_elapsed_ms(void *start, void *end, float *ms);
+int dmdqn_event_destroy(void *event);
+
 /* ------------------------------------------------------------------ streams
  * Seed E MT19937 streams on the device.
  *  _np: numpy legacy RandomState.seed(int) (init_genrand); replaces the global

@@ -44,7 +44,8 @@ def test_python_bindings_cover_header(lib):
     declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version", "dmdqn_debug_status",
                                    "dmdqn_debug_build", "dmdqn_learn_shared_work_bytes"}
     host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy", "dmdqn_set_option",
-                 "dmdqn_get_option"}
+                 "dmdqn_get_option", "dmdqn_timing_event_create", "dmdqn_event_record",
+                 "dmdqn_event_synchronize", "dmdqn_event_elapsed_ms", "dmdqn_event_destroy"}
     assert declared - host_only <= set(ops.ENTRY_POINTS), sorted(declared - host_only -
                                                                  set(ops.ENTRY_POINTS))
     ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_reset_envs", "dmdqn_sim_step",
