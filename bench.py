@@ -240,6 +240,9 @@ def main():
     ap.add_argument("--time-every", type=int, default=4,
                     help="bracket every k-th learn launch of the timed region with timing "
                          "events (the roofline's average launch duration; 1 = every launch)")
+    ap.add_argument("--fenced-events", action="store_true",
+                    help="overlap env: order the side stream after the learns with default "
+                         "(system-scope) events instead of ordering-only ones (A/B)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="act / sim / observe / store as four launches instead of the fused "
                          "env step (dmdqn_env_step; bit-identical, A/B)")
@@ -292,7 +295,8 @@ def main():
     agent_cfg = AgentConfig(precision=args.precision, seed=1000 if args.shared else 1000 + rank,
                             shared_params=args.shared)
     tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side,
-                 split_learn=args.split_learn, fused=not args.no_fuse)
+                 split_learn=args.split_learn, fused=not args.no_fuse,
+                 war_events=not args.fenced_events)
     E, A = tr.env.E, tr.env.A
     NA = E * A
     prefill = agent_cfg.replay_buffer_size if args.prefill_steps is None else args.prefill_steps

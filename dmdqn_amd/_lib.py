@@ -36,6 +36,8 @@ SIGNATURES = {
     "dmdqn_set_option": [i32, i32],
     "dmdqn_get_option": [i32],
     "dmdqn_timing_event_create": [vp],
+    "dmdqn_order_event_create": [vp],
+    "dmdqn_stream_wait_event": [vp, vp],
     "dmdqn_event_record": [vp, vp],
     "dmdqn_event_synchronize": [vp],
     "dmdqn_event_elapsed_ms": [vp, vp, vp],
@@ -210,6 +212,39 @@ class TimingEvent:
         ms = C.c_float()
         call("dmdqn_event_elapsed_ms", C.c_void_p(self._ev), C.c_void_p(end._ev), C.byref(ms))
         return ms.value
+
+    def __del__(self):
+        ev, self._ev = getattr(self, "_ev", None), None
+        if ev:
+            try:
+                self._lib.dmdqn_event_destroy(C.c_void_p(ev))
+            except Exception:  # noqa: BLE001 -- interpreter shutdown
+                pass
+
+
+class OrderEvent:
+    """An ordering-only HIP event (dmdqn_order_event_create): a stream that
+    waits on it starts after the recorded work completed, without that work's
+    writes being released to it -- write-after-read ordering only (the
+    trainer's side stream may overwrite ring slots once a learn has read
+    them), never a data hand-over.  Recording it between dependent kernels
+    costs no cache write-back."""
+
+    def __init__(self):
+        out = C.c_void_p()
+        call("dmdqn_order_event_create", C.byref(out))
+        self._ev = out.value
+        self._lib = load()
+
+    def record(self, stream):
+        call("dmdqn_event_record", C.c_void_p(self._ev), C.c_void_p(stream.cuda_stream))
+
+    def wait(self, stream):
+        """Make `stream` wait for the last record."""
+        call("dmdqn_stream_wait_event", C.c_void_p(stream.cuda_stream), C.c_void_p(self._ev))
+
+    def synchronize(self):
+        call("dmdqn_event_synchronize", C.c_void_p(self._ev))
 
     def __del__(self):
         ev, self._ev = getattr(self, "_ev", None), None

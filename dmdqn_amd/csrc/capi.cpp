@@ -109,6 +109,24 @@ extern "C" int dmdqn_timing_event_create(void **out) {
     return DMDQN_OK;
 }
 
+extern "C" int dmdqn_order_event_create(void **out) {
+    DMDQN_REQUIRE(out, "dmdqn_order_event_create: null out");
+    hipEvent_t ev = nullptr;
+    const hipError_t e =
+        hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence);
+    DMDQN_REQUIRE(e == hipSuccess, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
+    *out = ev;
+    return DMDQN_OK;
+}
+
+extern "C" int dmdqn_stream_wait_event(void *stream, void *event) {
+    DMDQN_REQUIRE(event, "dmdqn_stream_wait_event: null event");
+    const hipError_t e = hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream),
+                                            reinterpret_cast<hipEvent_t>(event), 0);
+    DMDQN_REQUIRE(e == hipSuccess, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+    return DMDQN_OK;
+}
+
 extern "C" int dmdqn_event_record(void *event, void *stream) {
     DMDQN_REQUIRE(event, "dmdqn_event_record: null event");
     const hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(event),

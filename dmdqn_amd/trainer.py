@@ -71,7 +71,8 @@ class StepStats:
 
 class Trainer:
     def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
-                 overlap="none", side_stream=None, split_learn=False, fused=True):
+                 overlap="none", side_stream=None, split_learn=False, fused=True,
+                 war_events=True):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
         if overlap is True or overlap is False:
             overlap = "full" if overlap else "none"
@@ -100,6 +101,13 @@ class Trainer:
         if overlap == "env" and not self.fused:
             raise ValueError('overlap "env" runs the fused env step (int8 replay rows, fused=True)')
         self._ev_learn_prev = None  # overlap "env": the learn before the last one
+        # overlap "env" at a fixed epsilon of 1 (A-1: the side stream never reads
+        # a learn's output): the learn -> side-stream wait only orders the store
+        # of t+2 after learn t's ring reads, so it uses ordering-only events
+        # (_lib.OrderEvent, no cache write-back between the learns) from a ring
+        self._war_ring = ([_lib.OrderEvent() for _ in range(4)]
+                          if war_events and overlap == "env" else None)
+        self._war_i = 0
         self.obs = self.env.reset()
         self.episode = 0
         self.step_count = 0
@@ -206,9 +214,14 @@ class Trainer:
             self._join = False
         if self._ev_learn_prev is not None:
             # this store's slot is in the window of the learn two steps back
-            side.wait_event(self._ev_learn_prev)
+            if isinstance(self._ev_learn_prev, _lib.OrderEvent):
+                self._ev_learn_prev.wait(side)
+            else:
+                side.wait_event(self._ev_learn_prev)
         if agent.current_epsilon() < 1.0 and self._ev_learn is not None:
-            side.wait_event(self._ev_learn)  # greedy act reads the updated weights
+            # greedy act reads the updated weights (recorded as a full event:
+            # an ordering-only one is used only while epsilon is fixed at 1)
+            side.wait_event(self._ev_learn)
         with torch.cuda.stream(side):
             next_obs, reward, done, info = self._env_side()
             agent.presample(len(agent.ring))
@@ -218,8 +231,17 @@ class Trainer:
         main.wait_event(ev_env)  # the store learn t reads; what the caller reads after step()
         loss = agent.learn(collect_stats=collect_stats)
         self._ev_learn_prev = self._ev_learn
-        self._ev_learn = torch.cuda.Event()
-        self._ev_learn.record(main)
+        if (self._war_ring is not None and not agent.cfg.count_env_steps
+                and agent.current_epsilon() >= 1.0):
+            # epsilon cannot fall below 1 later (count_env_steps off): no act
+            # will read this learn's weights through the side stream
+            ev = self._war_ring[self._war_i]
+            self._war_i = (self._war_i + 1) % len(self._war_ring)
+            ev.record(main)
+            self._ev_learn = ev
+        else:
+            self._ev_learn = torch.cuda.Event()
+            self._ev_learn.record(main)
         self.last_loss, self.last_reward = loss, reward
         return StepStats(loss is not None, done)
 

@@ -98,6 +98,13 @@ int dmdqn_stream_destroy(void *stream);
  * between two recorded events in ms (both complete: synchronize first).  No
  * reference counterpart. */
 int dmdqn_timing_event_create(void **event);
+/* An ordering-only event (no timing, hipEventDisableSystemFence): a stream
+ * waiting on it (dmdqn_stream_wait_event) starts after the work recorded
+ * before it has COMPLETED, with no release of that work's writes -- for
+ * write-after-read ordering (the trainer's env step of t+2 may overwrite ring
+ * slots only after learn t has read them), never for handing data over. */
+int dmdqn_order_event_create(void **event);
+int dmdqn_stream_wait_event(void *stream, void *event);
 int dmdqn_event_record(void *event, void *stream);
 int dmdqn_event_synchronize(void *event);
 int dmdqn_event_elapsed_ms(void *start, void *end, float *ms);
