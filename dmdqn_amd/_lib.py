@@ -11,8 +11,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DMDQN_VARIANT=debug loads the debug-bounds build (libdmdqn_hip_debug.so and
 # its operator library): kernels check the indices they derive (common.hpp)
 VARIANT = os.environ.get("DMDQN_VARIANT", "")
-if VARIANT not in ("", "debug", "prof"):
-    raise ValueError(f"DMDQN_VARIANT must be '', 'debug' or 'prof', got {VARIANT!r}")
+if VARIANT not in ("", "debug", "prof", "exp"):
+    raise ValueError(f"DMDQN_VARIANT must be '', 'debug', 'prof' or 'exp', got {VARIANT!r}")
 _SUFFIX = f"_{VARIANT}" if VARIANT else ""
 LIB_PATH = os.path.join(_HERE, "lib", f"libdmdqn_hip{_SUFFIX}.so")
 _LIB = None

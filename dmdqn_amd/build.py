@@ -15,7 +15,10 @@ LIBDIR = os.path.join(HERE, "lib")
 # variants: "" (the product build) and "debug" (-DDMDQN_DEBUG_BOUNDS: kernels
 # check and clamp the indices they derive, dmdqn_debug_status reports them)
 # ("prof": the sim's per-pass timers, tools/sim_profile.py; built on demand)
-VARIANT_FLAGS = {"": [], "debug": ["-DDMDQN_DEBUG_BOUNDS"], "prof": ["-DDMDQN_SIM_PROFILE"]}
+# ("exp": an A/B build whose only flags are DMDQN_EXTRA_FLAGS; loaded with
+# DMDQN_VARIANT=exp through the torch operators like the product library)
+VARIANT_FLAGS = {"": [], "debug": ["-DDMDQN_DEBUG_BOUNDS"], "prof": ["-DDMDQN_SIM_PROFILE"],
+                 "exp": []}
 
 
 def _suffix(variant):

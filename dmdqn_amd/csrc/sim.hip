@@ -158,6 +158,12 @@ __device__ __forceinline__ QNext next_vehicle(const View &V, int p) {
     return QNext{(int)V.q_ids[p], (int)V.q_dst[p]};
 }
 
+#ifndef SIM_LANE_STRIDE_NT
+#define SIM_LANE_STRIDE_NT 1  // 0: the lane arrays NL apart, as before round 4 (A/B)
+#endif
+#ifndef SIM_VPREF
+#define SIM_VPREF 0  // 1: pass C reads the next follower's speed one vehicle ahead (A/B)
+#endif
 #ifdef DMDQN_SIM_PROFILE  // diagnostic build: per-pass ticks of thread 0 -> halt[env][0][0..7]
 #define SIM_PROF(i)                                                          \
     do {                                                                     \
@@ -1064,17 +1070,21 @@ __device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP]
     lv = vv;
 }
 
-__host__ __device__ inline size_t sim_reg_lds_bytes(int R, int C) {
-    const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
-    return (size_t)NL * 9 * 4 + (size_t)A * 8 + (size_t)A * 48 + 16 + topo_bytes(R, C);
+// The nine per-lane arrays are `ls` entries apart (ls = the block's thread
+// count, a compile-time constant in the kernel): every lane array is then the
+// thread's one LDS address plus an immediate offset, instead of a VGPR per
+// array held across the substep loop (the 1024-thread kernel spilled them).
+__host__ __device__ inline size_t sim_reg_lds_bytes(int R, int C, int ls) {
+    const int A = R * C;
+    return (size_t)ls * 9 * 4 + (size_t)A * 8 + (size_t)A * 48 + 16 + topo_bytes(R, C);
 }
 
 // Offset of the speed columns (1024-thread blocks) past the block's own LDS
 // (and the fused step's MT stream / epilogue scratch).
-__host__ __device__ inline size_t reg_vcol_off(int R, int C, bool fused) {
-    const int A = R * C, NL = 3 * (4 * A + 2 * R + 2 * C);
-    size_t b = sim_reg_lds_bytes(R, C);
-    if (fused) b = fuse_layout(b, 0, (size_t)NL * 9 * 4, A).bytes;
+__host__ __device__ inline size_t reg_vcol_off(int R, int C, bool fused, int ls) {
+    const int A = R * C;
+    size_t b = sim_reg_lds_bytes(R, C, ls);
+    if (fused) b = fuse_layout(b, 0, (size_t)ls * 9 * 4, A).bytes;
     return (b + 15) & ~(size_t)15;
 }
 
@@ -1084,18 +1094,24 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                int max_time, int32_t *halt, int32_t *phase_out, int32_t *tspent, uint8_t *done,
                dmdqn_env_fuse F) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
+#ifdef DMDQN_SIM_PROFILE
+    const uint64_t prof_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int t0 = S.t_env ? S.t_env[blockIdx.x] : t0_arg;  // the replica's own clock
     const IdmK P(Pa);
     EnvView G(S, blockIdx.x);
     const int A = G.A, NL = G.NL, cap = G.cap;
     const int tid = threadIdx.x;
     // ---- LDS: published per-lane values, signals, detector times, stats, topology
+    // lane arrays LS entries apart (sim_reg_lds_bytes)
+    constexpr int LS_ = SIM_LANE_STRIDE_NT ? NT : 0;
+    const int LS = LS_ ? LS_ : NL;
     int32_t *s_cnt = reinterpret_cast<int32_t *>(dyn);
-    float *s_lx = reinterpret_cast<float *>(s_cnt + NL), *s_lv = s_lx + NL;
-    int32_t *s_req = reinterpret_cast<int32_t *>(s_lv + NL), *s_gfrom = s_req + NL;
-    float *s_fx = reinterpret_cast<float *>(s_gfrom + NL), *s_fv = s_fx + NL;
-    int32_t *s_mdst = reinterpret_cast<int32_t *>(s_fv + NL), *s_ins = s_mdst + NL;
-    int32_t *s_phase = s_ins + NL, *s_ts = s_phase + A, *s_ldet = s_ts + A;
+    float *s_lx = reinterpret_cast<float *>(s_cnt + LS), *s_lv = s_lx + LS;
+    int32_t *s_req = reinterpret_cast<int32_t *>(s_lv + LS), *s_gfrom = s_req + LS;
+    float *s_fx = reinterpret_cast<float *>(s_gfrom + LS), *s_fv = s_fx + LS;
+    int32_t *s_mdst = reinterpret_cast<int32_t *>(s_fv + LS), *s_ins = s_mdst + LS;
+    int32_t *s_phase = s_ins + LS, *s_ts = s_phase + A, *s_ldet = s_ts + A;
     int32_t *s_stats = s_ldet + 12 * A;  // inserted, arrived, running, pending
     const Topo T = build_topo(s_stats + 4, S.R, S.C, S.exit_id, S.exit_ao, P.len_inner,
                               P.len_outer);  // synced below
@@ -1106,7 +1122,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     constexpr bool kL = NT > 512;  // speeds in the LDS column (VColL)
     float X_[RCAP], V_[RCAP];
     VColL Vc{nullptr, 0, NT};
-    if constexpr (kL) Vc.p = reinterpret_cast<float *>(dyn + reg_vcol_off(S.R, S.C, kFuse)) + tid;
+    if constexpr (kL) Vc.p = reinterpret_cast<float *>(dyn + reg_vcol_off(S.R, S.C, kFuse, LS)) + tid;
     int D_[RCAP];
     int n = 0;
     float lx = 0.0f, lv = 0.0f;
@@ -1149,7 +1165,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     // fused step: the MT stream past the block's own LDS; the halting counts
     // later in the topology tables' place, the epilogue's scratch in the
     // published-lane arrays (both dead by then)
-    const FuseLayout fl = fuse_layout(sim_reg_lds_bytes(S.R, S.C), 0, (size_t)NL * 9 * 4, A);
+    const FuseLayout fl = fuse_layout(sim_reg_lds_bytes(S.R, S.C, LS), 0, (size_t)LS * 9 * 4, A);
     int32_t *const s_halt = s_stats + 4;
     int my_act = 0;
     bool act_fast = false;
@@ -1217,6 +1233,10 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
 
     tl_pass(t0);
     __syncthreads();
+#ifdef DMDQN_SIM_PROFILE
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memrealtime();
+    prof[6] = prof_t - prof_t0;  // staging
+#endif
     for (int k = 0; k < K; k++) {
         const int t = t0 + k;
         TAKE_INSERT();
@@ -1269,6 +1289,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         }
         if (own) s_req[l] = rq;
         __syncthreads();
+        SIM_PROF(1);
 
         // ---- B: this lane, as a target, grants one request if it has room
         if (own) {
@@ -1297,6 +1318,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             s_gfrom[l] = g;
         }
         __syncthreads();
+        SIM_PROF(2);
 
         // ---- C: advance this lane front to back; the front leaves or arrives
         {
@@ -1325,9 +1347,19 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 bool det = lead_x_new >= dp && lead_x_old0 < dpl;
                 float lead_x_old = lead_x_old0, lead_v_old = lead_v_old0;
                 float last_x = X_[0], last_v = vget<kL>(V_, Vc, 0);
+#if SIM_VPREF
+                // (LDS speed column) the next follower's speed is read one
+                // vehicle ahead, so its LDS latency overlaps this one's IDM
+                float v_nx = nm > 1 ? vget<kL>(V_, Vc, 1) : 0.0f;
+#endif
                 for (int i = 1; i < nm; i++) {
                     if (i < n) {
+#if SIM_VPREF
+                        const float xi = X_[i], vi = kL ? v_nx : vget<kL>(V_, Vc, i);
+                        if (kL && i + 1 < nm) v_nx = vget<kL>(V_, Vc, i + 1);
+#else
                         const float xi = X_[i], vi = vget<kL>(V_, Vc, i);
+#endif
                         const float gap = (lead_x_old - P.length) - xi;
                         const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
                         float vn = clamp_speed(vi + acc, P);
@@ -1370,6 +1402,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             }
         }
         __syncthreads();
+        SIM_PROF(3);
 
         // ---- D: this lane appends the vehicle it granted
         if (own) {
@@ -1392,6 +1425,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             }
         }
         __syncthreads();
+        SIM_PROF(4);
 
         // ---- E: each origin queue inserts its next departed vehicle if there is
         // room (the lane's owner takes it into its registers at the next pass);
@@ -1417,6 +1451,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         }
         if (k + 1 < K) tl_pass(t + 1);
         __syncthreads();
+        SIM_PROF(5);  // E + the signals (pass "TL" stays 0 here)
     }
     TAKE_INSERT();
 #undef TAKE_INSERT
@@ -1475,6 +1510,13 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         fused_tail<!kL>(F, S.R, S.C, t, done_e, act_back, pre, s_halt, s_phase, s_ts,
                         dyn + fl.tail_off);
     }
+#ifdef DMDQN_SIM_PROFILE
+    __syncthreads();
+    if (tid == 0) {
+        prof[7] = __builtin_amdgcn_s_memrealtime() - prof_t;  // halting + write-back
+        for (int i = 0; i < 8; i++) halt[(size_t)blockIdx.x * 12 * A + i] = (int32_t)prof[i];
+    }
+#endif
 }
 
 __global__ void k_sim_reset(dmdqn_sim S, const uint8_t *mask) {
@@ -1560,9 +1602,10 @@ static int launch_sim(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t 
     const dmdqn_env_fuse f = F ? *F : dmdqn_env_fuse{};
     if (use_reg) {
         const int nt = NL <= 256 ? 256 : NL <= 512 ? 512 : 1024;
-        size_t rlds = sim_reg_lds_bytes(sim->R, sim->C);
-        if (F) rlds = fuse_layout(rlds, 0, (size_t)NL * 9 * 4, A).bytes;
-        if (nt > 512) rlds = reg_vcol_off(sim->R, sim->C, F != nullptr) + (size_t)RCAP * nt * 4;
+        const int ls = SIM_LANE_STRIDE_NT ? nt : NL;  // the kernel's lane-array stride
+        size_t rlds = sim_reg_lds_bytes(sim->R, sim->C, ls);
+        if (F) rlds = fuse_layout(rlds, 0, (size_t)ls * 9 * 4, A).bytes;
+        if (nt > 512) rlds = reg_vcol_off(sim->R, sim->C, F != nullptr, ls) + (size_t)RCAP * nt * 4;
         DMDQN_REQUIRE(rlds <= 160 * 1024, "dmdqn_sim_step: register path needs %zu bytes of LDS", rlds);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(sim->E), dim3(nt), rlds, as_stream(stream), *sim, *idm,
