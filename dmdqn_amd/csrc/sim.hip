@@ -161,9 +161,6 @@ __device__ __forceinline__ QNext next_vehicle(const View &V, int p) {
 #ifndef SIM_LANE_STRIDE_NT
 #define SIM_LANE_STRIDE_NT 1  // 0: the lane arrays NL apart, as before round 4 (A/B)
 #endif
-#ifndef SIM_VPREF
-#define SIM_VPREF 0  // 1: pass C reads the next follower's speed one vehicle ahead (A/B)
-#endif
 #ifdef DMDQN_SIM_PROFILE  // diagnostic build: per-pass ticks of thread 0 -> halt[env][0][0..7]
 #define SIM_PROF(i)                                                          \
     do {                                                                     \
@@ -1347,19 +1344,9 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 bool det = lead_x_new >= dp && lead_x_old0 < dpl;
                 float lead_x_old = lead_x_old0, lead_v_old = lead_v_old0;
                 float last_x = X_[0], last_v = vget<kL>(V_, Vc, 0);
-#if SIM_VPREF
-                // (LDS speed column) the next follower's speed is read one
-                // vehicle ahead, so its LDS latency overlaps this one's IDM
-                float v_nx = nm > 1 ? vget<kL>(V_, Vc, 1) : 0.0f;
-#endif
                 for (int i = 1; i < nm; i++) {
                     if (i < n) {
-#if SIM_VPREF
-                        const float xi = X_[i], vi = kL ? v_nx : vget<kL>(V_, Vc, i);
-                        if (kL && i + 1 < nm) v_nx = vget<kL>(V_, Vc, i + 1);
-#else
                         const float xi = X_[i], vi = vget<kL>(V_, Vc, i);
-#endif
                         const float gap = (lead_x_old - P.length) - xi;
                         const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
                         float vn = clamp_speed(vi + acc, P);
