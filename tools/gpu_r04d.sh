@@ -1,5 +1,8 @@
 #!/bin/bash
 # C5 shared-learn variant A/B, unperturbed HIP-event timing (tools/stamp_shared.py --nostamp).
+# The exp/ libraries were built by tools/build_exp.py from round-4 switches
+# (dH1/dW2 order, rows per pass, next-pass tiles/waves) that were measured
+# without a gain and are no longer in the tree; kept as a record.
 set -e
 O=gpurun_out/r04d
 mkdir -p $O
