@@ -102,3 +102,35 @@ def _compare(ref, ovl, a, b):
         assert torch.equal(getattr(ra.ring, name), getattr(rb.ring, name)), "ring." + name
     if ra.target_h is not None:
         assert torch.equal(ra.target_h, rb.target_h)
+
+
+def test_fence_free_timing_and_ordering_events():
+    """_lib.TimingEvent (bench.py's per-learn timing) measures what a torch
+    timing event measures around the same GPU sleep, and _lib.OrderEvent (the
+    env schedule's learn -> side-stream wait) orders: the side stream's work
+    recorded after waiting on it starts only after the main stream's sleep."""
+    from dmdqn_amd._lib import OrderEvent, TimingEvent
+    main, side = torch.cuda.Stream(), torch.cuda.Stream()
+    cycles = 2_000_000
+    t0, t1 = TimingEvent(), TimingEvent()
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(main):
+        r0.record(main)
+        t0.record(main)
+        torch.cuda._sleep(cycles)
+        t1.record(main)
+        r1.record(main)
+    torch.cuda.synchronize()
+    ours, ref = t0.elapsed_time(t1), r0.elapsed_time(r1)
+    assert ours > 0.1 and abs(ours - ref) <= 0.05 * ref + 0.02, (ours, ref)
+    # ordering: side waits for main's sleep through an OrderEvent
+    start, after = TimingEvent(), TimingEvent()
+    ev = OrderEvent()
+    with torch.cuda.stream(main):
+        start.record(main)
+        torch.cuda._sleep(cycles)
+        ev.record(main)
+    ev.wait(side)
+    after.record(side)
+    torch.cuda.synchronize()
+    assert start.elapsed_time(after) >= 0.9 * ref, (start.elapsed_time(after), ref)
