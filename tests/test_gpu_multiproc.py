@@ -110,13 +110,13 @@ def test_c5_shared_allreduce_equals_union_batch():
     np.testing.assert_allclose(res[0]["params"], one["params"], rtol=0, atol=2e-6)
 
 
-@pytest.mark.parametrize("shared", [False, True])
-def test_bench_two_rank_launch(shared):
+@pytest.mark.parametrize("shared,ranks", [(False, 2), (True, 2), (False, 4)])
+def test_bench_multi_rank_launch(shared, ranks):
     """The launch the driver's multi-GPU bench uses (torch.distributed.run,
-    one rank per GPU, max-over-ranks timing), rehearsed with 2 ranks on this
-    one GPU (DMDQN_DEVICE_OVERRIDE=0, gloo: RCCL needs a device per rank):
-    rank 0 prints one JSON line with n_gpus 2, the whole-job value over both
-    ranks' replicas, "weak" scaling; the shared run goes through the C5
+    one rank per GPU, max-over-ranks timing), rehearsed with 2 and 4 ranks on
+    this one GPU (DMDQN_DEVICE_OVERRIDE=0, gloo: RCCL needs a device per rank):
+    rank 0 prints one JSON line with n_gpus = ranks, the whole-job value over
+    every rank's replicas, "weak" scaling; the shared run goes through the C5
     gradient all-reduce every learn."""
     import json
     import subprocess
@@ -124,9 +124,9 @@ def test_bench_two_rank_launch(shared):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     E = 64
     args = ["--rows", "8", "--cols", "8", "--shared"] if shared else ["--rows", "2", "--cols", "2"]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(root, "bench.py"), "--gpus", "2", "--envs", str(E), "--steps", "5",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(ranks), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", str(ranks), "--envs", str(E), "--steps", "5",
            "--warmup", "2", "--prefill-steps", "130", "--no-cpu-baseline",
            "--dist-backend", "gloo"] + args
     env = dict(os.environ, DMDQN_DEVICE_OVERRIDE="0", MASTER_ADDR="127.0.0.1")
@@ -136,11 +136,11 @@ def test_bench_two_rank_launch(shared):
     assert len(lines) == 1, r.stdout  # rank 0 only
     out = json.loads(lines[0])
     A = 64 if shared else 4
-    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
-    assert out["config"]["global_envs"] == 2 * E
+    assert out["n_gpus"] == ranks and out["scaling"] == "weak"
+    assert out["config"]["global_envs"] == ranks * E
     assert out["steps"] == 5 and out["value"] > 0
-    # value = agent-env steps of both ranks / max-over-ranks wall time
-    np.testing.assert_allclose(out["value"], 5 * 2 * E * A / (out["ms_per_step"] * 5 / 1e3),
+    # value = agent-env steps of every rank / max-over-ranks wall time
+    np.testing.assert_allclose(out["value"], 5 * ranks * E * A / (out["ms_per_step"] * 5 / 1e3),
                                rtol=2e-3)
     if shared:
         assert "all-reduce" in out["config"]["parallelism"]
