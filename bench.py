@@ -253,6 +253,8 @@ def main():
                          "before the run exits non-zero naming the rank and call "
                          "(default DMDQN_DIST_TIMEOUT_S or 180)")
     args = ap.parse_args()
+    if args.time_every < 1:
+        ap.error("--time-every must be >= 1")
 
     import torch
     import torch.distributed as dist
@@ -272,8 +274,6 @@ def main():
 
     # all work on one dedicated stream: HIP events recorded on the legacy null
     # stream block the host and would inflate the timed region
-    if args.time_every < 1:
-        ap.error("--time-every must be >= 1")
     if args.overlap == "auto":
         small = (not args.shared and not args.no_fuse and not args.split_learn
                  and args.rows * args.cols * args.envs <= AUTO_ENV_MAX_AGENTS)
