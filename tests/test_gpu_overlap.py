@@ -123,14 +123,17 @@ def test_fence_free_timing_and_ordering_events():
     torch.cuda.synchronize()
     ours, ref = t0.elapsed_time(t1), r0.elapsed_time(r1)
     assert ours > 0.1 and abs(ours - ref) <= 0.05 * ref + 0.02, (ours, ref)
-    # ordering: side waits for main's sleep through an OrderEvent
-    start, after = TimingEvent(), TimingEvent()
+    # ordering: side waits for main's sleep through an OrderEvent (the sleep's
+    # own end, timed on main, bounds the side's first record from below)
+    start, slept, after = TimingEvent(), TimingEvent(), TimingEvent()
     ev = OrderEvent()
     with torch.cuda.stream(main):
         start.record(main)
         torch.cuda._sleep(cycles)
+        slept.record(main)
         ev.record(main)
     ev.wait(side)
     after.record(side)
     torch.cuda.synchronize()
-    assert start.elapsed_time(after) >= 0.9 * ref, (start.elapsed_time(after), ref)
+    t_sleep, t_after = start.elapsed_time(slept), start.elapsed_time(after)
+    assert t_sleep > 0.1 and t_after >= t_sleep - 0.005, (t_after, t_sleep)
