@@ -189,9 +189,10 @@ def _step_roofline(value, K, vbar, A, P, shared, NA):
 
 
 # --overlap auto: C2 (1,024 agents) runs 3.35 M steps/s on one
-# stream, 4.03 M with the env step of t+1 beside learn t, 4.21 M with that side
-# stream on 64 CUs (32: 3.92 M, 96: 3.79 M); C3 gains 1-3 % with a slower learn
-# kernel, so it and C5 stay on one stream (profiles/r04/c2_schedules, c3_schedules)
+# stream, 4.03 M with the env step of t+1 beside learn t, 4.41 M with that side
+# stream on 64 CUs -- the CUs C2's 256 env blocks (four per CU) fill in one round
+# (48: 3.99 M, 80: 4.00 M); C3 gains 1-3 % with a slower learn kernel, so it and
+# C5 stay on one stream (profiles/r04/c2_schedules, c2_cusplit_end, c3_schedules)
 AUTO_ENV_MAX_AGENTS = 4096
 AUTO_ENV_CU_SPLIT = 64
 
