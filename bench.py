@@ -197,6 +197,17 @@ AUTO_ENV_MAX_AGENTS = 4096
 AUTO_ENV_CU_SPLIT = 64
 
 
+def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split):
+    """--overlap auto -> (schedule, side-stream CUs): "env" on AUTO_ENV_CU_SPLIT
+    CUs (unless --cu-split names a count) for independent nets of at most
+    AUTO_ENV_MAX_AGENTS agents on the fused path, else one stream."""
+    small = (not shared and not no_fuse and not split_learn
+             and rows * cols * envs <= AUTO_ENV_MAX_AGENTS)
+    if not small:
+        return "none", cu_split
+    return "env", AUTO_ENV_CU_SPLIT if cu_split is None else cu_split
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -276,11 +287,8 @@ def main():
     # all work on one dedicated stream: HIP events recorded on the legacy null
     # stream block the host and would inflate the timed region
     if args.overlap == "auto":
-        small = (not args.shared and not args.no_fuse and not args.split_learn
-                 and args.rows * args.cols * args.envs <= AUTO_ENV_MAX_AGENTS)
-        args.overlap = "env" if small else "none"
-        if small and args.cu_split is None:
-            args.cu_split = AUTO_ENV_CU_SPLIT
+        args.overlap, args.cu_split = auto_schedule(args.rows, args.cols, args.envs, args.shared,
+                                                    args.no_fuse, args.split_learn, args.cu_split)
     side = None
     if args.cu_split:
         from dmdqn_amd._lib import cu_masked_stream

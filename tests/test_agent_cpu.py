@@ -93,3 +93,16 @@ def test_replay_ring_spare_slot_arithmetic():
             assert int(r.slots_of(0)) == (t - cap) % (cap + 1)
         r.advance()
     assert len(r) == cap and r.start == (40 - cap) % (cap + 1)
+
+
+def test_bench_auto_schedule():
+    """bench.py --overlap auto: C2 (1,024 independent agents, fused) runs the env
+    step beside the learn on 64 CUs (or the --cu-split given); C3, C5 (shared),
+    the unfused and split-learn paths stay on one stream."""
+    import bench
+    assert bench.auto_schedule(2, 2, 256, False, False, False, None) == ("env", 64)
+    assert bench.auto_schedule(2, 2, 256, False, False, False, 48) == ("env", 48)
+    assert bench.auto_schedule(4, 4, 1024, False, False, False, None) == ("none", None)
+    assert bench.auto_schedule(8, 8, 256, True, False, False, None) == ("none", None)
+    assert bench.auto_schedule(2, 2, 256, False, True, False, None) == ("none", None)
+    assert bench.auto_schedule(2, 2, 256, False, False, True, None) == ("none", None)
