@@ -195,6 +195,11 @@ def _step_roofline(value, K, vbar, A, P, shared, NA):
 # C5 stay on one stream (profiles/r04/c2_schedules, c2_cusplit_end, c3_schedules)
 AUTO_ENV_MAX_AGENTS = 4096
 AUTO_ENV_CU_SPLIT = 64
+# with it, the side stream learns one agent per side CU behind its env step
+# (its CUs idle otherwise while the learn stream works): C2 4.42 -> 4.65-4.69 M;
+# 32 / 48 / 80 / 96 / 128 agents measured 4.34 / 4.38 / 4.45 / 4.44 / 4.39 M
+# (profiles/r04/side_learn)
+AUTO_SIDE_LEARN_PER_CU = 1
 
 
 def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split):
@@ -252,6 +257,9 @@ def main():
     ap.add_argument("--time-every", type=int, default=4,
                     help="bracket every k-th learn launch of the timed region with timing "
                          "events (the roofline's average launch duration; 1 = every launch)")
+    ap.add_argument("--side-learn", type=int, default=None,
+                    help="overlap env: learn this many agents on the side stream behind its env "
+                         "step (default with --overlap auto: one per side-stream CU; else 0)")
     ap.add_argument("--fenced-events", action="store_true",
                     help="overlap env: order the side stream after the learns with default "
                          "(system-scope) events instead of ordering-only ones (A/B)")
@@ -289,6 +297,10 @@ def main():
     if args.overlap == "auto":
         args.overlap, args.cu_split = auto_schedule(args.rows, args.cols, args.envs, args.shared,
                                                     args.no_fuse, args.split_learn, args.cu_split)
+        if args.side_learn is None and args.overlap == "env" and args.cu_split:
+            args.side_learn = AUTO_SIDE_LEARN_PER_CU * args.cu_split
+    if args.side_learn is None:
+        args.side_learn = 0
     side = None
     if args.cu_split:
         from dmdqn_amd._lib import cu_masked_stream
@@ -307,7 +319,7 @@ def main():
                             shared_params=args.shared)
     tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side,
                  split_learn=args.split_learn, fused=not args.no_fuse,
-                 war_events=not args.fenced_events)
+                 war_events=not args.fenced_events, side_learn=args.side_learn)
     E, A = tr.env.E, tr.env.A
     NA = E * A
     prefill = agent_cfg.replay_buffer_size if args.prefill_steps is None else args.prefill_steps
@@ -396,7 +408,10 @@ def main():
         from dmdqn_amd.agent import n_params_keras
         P = n_params_keras(tr.agent.H)  # the reference's 28,548 parameters
         # independent = NA * (128*721 + 28P); shared (C5) = NA*128*721 + 28P
-        bpl = (NA * 128 * REPLAY_ROW_BYTES + 28 * P) if args.shared else NA * learn_bytes_per_agent(P)
+        # the timed launch: every agent, or the learn stream's part with --side-learn
+        na_timed = NA - args.side_learn
+        bpl = ((NA * 128 * REPLAY_ROW_BYTES + 28 * P) if args.shared
+               else na_timed * learn_bytes_per_agent(P))
         avg_learn_s = float(np.mean(learn_ms)) / 1e3 if learn_ms else float("nan")
         achieved = bpl / avg_learn_s / 1e9
         wl = f"{args.rows}x{args.cols}x{args.envs}"
@@ -450,7 +465,9 @@ def main():
                             + ("; act + sim + observe + store fused in one launch per env"
                                if tr.fused else "")
                             + (f"; side stream on {args.cu_split} CUs"
-                               + (" (strided)" if args.cu_stride else "") if args.cu_split else ""),
+                               + (" (strided)" if args.cu_stride else "") if args.cu_split else "")
+                            + (f"; the learn of {args.side_learn} agents on the side stream"
+                               if args.side_learn else ""),
             },
             "cpu_baseline": cpu,
             # secondary figures SURVEY 8d asks for next to the headline roofline
@@ -479,7 +496,7 @@ def main():
             "bytes_per_launch": bpl,
             **timing,
         }
-        flop = NA * LEARN_FLOP_PER_AGENT
+        flop = (NA if args.shared else na_timed) * LEARN_FLOP_PER_AGENT
         mfma_roof = {
             "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared
                        else LEARN_KERNELS[args.precision]) +

@@ -424,9 +424,19 @@ class BatchedDQN:
         """One fused learn for every agent (None while underfilled).  With
         collect_stats, self.qstats [NA, 6] receives the batch metrics of
         dqn_agent.py:361-363 (see learn_metrics)."""
+        if not self.learn_begin(collect_stats):
+            return None
+        return self.learn_range(0, self.NA)
+
+    def learn_begin(self, collect_stats=False):
+        """The host half of learn(): the replay draws (or the presampled ones),
+        the learn counter and the Keras Adam constants of this learn.  False
+        while underfilled.  The launches follow with learn_range(lo, hi) over
+        agent ranges that cover [0, NA) -- independent agents, so ranges may
+        run on different streams (trainer overlap "env" with side_learn)."""
         n = len(self.ring)
         if n < self.cfg.batch_size:
-            return None
+            return False
         cfg = self.cfg
         if self._presampled is not None:
             pn, buf = self._presampled
@@ -441,28 +451,44 @@ class BatchedDQN:
         sync = self.learn_step_counter % cfg.target_update_frequency == 0
         qstats = self.qstats.zero_() if collect_stats else None
         self._last_learn = (alpha, c1, c2, eps, sync, qstats)
-        if self.learn_hook:
-            self.learn_hook(True)
-        ring = self.ring
+        self.learn_launches += 1
+        return True
+
+    def learn_range(self, lo, hi):
+        """Launch the learn begun by learn_begin() for agents [lo, hi) on the
+        current stream (the whole range for the shared net).  The timing hook
+        brackets the range that starts at agent 0.  Returns self.loss."""
+        alpha, c1, c2, eps, sync, qstats = self._last_learn
+        cfg, ring = self.cfg, self.ring
+        hook = self.learn_hook if lo == 0 else None
+        if hook:
+            hook(True)
         if self.shared:
+            if (lo, hi) != (0, self.NA):
+                raise ValueError("the shared-net learn runs over every agent at once")
             self._learn_shared(alpha, c1, c2, eps, sync, qstats)
         else:
             xs = xn = None
             if ring.row_format == "f32":  # float rows: the batch gathered in order first
+                if (lo, hi) != (0, self.NA):
+                    raise ValueError("float-row learns run over every agent at once")
                 if self._xs is None:
                     shape = (self.NA, cfg.batch_size, K.ROW_FLOATS)
                     self._xs = torch.empty(shape, dtype=torch.float32, device=self.device)
                     self._xn = torch.empty(shape, dtype=torch.float32, device=self.device)
                 ring.gather_f32(self.idx, self._xs, self._xn)
                 xs, xn = self._xs, self._xn
-            self._ops.learn_step(ring.s, ring.n, ring.a, ring.d, ring.r, self.idx, self.params,
-                                 self.adam_m, self.adam_v, self.target, self.target_h, self.loss,
-                                 ring.start, self.H, PRECISIONS[cfg.precision], sync, cfg.gamma,
-                                 alpha, c1, c2, eps, LOSSES[cfg.loss], qstats, self.rn_out,
-                                 self.stamps, grad=self._split_grad, xs=xs, xn=xn)
-        if self.learn_hook:
-            self.learn_hook(False)
-        self.learn_launches += 1
+
+            def sl(t):
+                return None if t is None else t[lo:hi]
+            self._ops.learn_step(sl(ring.s), sl(ring.n), sl(ring.a), sl(ring.d), sl(ring.r),
+                                 sl(self.idx), sl(self.params), sl(self.adam_m), sl(self.adam_v),
+                                 sl(self.target), sl(self.target_h), sl(self.loss), ring.start,
+                                 self.H, PRECISIONS[cfg.precision], sync, cfg.gamma, alpha, c1, c2,
+                                 eps, LOSSES[cfg.loss], sl(qstats), sl(self.rn_out),
+                                 sl(self.stamps), grad=sl(self._split_grad), xs=xs, xn=xn)
+        if hook:
+            hook(False)
         return self.loss
 
     def c_learn_args(self):

@@ -43,7 +43,10 @@ sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
               side:  [wait learn t-1] env_step_{t+1} sample_{t+1} (ev_env)
               main:  [wait ev_env of t] learn_t
             With a CU-masked side stream (bench --cu-split) the two split the
-            chip.
+            chip.  side_learn=m runs the learn of the last m agents on the side
+            stream behind its env step and draws (those CUs idle otherwise):
+              side:  ... sample_{t+1} (ev_env) learn_{t+1}[NA-m, NA)
+              main:  [wait ev_env] learn_{t+1}[0, NA-m)
 
 What a step returns or exposes per step (obs, reward, loss, agent.actions,
 agent.idx) is fresh or double-buffered, so the caller may read it on its own
@@ -72,7 +75,7 @@ class StepStats:
 class Trainer:
     def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
                  overlap="none", side_stream=None, split_learn=False, fused=True,
-                 war_events=True):
+                 war_events=True, side_learn=0):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
         if overlap is True or overlap is False:
             overlap = "full" if overlap else "none"
@@ -101,6 +104,16 @@ class Trainer:
         if overlap == "env" and not self.fused:
             raise ValueError('overlap "env" runs the fused env step (int8 replay rows, fused=True)')
         self._ev_learn_prev = None  # overlap "env": the learn before the last one
+        # overlap "env": the learn of the last `side_learn` agents runs on the
+        # side stream behind the env step and the draws (its CUs idle
+        # otherwise while the learn stream works), the rest on the learn
+        # stream; independent agents, so the results are the same
+        self.side_learn = int(side_learn)
+        if self.side_learn:
+            if overlap != "env":
+                raise ValueError('side_learn runs with overlap "env"')
+            if self.agent.shared or not 0 < self.side_learn < self.agent.NA:
+                raise ValueError("side_learn: independent nets, 0 < side_learn < E*A")
         # overlap "env" at a fixed epsilon of 1 (A-1: the side stream never reads
         # a learn's output): the learn -> side-stream wait only orders the store
         # of t+2 after learn t's ring reads, so it uses ordering-only events
@@ -228,8 +241,17 @@ class Trainer:
             self.obs = self._after_step(done, next_obs, info)  # (an episode reset: on side)
             ev_env = torch.cuda.Event()
             ev_env.record(side)
+        learned = agent.learn_begin(collect_stats)  # the draws above, the Adam constants
+        ev_side = None
+        if learned and self.side_learn:
+            with torch.cuda.stream(side):
+                agent.learn_range(agent.NA - self.side_learn, agent.NA)
+                ev_side = torch.cuda.Event()
+                ev_side.record(side)
         main.wait_event(ev_env)  # the store learn t reads; what the caller reads after step()
-        loss = agent.learn(collect_stats=collect_stats)
+        loss = None
+        if learned:
+            loss = agent.learn_range(0, agent.NA - self.side_learn)
         self._ev_learn_prev = self._ev_learn
         if (self._war_ring is not None and not agent.cfg.count_env_steps
                 and agent.current_epsilon() >= 1.0):
@@ -242,6 +264,10 @@ class Trainer:
         else:
             self._ev_learn = torch.cuda.Event()
             self._ev_learn.record(main)
+        if ev_side is not None:
+            # the side's part of the loss / stats, for the caller's stream (the
+            # next learn waits for it anyway: it is behind the next env step)
+            main.wait_event(ev_side)
         self.last_loss, self.last_reward = loss, reward
         return StepStats(loss is not None, done)
 

@@ -14,12 +14,12 @@ from dmdqn_amd.env import EnvConfig  # noqa: E402
 from dmdqn_amd.trainer import Trainer  # noqa: E402
 
 
-def _trainer(overlap, precision, shared, greedy, side_stream=None, cap=200):
+def _trainer(overlap, precision, shared, greedy, side_stream=None, cap=200, side_learn=0):
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=8, seed=11, max_sim_time=500),
                  AgentConfig(replay_buffer_size=cap, target_update_frequency=9, seed=4,
                              precision=precision, shared_params=shared,
                              count_env_steps=greedy),
-                 overlap=overlap, side_stream=side_stream)
+                 overlap=overlap, side_stream=side_stream, side_learn=side_learn)
     if greedy:  # past the 8000-step epsilon floor (dqn_agent.py:258-261)
         tr.agent.global_step_count = 12000
     return tr
@@ -45,6 +45,28 @@ def test_overlap_matches_sequential(mode, precision, shared, greedy):
     assert ovl.side is not None and ref.side is None
     a, b = _run(ref, 170), _run(ovl, 170)   # 3 episodes of 50 steps, learn from step 128
     _compare(ref, ovl, a, b)
+
+
+@pytest.mark.parametrize("precision,greedy,masked", [
+    ("fp16", False, True), ("bf16", False, False), ("fp32", False, True), ("fp16", True, True)])
+def test_side_learn_matches_sequential(precision, greedy, masked):
+    """overlap "env" with side_learn: the last 12 of 32 agents learn on the side
+    stream behind the env step (the rest on the learn stream), across episode
+    resets, target syncs and a greedy act that reads both parts' weights:
+    bit-identical to the sequential loop."""
+    side = None
+    if masked:
+        from dmdqn_amd._lib import cu_masked_stream
+        side = cu_masked_stream(range(32))
+        main = cu_masked_stream(range(32, torch.cuda.get_device_properties(0).multi_processor_count))
+        torch.cuda.set_stream(main)
+    try:
+        ref = _trainer("none", precision, False, greedy)
+        ovl = _trainer("env", precision, False, greedy, side_stream=side, side_learn=12)
+        a, b = _run(ref, 170), _run(ovl, 170)
+        _compare(ref, ovl, a, b)
+    finally:
+        torch.cuda.set_stream(torch.cuda.default_stream())
 
 
 def test_overlap_on_cu_masked_streams_matches_sequential():
