@@ -50,6 +50,9 @@ for CFG in "$@"; do
          python3 tools/pmc_learn.py "$F" "$W" "${KEY%%_*}_envstep" "$ENVK" "profiles/$TAG/$CFG" &&
          for K1 in ${LK//|/ }; do python3 tools/pmc_mfma.py "$M" "$K1" > $O/mfma_busy_$K1.json; done)
     cp "$(find $O/stats -name '*kernel_stats.csv' | head -n 1)" $O/kernel_stats.csv
+    # per launch size (a kernel launched at two sizes, e.g. C2's side-stream learn)
+    python3 $R/tools/trace_by_grid.py "$(find $O/stats -name '*kernel_trace.csv' | head -n 1)" \
+        k_learn k_shared k_sim_step k_sample > $O/kernel_stats_by_grid.json
     gzip -c "$F" > $O/fetch_size_counter_collection.csv.gz
     gzip -c "$W" > $O/write_size_counter_collection.csv.gz
     gzip -c "$M" > $O/mfma_counter_collection.csv.gz
