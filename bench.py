@@ -174,6 +174,44 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, traffic_src, traffic_stale, in_ld
 
 
 SIM_PROBE_STEPS = 10  # untimed steps after the timed region that time the sim
+STREAM_PROBE_BYTES = 4 << 30  # bytes copied per launch by the HBM streaming probe
+STREAM_PROBE_REPS = 5
+
+
+def stream_probe(stream, n_bytes=STREAM_PROBE_BYTES, reps=STREAM_PROBE_REPS):
+    """This box's HBM streaming rate, in this process, on the learn's stream
+    (dmdqn_stream_probe, csrc/probe.hip): a float4 copy of n_bytes (read n,
+    write n) and a triad (read 2n, write n, about the learn's own read:write
+    mix), each launched reps times behind one untimed launch and timed with
+    fence-free HIP events.  Returns {"copy_gbs", "triad_gbs"} (median of the
+    reps, algorithmic bytes / launch time) -- boxes of the pool differ by up
+    to ~15 % on one binary, so the learn's fraction of THIS figure separates
+    the box from the code."""
+    import ctypes as C
+
+    import torch
+    from dmdqn_amd._lib import TimingEvent, call
+    dev = stream.device
+    src = torch.empty(2 * n_bytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty(n_bytes // 4, dtype=torch.float32, device=dev)
+    src.fill_(1.0)
+    out = {}
+    for mode, name, moved in ((0, "copy_gbs", 2 * n_bytes), (1, "triad_gbs", 3 * n_bytes)):
+        ms = []
+        args = (C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), C.c_size_t(n_bytes), mode,
+                C.c_void_p(stream.cuda_stream))
+        call("dmdqn_stream_probe", *args)
+        for _ in range(reps):
+            e0, e1 = TimingEvent(), TimingEvent()
+            e0.record(stream)
+            call("dmdqn_stream_probe", *args)
+            e1.record(stream)
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        out[name] = round(moved / (float(np.median(ms)) / 1e3) / 1e9, 1)
+    del src, dst
+    torch.cuda.empty_cache()
+    return out
 
 
 def _step_roofline(value, K, vbar, A, P, shared, NA):
@@ -202,15 +240,37 @@ AUTO_ENV_CU_SPLIT = 64
 AUTO_SIDE_LEARN_PER_CU = 1
 
 
-def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split):
-    """--overlap auto -> (schedule, side-stream CUs): "env" on AUTO_ENV_CU_SPLIT
-    CUs (unless --cu-split names a count) for independent nets of at most
-    AUTO_ENV_MAX_AGENTS agents on the fused path, else one stream."""
-    small = (not shared and not no_fuse and not split_learn
-             and rows * cols * envs <= AUTO_ENV_MAX_AGENTS)
+def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split, side_learn=None):
+    """--overlap auto -> (schedule, side-stream CUs, side-stream agents): "env"
+    on AUTO_ENV_CU_SPLIT CUs (unless --cu-split names a count) for independent
+    nets of at most AUTO_ENV_MAX_AGENTS agents on the fused path, else one
+    stream.  Under "env" the side stream learns AUTO_SIDE_LEARN_PER_CU agents
+    per side CU (unless --side-learn names a count), at most half the agents
+    (Trainer needs 0 <= side_learn < E*A); side_learn is 0 otherwise."""
+    NA = rows * cols * envs
+    small = (not shared and not no_fuse and not split_learn and NA <= AUTO_ENV_MAX_AGENTS)
     if not small:
-        return "none", cu_split
-    return "env", AUTO_ENV_CU_SPLIT if cu_split is None else cu_split
+        return "none", cu_split, 0 if side_learn is None else side_learn
+    cus = AUTO_ENV_CU_SPLIT if cu_split is None else cu_split
+    if side_learn is None:
+        side_learn = min(AUTO_SIDE_LEARN_PER_CU * cus, NA // 2) if cus else 0
+    return "env", cus, side_learn
+
+
+def make_streams(dev, cu_split=None, cu_stride=False):
+    """(learn stream, side stream or None) of bench.py: with cu_split, two
+    CU-masked HIP streams (the side one on cu_split CUs: 0..k-1, or every
+    n_cu/k-th CU with cu_stride; the learn stream on the rest), else one
+    dedicated stream (events recorded on the legacy null stream block the host)."""
+    import torch
+    if not cu_split:
+        return torch.cuda.Stream(dev), None
+    from dmdqn_amd._lib import cu_masked_stream
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    k = cu_split
+    side_cus = [round(i * n_cu / k) for i in range(k)] if cu_stride else list(range(k))
+    work = cu_masked_stream([c for c in range(n_cu) if c not in set(side_cus)], dev)
+    return work, cu_masked_stream(side_cus, dev)
 
 
 def main():
@@ -263,6 +323,9 @@ def main():
     ap.add_argument("--fenced-events", action="store_true",
                     help="overlap env: order the side stream after the learns with default "
                          "(system-scope) events instead of ordering-only ones (A/B)")
+    ap.add_argument("--no-stream-probe", action="store_true",
+                    help="skip the HBM streaming probe after the timed region (roofline."
+                         "copy_gbs / frac_of_copy)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="act / sim / observe / store as four launches instead of the fused "
                          "env step (dmdqn_env_step; bit-identical, A/B)")
@@ -295,22 +358,12 @@ def main():
     # all work on one dedicated stream: HIP events recorded on the legacy null
     # stream block the host and would inflate the timed region
     if args.overlap == "auto":
-        args.overlap, args.cu_split = auto_schedule(args.rows, args.cols, args.envs, args.shared,
-                                                    args.no_fuse, args.split_learn, args.cu_split)
-        if args.side_learn is None and args.overlap == "env" and args.cu_split:
-            args.side_learn = AUTO_SIDE_LEARN_PER_CU * args.cu_split
+        args.overlap, args.cu_split, args.side_learn = auto_schedule(
+            args.rows, args.cols, args.envs, args.shared, args.no_fuse, args.split_learn,
+            args.cu_split, args.side_learn)
     if args.side_learn is None:
         args.side_learn = 0
-    side = None
-    if args.cu_split:
-        from dmdqn_amd._lib import cu_masked_stream
-        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-        k = args.cu_split
-        side_cus = ([round(i * n_cu / k) for i in range(k)] if args.cu_stride else list(range(k)))
-        work = cu_masked_stream([c for c in range(n_cu) if c not in set(side_cus)], dev)
-        side = cu_masked_stream(side_cus, dev)
-    else:
-        work = torch.cuda.Stream(dev)
+    work, side = make_streams(dev, args.cu_split, args.cu_stride)
     torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
@@ -401,7 +454,10 @@ def main():
     sim_ms = [s0.elapsed_time(s1) / SIM_PROBE_STEPS]
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    probe = stream_probe(work) if not args.no_stream_probe else None
     el_max = D.max_over_ranks(el, device=dev, timeout_s=args.dist_timeout)
+    # every rank's GPU (PCI address, UUID): a multi-GPU record shows N distinct devices
+    device_ids = D.gather_device_ids(dev, timeout_s=args.dist_timeout)
 
     if rank == 0:
         value = args.steps * NA * world / el_max
@@ -430,6 +486,10 @@ def main():
             "value": round(value, 1),
             "unit": "agent-env steps/s",
             "n_gpus": world,
+            # the process group's size and each rank's device (rank|name|PCI|UUID)
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "devices": device_ids,
+            "distinct_devices": len({d.split("|", 2)[2] for d in device_ids}),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el_max / args.steps * 1e3, 4),
@@ -496,6 +556,15 @@ def main():
             "bytes_per_launch": bpl,
             **timing,
         }
+        if probe:
+            # the same process's HBM streaming rate on this box (stream_probe)
+            hbm_roof.update({
+                "copy_gbs": probe["copy_gbs"], "triad_gbs": probe["triad_gbs"],
+                "frac_of_copy": round(achieved / probe["copy_gbs"], 4),
+                "frac_of_triad": round(achieved / probe["triad_gbs"], 4),
+                "probe": (f"dmdqn_stream_probe after the timed region, learn stream: float4 copy "
+                          f"of {STREAM_PROBE_BYTES >> 30} GiB (read + write) and triad (2 reads + "
+                          f"1 write), median of {STREAM_PROBE_REPS} launches")})
         flop = (NA if args.shared else na_timed) * LEARN_FLOP_PER_AGENT
         mfma_roof = {
             "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared

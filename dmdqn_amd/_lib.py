@@ -42,6 +42,7 @@ SIGNATURES = {
     "dmdqn_event_synchronize": [vp],
     "dmdqn_event_elapsed_ms": [vp, vp, vp],
     "dmdqn_event_destroy": [vp],
+    "dmdqn_stream_probe": [vp, vp, C.c_size_t, i32, vp],
 }
 
 

@@ -247,6 +247,8 @@ class AgentConfig:
 class BatchedDQN:
     """E*A independent DQN agents (agent index = env * A + junction)."""
 
+    OUT_BUFS = 3  # rotating loss / qstats buffers (see __init__)
+
     def __init__(self, num_envs, n_agents, cfg: AgentConfig = None, device="cuda",
                  env_seeds=None, init_weights=None, streams=None):
         self.cfg = cfg = cfg or AgentConfig()
@@ -322,8 +324,17 @@ class BatchedDQN:
                           for _ in range(2)]
         self.idx = self._idx_bufs[0]
         self._presampled = None  # (n, buffer) drawn ahead by presample()
-        self.loss = torch.zeros(NA, dtype=torch.float32, device=dev)
-        self.qstats = torch.zeros((NA, 6), dtype=torch.float32, device=dev)
+        # per-learn outputs rotate over OUT_BUFS buffers (learn k writes buffer
+        # k % OUT_BUFS): under trainer overlap "env" with side_learn, the side
+        # stream's learn of step t+1 may run before the caller's main-stream
+        # read of step t's loss / stats, and the side stream is ordered only
+        # after learn t-1 -- so learn t+1 and t+2 must write other buffers
+        # than the one step t's reader holds
+        self._loss_bufs = [torch.zeros(NA, dtype=torch.float32, device=dev)
+                           for _ in range(self.OUT_BUFS)]
+        self._qstats_bufs = [torch.zeros((NA, 6), dtype=torch.float32, device=dev)
+                             for _ in range(self.OUT_BUFS)]
+        self.loss, self.qstats = self._loss_bufs[0], self._qstats_bufs[0]
         # alternating action buffers: a caller may still read step t's actions on
         # its stream while the trainer's side stream writes step t+1's
         self._act_bufs = [torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
@@ -449,7 +460,13 @@ class BatchedDQN:
         self.learn_step_counter += 1
         alpha, c1, c2, eps = keras_adam_consts(self.learn_step_counter, cfg.learning_rate)
         sync = self.learn_step_counter % cfg.target_update_frequency == 0
-        qstats = self.qstats.zero_() if collect_stats else None
+        k = self.learn_step_counter % self.OUT_BUFS
+        self.loss = self._loss_bufs[k]
+        qstats = None
+        if collect_stats:
+            # zeroed per agent range by learn_range, on the stream that launches
+            # the range (the side stream's part must not wait on main)
+            self.qstats = qstats = self._qstats_bufs[k]
         self._last_learn = (alpha, c1, c2, eps, sync, qstats)
         self.learn_launches += 1
         return True
@@ -461,6 +478,8 @@ class BatchedDQN:
         alpha, c1, c2, eps, sync, qstats = self._last_learn
         cfg, ring = self.cfg, self.ring
         hook = self.learn_hook if lo == 0 else None
+        if qstats is not None:
+            qstats[lo:hi].zero_()  # the kernels accumulate into it
         if hook:
             hook(True)
         if self.shared:
@@ -552,13 +571,19 @@ class BatchedDQN:
         world = 1
         if dist.is_available() and dist.is_initialized():
             world = dist.get_world_size()
-            if world > 1 and dist.get_backend() == "gloo" and self.grad.is_cuda:
+        if world > 1:
+            # one flat 114 KB buffer per learn, bounded (dist.BoundedAllReduce:
+            # the host runs a few learns ahead; a stalled peer raises DistError)
+            from . import dist as D
+            if getattr(self, "_allreduce", None) is None:
+                self._allreduce = D.BoundedAllReduce()
+            if dist.get_backend() == "gloo" and self.grad.is_cuda:
                 # gloo (several ranks on one device: the multi-process tests) reduces host memory
                 g = self.grad.cpu()
-                dist.all_reduce(g, op=dist.ReduceOp.SUM)
+                self._allreduce(g)
                 self.grad.copy_(g)
-            elif world > 1:
-                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)  # one flat 114 KB buffer
+            else:
+                self._allreduce(self.grad)
         self._ops.adam(self.params, self.adam_m, self.adam_v, self.target, self.target_h,
                        self.params_h, self.grad, 1.0 / world, alpha, c1, c2, eps, sync)
 

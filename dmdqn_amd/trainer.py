@@ -249,6 +249,11 @@ class Trainer:
                 ev_side = torch.cuda.Event()
                 ev_side.record(side)
         main.wait_event(ev_env)  # the store learn t reads; what the caller reads after step()
+        # side-allocated outputs the caller reads on main: without
+        # this the allocator could hand their blocks to step t+2's side work
+        # while a main-stream read of them is still queued
+        for t in (next_obs, reward, env.local, self.obs):
+            t.record_stream(main)
         loss = None
         if learned:
             loss = agent.learn_range(0, agent.NA - self.side_learn)
@@ -256,7 +261,13 @@ class Trainer:
         if (self._war_ring is not None and not agent.cfg.count_env_steps
                 and agent.current_epsilon() >= 1.0):
             # epsilon cannot fall below 1 later (count_env_steps off): no act
-            # will read this learn's weights through the side stream
+            # will read this learn's weights through the side stream.  What the
+            # side stream reads of main's work is then nothing: the side learn
+            # (side_learn) reads only its own agents' weights, rings and draws,
+            # all written on the side stream -- so an ordering-only event
+            # (write after read: the store of t+2 after learn t's ring reads)
+            # is enough.  A data hand-over main -> side takes a full event.
+            assert self._side_reads_nothing_from_main(), "ordering-only event with a RAW hazard"
             ev = self._war_ring[self._war_i]
             self._war_i = (self._war_i + 1) % len(self._war_ring)
             ev.record(main)
@@ -270,6 +281,15 @@ class Trainer:
             main.wait_event(ev_side)
         self.last_loss, self.last_reward = loss, reward
         return StepStats(loss is not None, done)
+
+    def _side_reads_nothing_from_main(self):
+        """The "env" schedule's invariant for ordering-only learn events: no
+        greedy act (its forward reads the learn stream's weights) and the side
+        learn's agent range [NA - side_learn, NA) disjoint from the learn
+        stream's [0, NA - side_learn)."""
+        ag = self.agent
+        return (ag.current_epsilon() >= 1.0 and not ag.cfg.count_env_steps
+                and not ag.shared and 0 <= self.side_learn < ag.NA)
 
     def _after_step(self, done, next_obs, info, side=None, main=None):
         """Counters and the observation the next act sees (train.py:188-209).

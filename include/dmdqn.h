@@ -110,6 +110,15 @@ int dmdqn_event_synchronize(void *event);
 int dmdqn_event_elapsed_ms(void *start, void *end, float *ms);
 int dmdqn_event_destroy(void *event);
 
+/* HBM streaming probe (round 5): bench.py times it once, outside the timed
+ * region, on the learn's stream, and reports the learn's bandwidth as a
+ * fraction of what this box streams in the same process.  mode 0: copy,
+ * dst[i] = src[i] over n_bytes (n_bytes read, n_bytes written); mode 1:
+ * triad, dst[i] = src[i] + src[n_bytes/4 + i] in f32 (src holds 2 * n_bytes:
+ * 2 n_bytes read, n_bytes written).  16-B aligned, n_bytes a multiple of 16.
+ * No reference counterpart. */
+int dmdqn_stream_probe(void *dst, const void *src, size_t n_bytes, int mode, void *stream);
+
 /* ------------------------------------------------------------------ streams
  * Seed E MT19937 streams on the device.
  *  _np: numpy legacy RandomState.seed(int) (init_genrand); replaces the global

@@ -25,9 +25,10 @@ def _worker(rank, ws, port, q):
     off, seeds = D.shard(r, 8, base_seed=1000)
     m = D.max_over_ranks(1.5 + r)
     g = torch.full((5,), float(r + 1))
-    D.allreduce_mean_(g)
+    D.BoundedAllReduce()(g)
+    ids = D.gather_device_ids("cpu")
     D.barrier()
-    q.put((r, off, seeds.tolist(), m, g.tolist()))
+    q.put((r, off, seeds.tolist(), m, g.tolist(), ids))
     dist.destroy_process_group()
 
 
@@ -46,14 +47,15 @@ def test_shard_timing_and_allreduce(ws):
     assert len(set(seeds)) == 8 * ws                       # disjoint replicas
     assert [r[1] for r in res] == [0, 8]                   # env offsets
     assert all(r[3] == 1.5 + ws - 1 for r in res)          # max over ranks
-    assert all(np.allclose(r[4], (1 + ws) / 2.0) for r in res)  # mean of 1..ws
+    assert all(np.allclose(r[4], ws * (1 + ws) / 2.0) for r in res)  # sum of 1..ws
+    assert all(r[5] == [f"{k}|cpu|-|-" for k in range(ws)] for r in res)  # every rank's id
 
 
 def test_single_process_defaults():
     from dmdqn_amd import dist as D
     assert D.max_over_ranks(3.0) == 3.0
     t = torch.ones(3)
-    assert torch.equal(D.allreduce_mean_(t), torch.ones(3))
+    assert torch.equal(D.BoundedAllReduce()(t), torch.ones(3))
     off, seeds = D.shard(3, 4, 10)
     assert off == 12 and list(seeds) == [22, 23, 24, 25]
 
@@ -171,3 +173,96 @@ def test_stalled_barrier_fails_fast_with_its_cause():
         p.join(timeout=30)
     assert msg.startswith("rank 0 of 2: barrier failed"), msg
     assert dt < 30, dt
+
+
+def _skipping_peer(rank, port, q):
+    """C5 learn orchestration (kernels stubbed) where rank 1 skips its
+    gradient all-reduce and then stalls: rank 0's bounded all-reduce must
+    raise DistError naming the rank and the call within the timeout
+    (DMDQN_DIST_TIMEOUT_S, read at import)."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE="2", LOCAL_RANK=str(rank), DMDQN_DIST_TIMEOUT_S="4")
+    from types import SimpleNamespace
+
+    import dmdqn_amd.agent as AG
+    from dmdqn_amd import dist as D
+    D.init(backend="gloo")
+    if rank == 1:
+        time.sleep(30)
+        return
+    P = 8
+    ring = SimpleNamespace(s=None, n=None, a=None, d=None, r=None, start=0)
+    fake = SimpleNamespace(NA=4, n_slabs=2, P=P, device="cpu", ring=ring, idx=None,
+                           cfg=AG.AgentConfig(), loss=None, rn_out=None,
+                           slab=torch.zeros((2, P)), grad=torch.zeros(P),
+                           params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
+                           target=torch.zeros(P), target_h=None, params_h=None, shared_work=None,
+                           _ops=SimpleNamespace(learn_shared_grad=lambda *a, **k: None,
+                                                adam=lambda *a, **k: None))
+    t0 = time.time()
+    try:
+        AG.BatchedDQN._learn_shared(fake, 1e-3, 0.1, 1e-3, 1e-7, False, None)
+        q.put(("passed", time.time() - t0))
+    except D.DistError as e:
+        q.put((str(e), time.time() - t0))
+
+
+def test_skipped_gradient_allreduce_fails_fast_naming_the_rank():
+    """the C5 gradient all-reduce is bounded -- a peer that
+    skips it makes the learn raise within the timeout instead of hanging."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_skipping_peer, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    msg, dt = q.get(timeout=90)
+    for p in ps:  # rank 1 is still asleep
+        p.kill()
+        p.join(timeout=30)
+    assert msg.startswith("rank 0 of 2: all_reduce(SUM) of the shared-net gradient failed"), msg
+    assert dt < 30, dt
+
+
+class _FakeWork:
+    def __init__(self, done_after):
+        self.t = __import__("time").monotonic() + done_after
+
+    def wait(self, timeout=None):
+        return True
+
+    def is_completed(self):
+        return __import__("time").monotonic() >= self.t
+
+
+def test_bounded_allreduce_lag_and_timeout(monkeypatch):
+    """The RCCL branch of BoundedAllReduce without a device: the host blocks
+    only once more than `lag` reductions are incomplete, and raises DistError
+    (rank, call) once the oldest is older than the timeout."""
+    from dmdqn_amd import dist as D
+    works = []
+
+    def fake_all_reduce(t, op=None, async_op=False):
+        w = _FakeWork(done_after=works_delay[0])
+        works.append(w)
+        return w
+
+    works_delay = [0.0]
+    monkeypatch.setattr(D.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(D.dist, "get_world_size", lambda: 2)
+    monkeypatch.setattr(D.dist, "get_backend", lambda: "nccl")
+    monkeypatch.setattr(D.dist, "all_reduce", fake_all_reduce)
+    ar = D.BoundedAllReduce(lag=2, timeout_s=0.5)
+    t = torch.zeros(3)
+    for _ in range(5):  # complete at once: nothing stays pending
+        ar(t)
+    assert len(ar._pending) <= 1
+    works_delay[0] = 3600.0  # never completes within the test
+    ar(t)
+    ar(t)
+    import time
+    t0 = time.monotonic()
+    with pytest.raises(D.DistError, match="all_reduce\\(SUM\\) of the shared-net gradient failed"):
+        ar(t)  # the third incomplete one: blocks on the oldest, then times out
+    assert 0.3 < time.monotonic() - t0 < 5

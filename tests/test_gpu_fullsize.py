@@ -109,7 +109,7 @@ def _check_shared_grad(tr, raw, pre, agents0, n_sub=64):
     assert close.mean() > 0.99, f"{np.sum(~close)} shared-gradient entries off"
 
 
-def _check_learn(tr, agents, pre, precision, shared, t32=None):
+def _check_learn(tr, agents, pre, precision, shared, t32=None, stats=False):
     """One learn of tr's last step for `agents`, from the pre-step state `pre`.
     t32: the loss tolerance vs the fp32 oracle: an rtol, or "q-scaled"
     (default): TOL16's rtol or, where larger, the change in the mean squared
@@ -128,6 +128,7 @@ def _check_learn(tr, agents, pre, precision, shared, t32=None):
     loss = ag.loss.cpu().numpy()
     assert np.isfinite(loss).all(), "every agent's loss is finite"
     idx = ag.idx.cpu().numpy()
+    qs = ag.qstats.cpu().numpy() if stats else None
     rn = ag.rn_out.cpu().numpy()
     t = ag.learn_step_counter
     p_now = kernel_to_keras(ag.params[0:1].cpu().numpy(), 128)[0] if shared else None
@@ -137,6 +138,16 @@ def _check_learn(tr, agents, pre, precision, shared, t32=None):
         p0, t0, m0, v0 = (x[0 if shared else k] for x in pre)
         l_e, g_e, _, _, _ = _mixed_emulation(p0, t0, m0, v0, S, Aa, Rn, S2, D, t, rnd=rnd)
         np.testing.assert_allclose(loss[j], l_e, rtol=tl, err_msg=f"agent {j} vs emulation")
+        if stats:
+            # dqn_agent.py:361-363: sum Q, sum Q^2 and the action counts of
+            # the batch's online Q(S) -- the 16-bit forward of the pre-learn net
+            q = O.qnet_forward_mixed(p0, S, precision).astype(np.float64)
+            np.testing.assert_allclose(qs[j, 0], q.sum(), rtol=1e-3, atol=1e-3 * np.abs(q).sum(),
+                                       err_msg=f"agent {j}: sum Q")
+            np.testing.assert_allclose(qs[j, 1], (q * q).sum(), rtol=2e-3,
+                                       err_msg=f"agent {j}: sum Q^2")
+            np.testing.assert_array_equal(qs[j, 2:6], np.bincount(Aa, minlength=4),
+                                          err_msg=f"agent {j}: action counts")
         p1, m1, v1 = p0.copy(), m0.copy(), v0.copy()
         l32 = O.learn(p1, t0, m1, v1, S, Aa, Rn, S2, D, t)
         if q_scaled:
@@ -158,13 +169,16 @@ def _check_learn(tr, agents, pre, precision, shared, t32=None):
 
 
 def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, sparse_until=0,
-                t32=None, shared_grad_checks=()):
+                t32=None, shared_grad_checks=(), trainer_kw=None, stats_checks=()):
     """sparse_until: before this step, compare with the oracle only every 97th
     step (the oracle loops still run every step).  t32: _check_learn's.
     shared_grad_checks: learns (as in learn_checks) at which _check_shared_grad
-    also runs, on the agents of the middle replica."""
+    also runs, on the agents of the middle replica.  trainer_kw: extra Trainer
+    arguments (a schedule, its streams).  stats_checks: steps whose learn runs
+    with collect_stats, its per-agent Q statistics checked against the oracle
+    forward of the pre-learn weights for the picked agents."""
     cfg = AgentConfig(precision=precision, seed=0, shared_params=shared)
-    tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=0), cfg)
+    tr = Trainer(EnvConfig(rows=rows, cols=cols, num_envs=envs, seed=0), cfg, **(trainer_kw or {}))
     A, ag = tr.env.A, tr.agent
     sampled = [0, envs // 2, envs - 1]
     loops = [O.OracleLoop(rows, cols, int(tr.env.seeds[e]), learn=False) for e in sampled]
@@ -182,7 +196,7 @@ def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, 
                    for k in ["params", "target", "adam_m", "adam_v"]]
             if step + 1 in shared_grad_checks:
                 raw = [getattr(ag, k).clone() for k in ["params", "target", "adam_m", "adam_v"]]
-        tr.step()
+        tr.step(collect_stats=step + 1 in stats_checks)
         outs = [lp.step() for lp in loops]
         if step < sparse_until and step % 97 and pre is None:
             continue
@@ -196,7 +210,8 @@ def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, 
             for i, out in enumerate(outs):
                 np.testing.assert_array_equal(idx[i], out["idx"], err_msg=f"step {step} env {i}")
         if pre is not None:
-            _check_learn(tr, pick, pre, precision, shared, t32)
+            _check_learn(tr, pick, pre, precision, shared, t32,
+                         stats=step + 1 in stats_checks)
             if raw is not None:
                 _check_shared_grad(tr, raw, pre, sampled[1] * A)
             checked += 1
@@ -351,3 +366,87 @@ def test_c2_env_beside_learn_bit_identical_at_size():
         torch.cuda.empty_cache()
     for a, b in zip(res["none"], res["env"]):
         assert torch.equal(a, b)
+
+
+def _bench_c2_schedule():
+    """The schedule bench.py --overlap auto times at C2 (bench.auto_schedule,
+    bench.make_streams): the fused env step of t+1 and the draws beside learn
+    t on a 64-CU masked side stream, the last 64 agents learned on it."""
+    import bench
+    sched, cus, side_learn = bench.auto_schedule(2, 2, 256, False, False, False, None)
+    assert (sched, cus, side_learn) == ("env", 64, 64)
+    work, side = bench.make_streams(torch.device(DEV), cus)
+    return work, dict(overlap=sched, side_stream=side, side_learn=side_learn)
+
+
+def test_c2_bench_schedule_steady_state_wrapped_rings():
+    """C2 (2x2 x 256, bf16, replay 10,000) under the
+    exact schedule bench.py times -- env step beside the learn on 64 masked
+    CUs, agents 960..1023 learned on the side stream -- driven past 10,000
+    steps (wrapped rings, the store in the spare slot, the set-branch
+    sampler).  Sampled replicas {0, 128, 255} vs OracleLoop every 97th step
+    and at every step after the wrap: actions, observations, rewards, replay
+    indices bit-exact.  At learns 3 and 5 after the wrap, agents of both
+    launches (0, 3, 513, 515 on the learn stream; 1020..1023 on the side
+    stream) are checked: device z-score bit-exact, loss vs
+    oracle.learn_mixed (bf16, TOL16), gradient, and (learn 5) the Q
+    statistics of collect_stats (train.py:274-292, dqn_agent.py:29, 59-85)."""
+    cap = 10000
+    work, kw = _bench_c2_schedule()
+    try:
+        with torch.cuda.stream(work):
+            tr = _run_config(2, 2, 256, "bf16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap,
+                             trainer_kw=kw, stats_checks={cap + 5})
+            assert tr.side_learn == 64 and tr.overlap == "env"
+            ring = tr.agent.ring
+            assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
+            del tr
+    finally:
+        torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _run_schedule(kw, steps=420, cap=300, stats_every=7):
+    tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=256, seed=2),
+                 AgentConfig(precision="bf16", replay_buffer_size=cap, seed=2), **kw)
+    losses, stats, obs = [], [], []
+    for t in range(steps):
+        st = tr.step(collect_stats=t % stats_every == 0)
+        if tr.last_loss is not None:
+            losses.append(tr.last_loss.clone())
+            if t % stats_every == 0:
+                stats.append(tr.agent.qstats.clone())
+        obs.append(tr.obs.clone())
+        assert st.loss_launched == (t + 1 >= 128)
+    torch.cuda.synchronize()
+    assert tr.agent.ring.start != 0
+    ag = tr.agent
+    out = dict(losses=torch.stack(losses).cpu(), stats=torch.stack(stats).cpu(),
+               obs=torch.stack(obs).cpu(),
+               **{k: getattr(ag, k).cpu() for k in ("params", "target", "adam_m", "adam_v",
+                                                    "target_h", "np_state", "py_state")},
+               **{"ring_" + k: getattr(ag.ring, k).cpu() for k in ("s", "n", "a", "r", "d")})
+    del tr
+    torch.cuda.empty_cache()
+    return out
+
+
+@pytest.mark.parametrize("fenced", [False, True])
+def test_c2_bench_schedule_bit_identical_to_one_stream(fenced):
+    """C2 size, replay 300 (wrapped by step 300), 420
+    steps: the bench's C2 schedule (masked streams, side learn of 64 agents,
+    ordering-only learn events; fenced=True: default events, bench
+    --fenced-events) gives losses, Q statistics (collect_stats every 7th
+    step), observations, weights, Adam slots, target shadows,
+    random streams and rings bit-identical to the one-stream order."""
+    ref = _run_schedule({})
+    work, kw = _bench_c2_schedule()
+    kw["war_events"] = not fenced
+    try:
+        with torch.cuda.stream(work):
+            got = _run_schedule(kw)
+    finally:
+        torch.cuda.synchronize()
+    assert ref.keys() == got.keys()
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
