@@ -181,12 +181,15 @@ STREAM_PROBE_REPS = 5
 def stream_probe(stream, n_bytes=STREAM_PROBE_BYTES, reps=STREAM_PROBE_REPS):
     """This box's HBM streaming rate, in this process, on the learn's stream
     (dmdqn_stream_probe, csrc/probe.hip): a float4 copy of n_bytes (read n,
-    write n) and a triad (read 2n, write n, about the learn's own read:write
-    mix), each launched reps times behind one untimed launch and timed with
-    fence-free HIP events.  Returns {"copy_gbs", "triad_gbs"} (median of the
-    reps, algorithmic bytes / launch time) -- boxes of the pool differ by up
-    to ~15 % on one binary, so the learn's fraction of THIS figure separates
-    the box from the code."""
+    write n), a triad (read 2n, write n: about the learn's own read:write
+    mix) and a read of n, each with plain and with non-temporal accesses,
+    plus the runtime's device-to-device copy (torch copy_, hipMemcpyAsync).
+    Each is launched reps times behind one untimed launch and timed with
+    fence-free HIP events; rates are algorithmic bytes / median launch time.
+    Returns {"copy_gbs", "triad_gbs", "read_gbs"} (the best variant of each)
+    and "modes" (every variant) -- boxes of the pool differ by up to ~15 % on
+    one binary, so the learn's fraction of THIS box's rate separates the box
+    from the code."""
     import ctypes as C
 
     import torch
@@ -194,24 +197,38 @@ def stream_probe(stream, n_bytes=STREAM_PROBE_BYTES, reps=STREAM_PROBE_REPS):
     dev = stream.device
     src = torch.empty(2 * n_bytes // 4, dtype=torch.float32, device=dev)
     dst = torch.empty(n_bytes // 4, dtype=torch.float32, device=dev)
-    src.fill_(1.0)
-    out = {}
-    for mode, name, moved in ((0, "copy_gbs", 2 * n_bytes), (1, "triad_gbs", 3 * n_bytes)):
+    with torch.cuda.stream(stream):
+        src.fill_(1.0)
+    modes = {}
+
+    def timed(name, moved, launch):
+        launch()
         ms = []
-        args = (C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), C.c_size_t(n_bytes), mode,
-                C.c_void_p(stream.cuda_stream))
-        call("dmdqn_stream_probe", *args)
         for _ in range(reps):
             e0, e1 = TimingEvent(), TimingEvent()
             e0.record(stream)
-            call("dmdqn_stream_probe", *args)
+            launch()
             e1.record(stream)
             e1.synchronize()
             ms.append(e0.elapsed_time(e1))
-        out[name] = round(moved / (float(np.median(ms)) / 1e3) / 1e9, 1)
+        modes[name] = round(moved / (float(np.median(ms)) / 1e3) / 1e9, 1)
+
+    for mode, name, moved in ((0, "copy", 2 * n_bytes), (1, "triad", 3 * n_bytes),
+                              (2, "read", n_bytes), (3, "copy_nt", 2 * n_bytes),
+                              (4, "triad_nt", 3 * n_bytes), (5, "read_nt", n_bytes)):
+        args = (C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), C.c_size_t(n_bytes), mode,
+                C.c_void_p(stream.cuda_stream))
+        timed(name, moved, lambda: call("dmdqn_stream_probe", *args))
+
+    def runtime_copy():
+        with torch.cuda.stream(stream):
+            dst.copy_(src[:n_bytes // 4])
+    timed("copy_runtime", 2 * n_bytes, runtime_copy)
     del src, dst
     torch.cuda.empty_cache()
-    return out
+    return {"copy_gbs": max(modes["copy"], modes["copy_nt"], modes["copy_runtime"]),
+            "triad_gbs": max(modes["triad"], modes["triad_nt"]),
+            "read_gbs": max(modes["read"], modes["read_nt"]), "modes": modes}
 
 
 def _step_roofline(value, K, vbar, A, P, shared, NA):
@@ -560,11 +577,15 @@ def main():
             # the same process's HBM streaming rate on this box (stream_probe)
             hbm_roof.update({
                 "copy_gbs": probe["copy_gbs"], "triad_gbs": probe["triad_gbs"],
+                "read_gbs": probe["read_gbs"],
                 "frac_of_copy": round(achieved / probe["copy_gbs"], 4),
                 "frac_of_triad": round(achieved / probe["triad_gbs"], 4),
-                "probe": (f"dmdqn_stream_probe after the timed region, learn stream: float4 copy "
-                          f"of {STREAM_PROBE_BYTES >> 30} GiB (read + write) and triad (2 reads + "
-                          f"1 write), median of {STREAM_PROBE_REPS} launches")})
+                "probe_modes_gbs": probe["modes"],
+                "probe": (f"dmdqn_stream_probe after the timed region, learn stream, "
+                          f"{STREAM_PROBE_BYTES >> 30} GiB: float4 copy (read + write), triad "
+                          f"(2 reads + 1 write), read; plain and non-temporal; plus the "
+                          f"runtime's D2D copy; best of each, median of {STREAM_PROBE_REPS} "
+                          "launches")})
         flop = (NA if args.shared else na_timed) * LEARN_FLOP_PER_AGENT
         mfma_roof = {
             "kernel": ("k_shared_next + k_shared_grad + k_reduce_slabs + k_adam" if args.shared

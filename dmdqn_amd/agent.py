@@ -247,7 +247,7 @@ class AgentConfig:
 class BatchedDQN:
     """E*A independent DQN agents (agent index = env * A + junction)."""
 
-    OUT_BUFS = 3  # rotating loss / qstats buffers (see __init__)
+    OUT_BUFS = 3  # rotating per-step output buffers: loss, qstats, actions, idx (see __init__)
 
     def __init__(self, num_envs, n_agents, cfg: AgentConfig = None, device="cuda",
                  env_seeds=None, init_weights=None, streams=None):
@@ -318,10 +318,14 @@ class BatchedDQN:
         else:
             self.np_state = K.seed_streams(seeds, "np", dev)
             self.py_state = K.seed_streams(seeds, "py", dev)
-        # two index buffers: presample() may draw the next learn's batch (on
-        # another stream) while the current learn still reads its own
+        # rotating index buffers: presample() may draw the next learn's batch
+        # (on another stream) while the current learn still reads its own, and
+        # a caller's read of step t's indices on its stream (queued behind
+        # learn t) must not meet the draws of step t+2 (the side stream of
+        # trainer overlap "env" waits only for learn t): OUT_BUFS of them
         self._idx_bufs = [torch.empty((NA, cfg.batch_size), dtype=torch.int32, device=dev)
-                          for _ in range(2)]
+                          for _ in range(self.OUT_BUFS)]
+        self._idx_i = 0
         self.idx = self._idx_bufs[0]
         self._presampled = None  # (n, buffer) drawn ahead by presample()
         # per-learn outputs rotate over OUT_BUFS buffers (learn k writes buffer
@@ -335,10 +339,13 @@ class BatchedDQN:
         self._qstats_bufs = [torch.zeros((NA, 6), dtype=torch.float32, device=dev)
                              for _ in range(self.OUT_BUFS)]
         self.loss, self.qstats = self._loss_bufs[0], self._qstats_bufs[0]
-        # alternating action buffers: a caller may still read step t's actions on
-        # its stream while the trainer's side stream writes step t+1's
+        # rotating action buffers: a caller may still read step t's actions on
+        # its stream while the trainer's side stream writes steps t+1 and t+2
+        # (overlap "env": the side stream waits only for learn t, before which
+        # the caller's read of step t is queued) -- OUT_BUFS of them
         self._act_bufs = [torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
-                          for _ in range(2)]
+                          for _ in range(self.OUT_BUFS)]
+        self._act_i = 0
         self.actions = self._act_bufs[0]
         self.greedy = torch.empty((num_envs, n_agents), dtype=torch.int32, device=dev)
         self._done_flags = [torch.full((NA,), v, dtype=torch.uint8, device=dev) for v in (0, 1)]
@@ -400,7 +407,8 @@ class BatchedDQN:
                                obs.reshape(self.NA, D_IN).contiguous(), self.greedy, None,
                                self.shared)
             greedy = self.greedy
-        self.actions = self._act_bufs[1] if self.actions is self._act_bufs[0] else self._act_bufs[0]
+        self._act_i = (self._act_i + 1) % self.OUT_BUFS
+        self.actions = self._act_bufs[self._act_i]
         return eps, greedy, self.actions
 
     def remembered(self):
@@ -541,7 +549,8 @@ class BatchedDQN:
             return False
         if self._presampled is not None:
             raise RuntimeError("presample called twice before a learn")
-        buf = self._idx_bufs[1] if self.idx is self._idx_bufs[0] else self._idx_bufs[0]
+        self._idx_i = (self._idx_i + 1) % self.OUT_BUFS
+        buf = self._idx_bufs[self._idx_i]
         K.replay_sample(self.py_state, self.A, n, self.cfg.batch_size, out=buf)
         self._presampled = (n, buf)
         return True

@@ -7,7 +7,7 @@
 //                   s' rows, target and online forwards of S', first-max
 //                   argmax, y = r^ + (gamma (1 - d)) Q_t(S')[a*] (:342-347);
 //                   writes y and the batch actions.  Both nets in LDS.
-//   k_shared_grad3  per agent: X(S), online forward, MSE / Huber dL/dQ, and
+//   k_shared_grad4  per agent: X(S), online forward, MSE / Huber dL/dQ, and
 //                   the backward; the weight gradients of all the agents a
 //                   workgroup walks accumulate in registers and are written
 //                   once per workgroup as a partial slab (k_reduce_slabs,
@@ -475,86 +475,13 @@ __device__ __forceinline__ void row_loss(int kind, float diff, float &term, floa
     }
 }
 
-// ---------------------------------------------------------------- pass 2, v3: neuron-owning
-// Four waves (one per SIMD, up to 512 VGPRs each); wave w owns layer-1 and
-// layer-2 neurons 32w .. 32w+31 (two 16-neuron tiles) for ALL 128 rows of an
-// agent, and keeps its slice of the weights -- W1^T, W2^T (forward), W2
-// (dH1), W3 -- in registers for the whole launch, so every MFMA streams only
-// an activation fragment from LDS, shared by the wave's two neuron tiles, and
-// each K-step issues 16 independent MFMAs (eight 16-row tiles x two neuron
-// tiles).  Layers exchange activations through LDS images:
-//   L1  Z1^T = W1^T X^T      (X image)            -> H1 own (regs) + H1 image
-//   L2  Z2^T = W2^T H1^T     (H1 image, all j)    -> H2 own (regs) + H2 image (own columns)
-//   L3  partial Q over own k (H2 regs, kperm)     -> Q partials [4 waves]
-//   loss (wave w: rows 32w..32w+31)                -> dq, act, DQ image
-//   dW3 (H2 image own, DQ) ; dZ2 own (regs)       -> dZ2 image
-//   dH1 = dZ2 W2^T (dZ2 image, all k) -> dZ1 own   -> dZ1 image (own columns, over H2's)
-//   dW2 (H1 image all j, dZ2 own) ; dW1 (X image, dZ1 own)
-// Five barriers per agent; the next agent's X rows are loaded during this
-// agent's layers and staged into the other X buffer behind the loss.
-namespace g3 {
+// ---------------------------------------------------------------- pass 2: shared helpers
+// (The round-3 neuron-owning gradient pass, k_shared_grad3, was an A/B
+// template here until round 4; it lives on in git history -- rebuild it for a
+// same-box A/B with tools/build_rev.py 2d71bef <name> -DSH_GRAD=3.)
+namespace gx {
 constexpr int X_BYTES = B_ * DP * 2;             // [128][96] f16
 constexpr int IMG = B_ * H * 2;                  // [128][128] f16
-constexpr int OFF_X = 0;                         // two X buffers
-constexpr int OFF_H1 = 2 * X_BYTES;
-constexpr int OFF_Z2 = OFF_H1 + IMG;             // dZ2; Q partials (f32 [waves][128][4]) before it
-constexpr int OFF_H2 = OFF_Z2 + IMG;             // H2 own columns, then dZ1 own columns
-constexpr int OFF_DQ = OFF_H2 + IMG;             // [128][16]
-constexpr int OFF_SC = OFF_DQ + B_ * 16 * 2;     // sdq f32 [128], sact int [128], sloss [8]
-constexpr int LDS = OFF_SC + B_ * 8 + 32;
-static_assert(LDS <= 160 * 1024, "k_shared_grad3 LDS");
-static_assert(8 * B_ * 16 <= IMG, "Q partials fit the dZ2 image");
-
-// Weights of a wave's NT-tile neuron slice (registers for the launch); the
-// wave's neurons are n(t) = 16 (NT w + t) + (0..15).
-template <int NT>
-struct WSlice {
-    half8 w1[NT][3];   // lane (i, g): W1^T[n(t) + i][32s + 8g + e] (0 past feature 88)
-    half8 w2[NT][4];   // W2^T[n(t) + i][32s + 8g + e]
-    half8 w2b[NT][4];  // W2[n(t) + i][32s + 8g + e]   (= W2^T[k][j])
-    half8 w3;          // lanes i < 4: W3^T[i][k(g, e)], slot e < 4 of tile 0, e >= 4 of tile 1
-    half4v w3k[NT][4]; // W3[n(t) + 4g + e][a = 0..3]  (dZ2 of a row's action)
-    half4v b1[NT], b2[NT], b3;
-};
-
-template <int NT>
-__device__ __forceinline__ void load_slice(const h16 *WH, int w, WSlice<NT> &S) {
-    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const int n0 = 16 * (NT * w + t), j = n0 + i;
-#pragma unroll
-        for (int s = 0; s < 3; s++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const int f = 32 * s + 8 * g + e;
-                S.w1[t][s][e] = f < QN_D ? WH[L::oW1T + qn_w1<H>(j, f)] : (h16)0.0f;
-            }
-#pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const int c = 32 * s + 8 * g + e;
-                S.w2[t][s][e] = WH[L::oW2T + qn_wt(j, c, H)];   // W2^T[k = j-slot][j = c]
-                S.w2b[t][s][e] = WH[L::oW2T + qn_wt(c, j, H)];  // W2^T[k = c][j]
-            }
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int k = n0 + 4 * g + e;
-#pragma unroll
-            for (int a = 0; a < NACT; a++) S.w3k[t][e][a] = WH[L::oW3T + a * H + k];
-            S.b1[t][e] = WH[L::ob1 + k];
-            S.b2[t][e] = WH[L::ob1 + H + k];
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-        const int t = e >> 2, k = 16 * (NT * w + t) + 4 * g + (e & 3);
-        S.w3[e] = (i < NACT && t < NT) ? WH[L::oW3T + i * H + k] : (h16)0.0f;
-    }
-#pragma unroll
-    for (int a = 0; a < NACT; a++) S.b3[a] = WH[L::ob1 + 2 * H + a];
-}
 
 // One agent's X(S) rows: 2 x 48 bytes per row over the workgroup's threads.
 struct XRows {
@@ -602,14 +529,6 @@ __device__ __forceinline__ int pos3(const dmdqn_learn_args &a, int agent, int pa
     return agent < a.NA && part < 2 * B_ ? a.idx[(size_t)agent * B_ + (part >> 1)] : 0;
 }
 
-// v[k] for k in 0..3 without branches (a nested ?: on halves was turned into
-// exec-mask control flow): two 32-bit selects on the packed pairs
-__device__ __forceinline__ h16 pick4(half4v v, int k) {
-    const uint2 u = __builtin_bit_cast(uint2, v);
-    const uint32_t p = (k & 2) ? u.y : u.x;
-    return __builtin_bit_cast(h16, (uint16_t)(p >> (16 * (k & 1))));
-}
-
 __device__ __forceinline__ float pickf4(float q0, float q1, float q2, float q3, int k) {
     // (bit selects on the values: an indexed pick of a float[4] went to scratch)
     const bool b0 = k & 1, b1 = k & 2;
@@ -626,355 +545,14 @@ __device__ __forceinline__ half4v relu4(f32x4 c, half4v b) {
     return __builtin_bit_cast(half4v, __builtin_elementwise_max(__builtin_bit_cast(s4v, z), (s4v)(0)));
 }
 
-// NT neuron tiles per wave, NW = 8 / NT waves (NT = 2: one wave per SIMD,
-// 512 VGPRs; NT = 1: two waves per SIMD, 256 VGPRs each).  RH row tiles per
-// pass of the three row-loop GEMMs (L1, L2, dH1).
-template <bool QSTATS, int NT>
-__global__ void __launch_bounds__(64 * (8 / NT), 1) k_shared_grad3(dmdqn_learn_args a,
-                                                                 const float *y_in,
-                                                                 const uint8_t *act_in,
-                                                                 float *slab) {
-    constexpr int NW = 8 / NT, NTH = 64 * NW, LR = B_ / NW;  // LR loss rows per wave
-    constexpr int RH = 4;
-    __shared__ __attribute__((aligned(16))) char smem[LDS];
-    h16 *H1I = reinterpret_cast<h16 *>(smem + OFF_H1), *Z2I = reinterpret_cast<h16 *>(smem + OFF_Z2);
-    h16 *H2I = reinterpret_cast<h16 *>(smem + OFF_H2), *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
-    float *QP = reinterpret_cast<float *>(smem + OFF_Z2);
-    float *sdq = reinterpret_cast<float *>(smem + OFF_SC);
-    int *sact = reinterpret_cast<int *>(smem + OFF_SC + B_ * 4);
-    float *sloss = reinterpret_cast<float *>(smem + OFF_SC + B_ * 8);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    WSlice<NT> W;
-    load_slice<NT>(reinterpret_cast<const h16 *>(a.params_h), w, W);
-    half8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
-    f32x4 G1[6][NT], G2[8][NT], G3[NT], GB1[NT], GB2[NT], GB3;
-    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-#pragma unroll
-        for (int f = 0; f < 6; f++) G1[f][t] = z4;
-#pragma unroll
-        for (int j = 0; j < 8; j++) G2[j][t] = z4;
-        G3[t] = GB1[t] = GB2[t] = z4;
-    }
-    GB3 = z4;
-    for (int k = threadIdx.x; k < B_ * 16; k += NTH) DQI[k] = (h16)0.0f;
-    // loss rows of this wave (lanes l < LR): row LR w + l
-    const int lrow = LR * w + (l % LR);
-    // per-lane image bases (hsplit), w laundered through an empty asm so the
-    // derived offsets stay per-lane VGPR bases (wave-uniform SGPR offsets spilled):
-    //   row reads [16rt + i][32s + 8g] = bR / bX + 16 LD rt + 256 s
-    //   C-layout writes [16rt + i][n(t) + 4g] = bW[t] + 16 H rt
-    //   transposed reads, columns 16p + 32m + i: trH[p] / trX[p] + 256 m + 2048 s
-    //   (LD 128; X: 16 DP per 16 rows), own columns n(t) + i: trO[t]
-    int wv = w;
-    asm volatile("" : "+v"(wv));
-    const int bR = hoff(i, 8 * g), bX = hoff<DP>(i, 8 * g);
-    const int trH[2] = {hsplit(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    const int trX[2] = {hsplit<DP>(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit<DP>(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    int bW[NT], trO[NT];
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const int c0 = 16 * (NT * wv + t);  // 16-aligned own column block
-        bW[t] = hoff(i, (c0 & 16) + 4 * g) + 256 * (c0 >> 5);
-        trO[t] = hsplit(8 * (g & 1) + (i >> 2), (c0 & 16) + 4 * (i & 3), g >> 1, 0) + 256 * (c0 >> 5);
-    }
-    // X staging: 256 parts (row p >> 1, half p & 1), part = threadIdx.x; with
-    // 512 threads the first 256 stage
-    constexpr int XP = 1;
-    const bool stager = threadIdx.x < 256;
-    int agent = blockIdx.x;
-    {
-        if (agent < a.NA && stager)
-#pragma unroll
-            for (int p = 0; p < XP; p++) {
-                const int part = threadIdx.x + NTH * p;
-                XRows x0;
-                xrows_issue<NTH>(a, agent, pos3(a, agent, part), part, x0);
-                xrows_commit(x0, reinterpret_cast<h16 *>(smem + OFF_X), part);
-            }
-    }
-    int npos[XP];
-#pragma unroll
-    for (int p = 0; p < XP; p++) npos[p] = pos3(a, agent + gridDim.x, threadIdx.x + NTH * p);
-    float yv = 0.0f;
-    int avl = 0;
-    if (agent < a.NA) {
-        yv = y_in[(size_t)agent * B_ + lrow];
-        avl = act_in[(size_t)agent * B_ + lrow];
-    }
-    __syncthreads();
-    int buf = 0;
-    for (; agent < a.NA; agent += gridDim.x, buf ^= 1) {
-        SH_STAMP(agent, 0, threadIdx.x);
-        const h16 *X = reinterpret_cast<const h16 *>(smem + OFF_X + buf * X_BYTES);
-        // the next agent's X rows and loss inputs, in flight behind L1 .. loss
-        const int nxt = agent + gridDim.x;
-        XRows xn[XP];
-        float yn = 0.0f;
-        int an = 0;
-        if (nxt < a.NA && stager)
-#pragma unroll
-            for (int p = 0; p < XP; p++) xrows_issue<NTH>(a, nxt, npos[p], threadIdx.x + NTH * p, xn[p]);
-        if (nxt < a.NA) {
-            yn = y_in[(size_t)nxt * B_ + lrow];
-            an = act_in[(size_t)nxt * B_ + lrow];
-        }
-#pragma unroll
-        for (int p = 0; p < XP; p++) npos[p] = pos3(a, nxt + gridDim.x, threadIdx.x + NTH * p);
-        // ---- L1: own neuron tiles, row tiles in passes of RH (H1 / H2 are not
-        // kept in registers: the relu masks of dZ1 / dZ2 are read back from the
-        // images, which frees 32 NT VGPRs)
-#pragma unroll
-        for (int hf = 0; hf < 8 / RH; hf++) {
-            f32x4 c[RH][NT];
-#pragma unroll
-            for (int r = 0; r < RH; r++)
-#pragma unroll
-                for (int t = 0; t < NT; t++) c[r][t] = z4;
-#pragma unroll
-            for (int s = 0; s < 3; s++) {
-                half8 xb[RH];
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    xb[r] = *reinterpret_cast<const half8 *>(X + bX + 16 * DP * (RH * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-#pragma unroll
-                    for (int t = 0; t < NT; t++) c[r][t] = mfma(W.w1[t][s], xb[r], c[r][t]);
-            }
-#pragma unroll
-            for (int r = 0; r < RH; r++)
-#pragma unroll
-                for (int t = 0; t < NT; t++) {
-                    const int rt = RH * hf + r;
-                    *reinterpret_cast<half4v *>(H1I + bW[t] + 16 * H * rt) = relu4(c[r][t], W.b1[t]);
-                }
-        }
-        SH_STAMP(agent, 1, threadIdx.x);
-        __syncthreads();  // B1: H1 image
-        // ---- L2: own tiles ; H2 own -> image ; L3 partial Q -> QP (over the dZ2 image)
-#pragma unroll
-        for (int hf = 0; hf < 8 / RH; hf++) {
-            f32x4 c[RH][NT];
-#pragma unroll
-            for (int r = 0; r < RH; r++)
-#pragma unroll
-                for (int t = 0; t < NT; t++) c[r][t] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 hb[RH];
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    hb[r] = *reinterpret_cast<const half8 *>(H1I + bR + 16 * H * (RH * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-#pragma unroll
-                    for (int t = 0; t < NT; t++) c[r][t] = mfma(W.w2[t][s], hb[r], c[r][t]);
-            }
-#pragma unroll
-            for (int r = 0; r < RH; r++) {
-                const int rt = RH * hf + r;
-                half4v h2[NT];
-#pragma unroll
-                for (int t = 0; t < NT; t++) {
-                    h2[t] = relu4(c[r][t], W.b2[t]);
-                    *reinterpret_cast<half4v *>(H2I + bW[t] + 16 * H * rt) = h2[t];
-                }
-                half8 hq;  // slots e < 4: tile 0, e >= 4: tile 1 (or zero)
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    hq[e] = h2[0][e];
-                    hq[e + 4] = NT > 1 ? h2[NT - 1][e] : (h16)0.0f;
-                }
-                const f32x4 cq = mfma(W.w3, hq, z4);
-                if (g == 0)
-                    *reinterpret_cast<f32x4 *>(QP + (w * B_ + 16 * rt + i) * 4) = cq;
-            }
-        }
-        SH_STAMP(agent, 2, threadIdx.x);
-        __syncthreads();  // B2: Q partials
-        // ---- loss: wave w, rows LR w .. LR w + LR - 1 (lanes l < LR)
-        {
-            float term = 0.0f;
-            if (l < LR) {
-                float q[4];
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    float s = QP[lrow * 4 + e];  // the waves' partials in order
-#pragma unroll
-                    for (int v = 1; v < NW; v++) s += QP[(v * B_ + lrow) * 4 + e];
-                    q[e] = r16(r16(s) + (float)W.b3[e]);
-                }
-                const float qa = pickf4(q[0], q[1], q[2], q[3], avl);
-                float dq;
-                row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
-                dq = r16(dq);
-                sdq[lrow] = dq;
-                sact[lrow] = avl;
-                half4v d;
-#pragma unroll
-                for (int e = 0; e < 4; e++) d[e] = e == avl ? (h16)dq : (h16)0.0f;
-                *reinterpret_cast<half4v *>(DQI + lrow * 16) = d;
-                if (QSTATS) {
-                    float s1 = (q[0] + q[1]) + (q[2] + q[3]);
-                    float s2 = (q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]);
-                    for (int off = LR / 2; off > 0; off >>= 1) {
-                        s1 += __shfl_xor(s1, off);
-                        s2 += __shfl_xor(s2, off);
-                    }
-                    if (l == 0) {
-                        atomicAdd(a.qstats + (size_t)agent * 6 + 0, s1);
-                        atomicAdd(a.qstats + (size_t)agent * 6 + 1, s2);
-                    }
-                }
-            }
-            if (QSTATS)
-#pragma unroll
-                for (int e = 0; e < NACT; e++) {  // every lane takes part in the ballot
-                    const float cnt = (float)__popcll(__ballot(l < LR && avl == e));
-                    if (l == 0) atomicAdd(a.qstats + (size_t)agent * 6 + 2 + e, cnt);
-                }
-            for (int off = LR / 2; off > 0; off >>= 1) term += __shfl_xor(term, off);
-            if (l == 0) sloss[w] = term;
-        }
-        // the next agent's X into the other buffer (last read two agents ago)
-        if (nxt < a.NA && stager)
-#pragma unroll
-            for (int p = 0; p < XP; p++)
-                xrows_commit(xn[p], reinterpret_cast<h16 *>(smem + OFF_X + (buf ^ 1) * X_BYTES),
-                             threadIdx.x + NTH * p);
-        SH_STAMP(agent, 3, threadIdx.x);
-        __syncthreads();  // B3: dq, act, DQ image, loss partials, next X; QP consumed
-        if (threadIdx.x == 0 && a.loss) {
-            float ls = sloss[0];
-            for (int v = 1; v < NW; v++) ls += sloss[v];
-            a.loss[agent] = ls / (float)B_;
-        }
-        // ---- dW3 (own k) and db3 (wave 0) ; dZ2 own -> image
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const half8 dqf = frag_tr(DQI, 16, 32 * s, 0);
-#pragma unroll
-            for (int t = 0; t < NT; t++) G3[t] = mfma(frag_tr_p(H2I + trO[t] + 2 * 16 * H * s), dqf, G3[t]);
-            if (w == 0) GB3 = mfma(ones, dqf, GB3);
-        }
-#pragma unroll
-        for (int rt = 0; rt < 8; rt++) {
-            const int row = 16 * rt + i;
-            const float dqb = sdq[row];
-            const int ab = sact[row];
-#pragma unroll
-            for (int t = 0; t < NT; t++) {
-                half4v o;
-                const half4v hv = *reinterpret_cast<const half4v *>(H2I + bW[t] + 16 * H * rt);
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const h16 w3 = pick4(W.w3k[t][e], ab);
-                    o[e] = hv[e] > (h16)0.0f ? (h16)(dqb * (float)w3) : (h16)0.0f;
-                }
-                *reinterpret_cast<half4v *>(Z2I + bW[t] + 16 * H * rt) = o;
-            }
-        }
-        SH_STAMP(agent, 4, threadIdx.x);
-        __syncthreads();  // B4: dZ2 image
-        // ---- dH1 (own j) -> dZ1 own -> image (over this wave's H2 columns)
-#pragma unroll
-        for (int hf = 0; hf < 8 / RH; hf++) {
-            f32x4 c[RH][NT];
-#pragma unroll
-            for (int r = 0; r < RH; r++)
-#pragma unroll
-                for (int t = 0; t < NT; t++) c[r][t] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 zb[RH];
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    zb[r] = *reinterpret_cast<const half8 *>(Z2I + bR + 16 * H * (RH * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-#pragma unroll
-                    for (int t = 0; t < NT; t++) c[r][t] = mfma(W.w2b[t][s], zb[r], c[r][t]);
-            }
-#pragma unroll
-            for (int r = 0; r < RH; r++)
-#pragma unroll
-                for (int t = 0; t < NT; t++) {
-                    const int rt = RH * hf + r;
-                    half4v o;
-                    const half4v hv = *reinterpret_cast<const half4v *>(H1I + bW[t] + 16 * H * rt);
-#pragma unroll
-                    for (int e = 0; e < 4; e++) o[e] = hv[e] > (h16)0.0f ? (h16)c[r][t][e] : (h16)0.0f;
-                    *reinterpret_cast<half4v *>(H2I + bW[t] + 16 * H * rt) = o;
-                }
-        }
-        SH_STAMP(agent, 5, threadIdx.x);
-        // ---- dW2[j][k own] and db2 ; dW1[f][j own] and db1 (K = rows)
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            half8 bq[NT], bv[NT];
-#pragma unroll
-            for (int t = 0; t < NT; t++) {
-                bq[t] = frag_tr_p(Z2I + trO[t] + 2 * 16 * H * s);
-                bv[t] = frag_tr_p(H2I + trO[t] + 2 * 16 * H * s);
-                GB2[t] = mfma(ones, bq[t], GB2[t]);
-                GB1[t] = mfma(ones, bv[t], GB1[t]);
-            }
-#pragma unroll
-            for (int jt = 0; jt < 8; jt++) {
-                const half8 af = frag_tr_p(H1I + trH[jt & 1] + 256 * (jt >> 1) + 2 * 16 * H * s);
-#pragma unroll
-                for (int t = 0; t < NT; t++) G2[jt][t] = mfma(af, bq[t], G2[jt][t]);
-            }
-#pragma unroll
-            for (int ft = 0; ft < 6; ft++) {
-                const half8 af = frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s);
-#pragma unroll
-                for (int t = 0; t < NT; t++) G1[ft][t] = mfma(af, bv[t], G1[ft][t]);
-            }
-        }
-        yv = yn;
-        avl = an;
-        SH_STAMP(agent, 6, threadIdx.x);
-        __syncthreads();  // B5: the images are rewritten by the next agent
-        SH_STAMP(agent, 7, threadIdx.x);
-    }
-    // partial sums of this workgroup, kernel layout (every index written once)
-    float *G = slab + (size_t)blockIdx.x * L::P;
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        const int n0 = 16 * (NT * w + t), n = n0 + i;  // this lane's neuron (C-tile column)
-        if (i < NACT)  // G3[t]: rows k = n0 + 4g + e, column a = i
-            *reinterpret_cast<float4 *>(G + L::oW3T + i * H + n0 + 4 * g) =
-                make_float4(G3[t][0], G3[t][1], G3[t][2], G3[t][3]);
-#pragma unroll
-        for (int jt = 0; jt < 8; jt++)  // G2[jt][t]: fan-in j = 16jt + 4g + e, fan-out k = n
-            *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(n, 16 * jt + 4 * g, H)) =
-                make_float4(G2[jt][t][0], G2[jt][t][1], G2[jt][t][2], G2[jt][t][3]);
-        if (g == 0) {
-            G[L::ob2 + n] = GB2[t][0];
-            G[L::ob1 + n] = GB1[t][0];
-        }
-#pragma unroll
-        for (int ft = 0; ft < 6; ft++)  // G1[ft][t]: features 16ft + 4g + e, neuron n
-            if (ft < 5 || g < 2)
-                *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(n, 16 * ft + 4 * g)) =
-                    make_float4(G1[ft][t][0], G1[ft][t][1], G1[ft][t][2], G1[ft][t][3]);
-        if (g == 2) G[L::oW1X + n] = G1[5][t][0];  // feature 88
-    }
-    if (w == 0 && g == 0 && i < NACT) G[L::ob3 + i] = GB3[0];
-}
-
-}  // namespace g3
+}  // namespace gx
 
 // ---------------------------------------------------------------- pass 2, v4
-// k_shared_grad3 with the output layer, the loss and dZ2 moved to ROW-owning
-// waves after the H2 image is complete: wave w takes batch rows 16w..16w+15,
+// Neuron-owning waves (round 3's k_shared_grad3: wave w owns layer-1 / layer-2
+// neurons 16w..16w+15 with its W1^T / W2^T / W2 slice in registers for the
+// launch, layers exchanging activations through LDS images), with the output
+// layer, the loss and dZ2 moved to ROW-owning waves after the H2 image is
+// complete: wave w takes batch rows 16w..16w+15,
 // reads their H2 rows once (the B operand of Q^T = W3^T H2^T, four MFMAs over
 // k = 0..127 from a W3^T LDS image), computes Q, the loss and dL/dQ on those
 // rows, then dZ2 = h16(dq W3[k][a]) masked by H2 > 0 for every k of the rows
@@ -987,10 +565,10 @@ __global__ void __launch_bounds__(64 * (8 / NT), 1) k_shared_grad3(dmdqn_learn_a
 //   RQ  rows 16w..: Q, loss, dq ; dZ2 rows  -> DQ image, dZ2 image (rows)
 //   G   dW3 (H2 own^T, DQ) ; dH1 own (dZ2 image) -> dZ1 own (over H2 own) ;
 //       dW2 (H1^T, dZ2 own) ; dW1 (X^T, dZ1 own)
-// Same rounding points as k_shared_grad3 (Keras' mixed policy).
+// Same rounding points as round 3's grad3 (Keras' mixed policy; same gradient bits).
 namespace g4 {
-using g3::X_BYTES;
-using g3::IMG;
+using gx::X_BYTES;
+using gx::IMG;
 constexpr int OFF_X = 0;                          // two X buffers
 constexpr int OFF_H1 = 2 * X_BYTES;
 constexpr int OFF_Z2 = OFF_H1 + IMG;              // dZ2 [128][128], written by rows
@@ -1088,11 +666,11 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
     const bool stager = threadIdx.x < 256;
     int agent = blockIdx.x;
     if (agent < a.NA && stager) {
-        g3::XRows x0;
-        g3::xrows_issue<NTH>(a, agent, g3::pos3(a, agent, threadIdx.x), threadIdx.x, x0);
-        g3::xrows_commit(x0, reinterpret_cast<h16 *>(smem + OFF_X), threadIdx.x);
+        gx::XRows x0;
+        gx::xrows_issue<NTH>(a, agent, gx::pos3(a, agent, threadIdx.x), threadIdx.x, x0);
+        gx::xrows_commit(x0, reinterpret_cast<h16 *>(smem + OFF_X), threadIdx.x);
     }
-    int npos = g3::pos3(a, agent + gridDim.x, threadIdx.x);
+    int npos = gx::pos3(a, agent + gridDim.x, threadIdx.x);
     float yv = 0.0f;
     int avl = 0;
     if (agent < a.NA) {
@@ -1105,15 +683,15 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         SH_STAMP(agent, 0, threadIdx.x);
         const h16 *X = reinterpret_cast<const h16 *>(smem + OFF_X + buf * X_BYTES);
         const int nxt = agent + gridDim.x;
-        g3::XRows xn;
+        gx::XRows xn;
         float yn = 0.0f;
         int an = 0;
-        if (nxt < a.NA && stager) g3::xrows_issue<NTH>(a, nxt, npos, threadIdx.x, xn);
+        if (nxt < a.NA && stager) gx::xrows_issue<NTH>(a, nxt, npos, threadIdx.x, xn);
         if (nxt < a.NA) {
             yn = y_in[(size_t)nxt * B_ + row];
             an = act_in[(size_t)nxt * B_ + row];
         }
-        npos = g3::pos3(a, nxt + gridDim.x, threadIdx.x);
+        npos = gx::pos3(a, nxt + gridDim.x, threadIdx.x);
         // ---- L1: own neuron tile, row tiles in passes of RH -> H1 image
 #pragma unroll
         for (int hf = 0; hf < 8 / RH; hf++) {
@@ -1131,7 +709,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             }
 #pragma unroll
             for (int r = 0; r < RH; r++)
-                *reinterpret_cast<half4v *>(H1I + bW + 16 * H * (RH * hf + r)) = g3::relu4(c[r], W.b1);
+                *reinterpret_cast<half4v *>(H1I + bW + 16 * H * (RH * hf + r)) = gx::relu4(c[r], W.b1);
         }
         SH_STAMP(agent, 1, threadIdx.x);
         __syncthreads();  // B1: H1 image
@@ -1152,7 +730,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             }
 #pragma unroll
             for (int r = 0; r < RH; r++)
-                *reinterpret_cast<half4v *>(H2I + bW + 16 * H * (RH * hf + r)) = g3::relu4(c[r], W.b2);
+                *reinterpret_cast<half4v *>(H2I + bW + 16 * H * (RH * hf + r)) = gx::relu4(c[r], W.b2);
         }
         SH_STAMP(agent, 2, threadIdx.x);
         __syncthreads();  // B2: H2 image
@@ -1170,7 +748,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         float q[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) q[e] = r16(r16(cq[e]) + (float)W.b3[e]);
-        const float qa = g3::pickf4(q[0], q[1], q[2], q[3], avl);
+        const float qa = gx::pickf4(q[0], q[1], q[2], q[3], avl);
         float term, dq;
         row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
         dq = r16(dq);  // dL/dQ in f16 (the gradient of the learn's tf.cast)
@@ -1210,7 +788,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         }
         // the next agent's X into the other buffer (last read two agents ago)
         if (nxt < a.NA && stager)
-            g3::xrows_commit(xn, reinterpret_cast<h16 *>(smem + OFF_X + (buf ^ 1) * X_BYTES),
+            gx::xrows_commit(xn, reinterpret_cast<h16 *>(smem + OFF_X + (buf ^ 1) * X_BYTES),
                              threadIdx.x);
         SH_STAMP(agent, 3, threadIdx.x);
         __syncthreads();  // B3: DQ, dZ2 image, loss partials, next X
@@ -1310,14 +888,7 @@ int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *s
     const int next_blocks = next_wg < n_slabs ? next_wg : n_slabs;
     hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(64 * NEXT_WAVES), 0, s, *a, y, act);
     DMDQN_LAUNCH_CHECK("k_shared_next");
-#ifndef SH_GRAD
-#define SH_GRAD 4  // 3: k_shared_grad3 (A/B builds, tools/build_exp.py -DSH_GRAD=3)
-#endif
-#if SH_GRAD == 3
-    auto k = a->qstats ? g3::k_shared_grad3<true, 1> : g3::k_shared_grad3<false, 1>;
-#else
     auto k = a->qstats ? g4::k_shared_grad4<true> : g4::k_shared_grad4<false>;
-#endif
     hipLaunchKernelGGL(k, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
     DMDQN_LAUNCH_CHECK("k_shared_grad");
     return DMDQN_OK;

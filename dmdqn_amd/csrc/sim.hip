@@ -898,8 +898,13 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         }
     } else if (actions) {
         for (int a = tid; a < A; a += nt) {
-            V.phase[a] = stride * actions[(size_t)blockIdx.x * A + a];
-            V.ts[a] = t0;
+            // a negative action: no setPhase, the junction's program runs on
+            // with its timer (the reference class's skipped actions)
+            const int act = actions[(size_t)blockIdx.x * A + a];
+            if (act >= 0) {
+                V.phase[a] = stride * act;
+                V.ts[a] = t0;
+            }
         }
     }
     __syncthreads();
@@ -1177,8 +1182,9 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         }
     } else {
         for (int a = tid; a < A; a += NT) {
-            s_phase[a] = actions ? stride * actions[(size_t)blockIdx.x * A + a] : G.phase[a];
-            s_ts[a] = actions ? t0 : G.ts[a];
+            const int act = actions ? actions[(size_t)blockIdx.x * A + a] : -1;  // < 0: keep
+            s_phase[a] = act >= 0 ? stride * act : G.phase[a];
+            s_ts[a] = act >= 0 ? t0 : G.ts[a];
         }
     }
     if (S.actuated)

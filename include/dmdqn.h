@@ -52,6 +52,12 @@ extern "C" {
 #define DMDQN_ROWS_F32 1
 
 const char *dmdqn_last_error(void);
+/* ABI version.  2 (round 4/5): the replay ring arguments `cap` of the learn,
+ * gather and store entry points are the PHYSICAL slot count of the ring -- a
+ * deque of maxlen N lives in N + 1 slots (position p at slot (start + p) %
+ * (N + 1), the next store in the one slot no position maps to), so a caller
+ * passes N + 1; dmdqn_learn_shared_grad requires `work`; dmdqn_sim_step takes
+ * action < 0 as "no setPhase".  1: cap = maxlen, work optional. */
 int dmdqn_version(void);
 
 /* Debug-bounds build (libdmdqn_hip_debug.so, -DDMDQN_DEBUG_BOUNDS): kernels
@@ -115,8 +121,10 @@ int dmdqn_event_destroy(void *event);
  * fraction of what this box streams in the same process.  mode 0: copy,
  * dst[i] = src[i] over n_bytes (n_bytes read, n_bytes written); mode 1:
  * triad, dst[i] = src[i] + src[n_bytes/4 + i] in f32 (src holds 2 * n_bytes:
- * 2 n_bytes read, n_bytes written).  16-B aligned, n_bytes a multiple of 16.
- * No reference counterpart. */
+ * 2 n_bytes read, n_bytes written); mode 2: read, n_bytes of src read, one
+ * 16-B sum per thread written to dst (8 MiB per 256 CUs); modes 3..5: the
+ * same with non-temporal loads and stores.  16-B aligned, n_bytes a multiple
+ * of 16.  No reference counterpart. */
 int dmdqn_stream_probe(void *dst, const void *src, size_t n_bytes, int mode, void *stream);
 
 /* ------------------------------------------------------------------ streams
@@ -266,7 +274,10 @@ int dmdqn_sim_reset_envs(const dmdqn_sim *sim, const uint8_t *mask, void *stream
 
 /* One RL step for every env (train.py:225-236): if actions != NULL set
  * phase = action_stride*action (ACTION_MAP {0:0,1:3,2:6,3:9}) with the phase
- * timer restarted at t0, then run K one-second substeps from time t0 (with
+ * timer restarted at t0 -- except where action < 0: no setPhase for that
+ * junction, its program runs on with its timer (the reference class skips
+ * unmapped actions and an unchanged phase, sumo_env.py:491-530) -- then run K
+ * one-second substeps from time t0 (with
  * sim->t_env: t0 = t_env[e] per replica, and t_env[e] += K).
  * With sim->actuated, phase 0 is SUMO's actuated phase (grid_3x3.net.xml:894):
  * it ends once it has run minDur = 5 s and no vehicle has been over a detector
@@ -335,6 +346,8 @@ int dmdqn_env_step(const dmdqn_sim *sim, const dmdqn_idm *idm, const dmdqn_env_f
 #define DMDQN_LOSS_MSE 0
 #define DMDQN_LOSS_HUBER 1
 
+/* cap: the ring's physical slot count (replay_buffer_size + 1, see
+ * dmdqn_version); start: the slot of deque position 0. */
 typedef struct dmdqn_learn_args {
     int32_t NA, cap, start, batch, hidden, precision, sync_target, P;
     const int8_t *ring_s, *ring_n;   /* [NA][cap][DMDQN_ROW_BYTES]; the 16-bit

@@ -512,8 +512,9 @@ static void substep(orc_env *g, int t) {
 
 void orc_env_step(orc_env *g, const int32_t *actions, int stride, int t0, int K, int max_time,
                   int32_t *halt, int32_t *phase, int32_t *tspent, uint8_t *done) {
-    if (actions)
-        for (int a = 0; a < g->A; a++) { g->phase[a] = stride * actions[a]; g->ts[a] = t0; }
+    if (actions)  /* a negative action: no setPhase (the program runs on, timer kept) */
+        for (int a = 0; a < g->A; a++)
+            if (actions[a] >= 0) { g->phase[a] = stride * actions[a]; g->ts[a] = t0; }
     for (int k = 0; k < K; k++) substep(g, t0 + k);
     int t = t0 + K, run = 0, pend = 0;
     for (int l = 0; l < g->NL; l++) {

@@ -15,13 +15,22 @@ What runs underneath is the train.py hot path this build replaces
 order_lanes.build_state_vector and train.py's reward (0.3 local + 0.7 global
 from the PRE-step states, train.py:159-165, :254) -- not sumo_env.py's 74-dim
 variant and its _calculate_rewards, which no training script of the reference
-calls.  Differences a caller can see, all stated here:
-  * setPhase is applied every step for every junction (train.py:225-226 --
-    the phase timer restarts); the reference class skips the call when the
-    junction is already in the requested phase (:519-520);
-  * every junction of the grid must be controlled (the simulator sets every
-    signal each step); ids that are not junctions of the network are dropped,
-    as the reference drops ids without a traffic light (:116-123);
+calls.  Actions follow the class's _apply_actions (:491-530): an id that is
+not a controlled junction, an action with no entry in that junction's
+action_phases, or a phase string the signal program does not have (the
+reference prints a warning) is skipped; setPhase is skipped too when the
+junction is already in the requested phase, so its timer runs on; a junction
+without an action this step keeps running its program.  Without
+"action_phases" a junction's map is empty (:113-117): every action is skipped
+and get_action_size() is 0, as in the reference.  Junctions not listed in
+controlled_intersections run their programs untouched and are absent from the
+observation and reward dicts.  Differences a caller can see, all stated here:
+  * action_phases entries may also be phase INDICES (an extension; the
+    reference takes state strings, and its `if sumo_phase_string:` would skip
+    an index 0 -- here 0 selects phase 0);
+  * ids that are not junctions of the network are dropped, as the reference
+    drops ids without a traffic light (:116-123); an empty result raises
+    ValueError (the reference exits);
   * a step always runs step_duration whole 1-second substeps (step_duration
     must be a whole number of seconds); the reference stops the substep loop
     at the second the network empties (:456-463), so simulation_time on that
@@ -52,17 +61,19 @@ TL_PROGRAM_STATES = [
     "GrrrrrGGGGrgGrrrrrGGGGrg", "yyyyyyyyyyyyyyyyyyyyyyyy", "rrrrrrrrrrrrrrrrrrrrrrrr",
     "GrrrrrGrryGgGrrrrrGrryGg", "yyyyyyyyyyyyyyyyyyyyyyyy", "rrrrrrrrrrrrrrrrrrrrrrrr",
 ]
-# train.py:57 ACTION_MAP, the action -> phase map when action_phases is absent
-DEFAULT_ACTION_PHASES = {0: 0, 1: 3, 2: 6, 3: 9}
+# train.py:57 ACTION_MAP as SUMO state strings: the action_phases of a caller
+# that wants train.py's four green phases (0, 3, 6, 9)
+TRAIN_PY_ACTION_PHASES = {a: TL_PROGRAM_STATES[3 * a] for a in range(4)}
 DEFAULT_MAX_LANES_PER_DIRECTION = 3
+NO_SET_PHASE = -1  # dmdqn_sim_step: no setPhase for this junction this step
 
 
 def _phase_index(phase):
-    """A phase given as a program state string or an index -> the index."""
+    """A phase given as a program state string or an index -> the index of
+    the FIRST program phase with that string (:510-514); -1 when the program
+    has no such phase (the reference warns and skips the action, :519-523)."""
     if isinstance(phase, str):
-        if phase not in TL_PROGRAM_STATES:
-            raise ValueError(f"phase state {phase!r} is not in the signal program")
-        return TL_PROGRAM_STATES.index(phase)
+        return TL_PROGRAM_STATES.index(phase) if phase in TL_PROGRAM_STATES else -1
     p = int(phase)
     if not 0 <= p < len(TL_PROGRAM_STATES):
         raise ValueError(f"phase index {p} outside the 12-phase program")
@@ -110,21 +121,21 @@ class SumoTrafficEnvironment:
                             max_sim_time=int(np.ceil(float(max_simulation_time))),
                             scenario=sumo_cfg_path, action_stride=1)
         self._build()
-        ids = self.env.get_controlled_intersection_ids()
+        ids = self.env.get_controlled_intersection_ids()  # every signal of the grid
         self.controlled_intersections_config = {c["id"]: c for c in controlled_intersections}
         kept = [j for j in self.controlled_intersections_config if j in ids]
-        missing = [j for j in ids if j not in kept]
-        if missing:
-            raise ValueError(f"every junction of the grid must be controlled; missing {missing}")
+        if not kept:
+            raise ValueError("None of the provided 'controlled_intersections' IDs correspond to "
+                             "traffic lights found in the network.")
         self.controlled_intersection_ids = kept
         self.traffic_light_ids = {j: j for j in kept}
-        # action -> phase index per junction (state strings as _apply_actions)
+        # :113-117: the action -> phase map per junction, empty without "action_phases"
         self.action_to_sumo_phase = {
-            j: dict(self.controlled_intersections_config[j].get("action_phases")
-                    or DEFAULT_ACTION_PHASES) for j in kept}
-        self._phase_of = {j: {int(a): _phase_index(p) for a, p in m.items()}
+            j: self.controlled_intersections_config[j].get("action_phases", {}) for j in kept}
+        self._phase_of = {j: {a: _phase_index(p) for a, p in m.items() if isinstance(p, int) or p}
                           for j, m in self.action_to_sumo_phase.items()}
         self._col = [ids.index(j) for j in kept]  # obs row of each controlled id
+        self._signal = {j: ids.index(j) for j in kept}  # signal index in the simulator
         self.state_vector_size = K.OBS_DIM
         self.current_time = 0.0
         self._started = False
@@ -160,12 +171,7 @@ class SumoTrafficEnvironment:
         info), the observation and reward of train.py:238-270."""
         if not self._started:
             raise RuntimeError("call reset() first (the simulation is not running)")
-        ph = np.zeros((1, self.env.A), np.int32)
-        for j, c in zip(self.controlled_intersection_ids, self._col):
-            a = int(actions[j])
-            if a not in self._phase_of[j]:
-                raise ValueError(f"action {a} of {j} has no phase in action_phases")
-            ph[0, c] = self._phase_of[j][a]
+        ph = self._apply_actions(actions)
         obs, rew, done, info = self.env.step(torch.from_numpy(ph).to(self.env.device),
                                              restart=False)
         self.current_time = float(info["simulation_time"])
@@ -175,6 +181,28 @@ class SumoTrafficEnvironment:
         r = rew[0].cpu().numpy()
         rewards = {j: float(r[c]) for j, c in zip(self.controlled_intersection_ids, self._col)}
         return self._dict(obs[0].cpu().numpy()), rewards, bool(done), out
+
+    def _apply_actions(self, actions):
+        """:491-530 -> the simulator's per-signal phase requests [1, A]: the
+        phase index to set, or NO_SET_PHASE (unknown id, unmapped action,
+        phase string not in the program, or already in that phase)."""
+        ph = np.full((1, self.env.A), NO_SET_PHASE, np.int32)
+        current = None
+        for j, a in actions.items():
+            if j not in self.traffic_light_ids:
+                continue
+            p = self._phase_of[j].get(a, NO_SET_PHASE)
+            if p == NO_SET_PHASE:
+                s = self.action_to_sumo_phase[j].get(a)
+                if s:
+                    print(f"Warning: SUMO phase string '{s}' (Action {a}) not found for TL {j}.")
+                continue
+            if current is None:  # traci.trafficlight.getPhase (:517), one read per step
+                current = self.env.phase[0].cpu().numpy()
+            c = self._signal[j]
+            if int(current[c]) != p:
+                ph[0, c] = p
+        return ph
 
     def _dict(self, obs):
         return {j: np.asarray(obs[c], np.float32)

@@ -19,10 +19,11 @@ def test_phase_strings_map_to_the_first_matching_phase():
     assert S._phase_index("yyyyyyyyyyyyyyyyyyyyyyyy") == 1
     assert S._phase_index("rrrrrrrrrrrrrrrrrrrrrrrr") == 2
     assert S._phase_index(9) == 9
-    with pytest.raises(ValueError):
-        S._phase_index("GGGGGGGGGGGGGGGGGGGGGGGG")
+    # a string the program does not have: the reference warns and skips (:519-523)
+    assert S._phase_index("GGGGGGGGGGGGGGGGGGGGGGGG") == S.NO_SET_PHASE
     with pytest.raises(ValueError):
         S._phase_index(12)
+    assert [S._phase_index(p) for p in S.TRAIN_PY_ACTION_PHASES.values()] == [0, 3, 6, 9]
 
 
 @pytest.mark.parametrize("kw,exc", [
