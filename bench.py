@@ -274,13 +274,19 @@ def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split, side
     return "env", cus, side_learn
 
 
-def make_streams(dev, cu_split=None, cu_stride=False):
+def make_streams(dev, cu_split=None, cu_stride=False, learn_priority=False):
     """(learn stream, side stream or None) of bench.py: with cu_split, two
     CU-masked HIP streams (the side one on cu_split CUs: 0..k-1, or every
     n_cu/k-th CU with cu_stride; the learn stream on the rest), else one
-    dedicated stream (events recorded on the legacy null stream block the host)."""
+    dedicated stream (events recorded on the legacy null stream block the
+    host) -- with learn_priority, the learn stream at the highest stream
+    priority and a side stream at the default one (the side stream's blocks
+    then fill what the learn's dispatch leaves, its tail)."""
     import torch
     if not cu_split:
+        if learn_priority:
+            lo, hi = torch.cuda.Stream.priority_range()
+            return torch.cuda.Stream(dev, priority=hi), torch.cuda.Stream(dev, priority=lo)
         return torch.cuda.Stream(dev), None
     from dmdqn_amd._lib import cu_masked_stream
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -340,6 +346,9 @@ def main():
     ap.add_argument("--fenced-events", action="store_true",
                     help="overlap env: order the side stream after the learns with default "
                          "(system-scope) events instead of ordering-only ones (A/B)")
+    ap.add_argument("--learn-priority", action="store_true",
+                    help="with --overlap sample/full/env and no --cu-split: the learn stream at "
+                         "the highest HIP stream priority, the side stream at the lowest")
     ap.add_argument("--no-stream-probe", action="store_true",
                     help="skip the HBM streaming probe after the timed region (roofline."
                          "copy_gbs / frac_of_copy)")
@@ -380,7 +389,9 @@ def main():
             args.cu_split, args.side_learn)
     if args.side_learn is None:
         args.side_learn = 0
-    work, side = make_streams(dev, args.cu_split, args.cu_stride)
+    if args.learn_priority and args.cu_split:
+        ap.error("--learn-priority: CU-masked streams have no priority")
+    work, side = make_streams(dev, args.cu_split, args.cu_stride, args.learn_priority)
     torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
@@ -543,6 +554,7 @@ def main():
                                if tr.fused else "")
                             + (f"; side stream on {args.cu_split} CUs"
                                + (" (strided)" if args.cu_stride else "") if args.cu_split else "")
+                            + ("; learn stream at high priority" if args.learn_priority else "")
                             + (f"; the learn of {args.side_learn} agents on the side stream"
                                if args.side_learn else ""),
             },

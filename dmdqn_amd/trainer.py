@@ -286,10 +286,11 @@ class Trainer:
         """The "env" schedule's invariant for ordering-only learn events: no
         greedy act (its forward reads the learn stream's weights) and the side
         learn's agent range [NA - side_learn, NA) disjoint from the learn
-        stream's [0, NA - side_learn)."""
+        stream's [0, NA - side_learn) (no side learn for the shared net, whose
+        one learn reads every agent)."""
         ag = self.agent
         return (ag.current_epsilon() >= 1.0 and not ag.cfg.count_env_steps
-                and not ag.shared and 0 <= self.side_learn < ag.NA)
+                and 0 <= self.side_learn < ag.NA and not (ag.shared and self.side_learn))
 
     def _after_step(self, done, next_obs, info, side=None, main=None):
         """Counters and the observation the next act sees (train.py:188-209).
