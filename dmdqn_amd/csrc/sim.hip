@@ -1054,17 +1054,41 @@ __device__ __forceinline__ void vpop(float (&V_)[RCAP], VColL &c) {
     }
 }
 
-// append a vehicle at the back of a register lane (constant indices only)
+// Route words (16 bits, sim.hpp) of a register lane, two per VGPR: vehicle i
+// in half i & 1 of D2_[i >> 1].  Packing halves the array (12 VGPRs instead of
+// 24): the 1024-thread kernel runs at 128 VGPRs per thread and spilled.
+constexpr int RCAP2 = RCAP / 2;
+static_assert(RCAP % 2 == 0, "route words in pairs");
+__device__ __forceinline__ int dget(const uint32_t (&D2_)[RCAP2], int i) {
+    return (int)((D2_[i >> 1] >> (16 * (i & 1))) & 0xffffu);
+}
+__device__ __forceinline__ void dset(uint32_t (&D2_)[RCAP2], int i, int w) {
+    const uint32_t sh = 16 * (i & 1), x = D2_[i >> 1];
+    D2_[i >> 1] = (x & ~(0xffffu << sh)) | ((uint32_t)w << sh);
+}
+// the front leaves: every word moves down one position (a funnel shift per pair)
+__device__ __forceinline__ void dpop(uint32_t (&D2_)[RCAP2]) {
+#pragma unroll
+    for (int p = 0; p < RCAP2 - 1; p++) D2_[p] = __builtin_amdgcn_alignbit(D2_[p + 1], D2_[p], 16);
+    D2_[RCAP2 - 1] >>= 16;
+}
+
+// append a vehicle at the back of a register lane (constant indices only; the
+// words past the lane's count are never read)
 template <bool kL>
 __device__ __forceinline__ void lane_append(float (&X_)[RCAP], float (&V_)[RCAP], const VColL &c,
-                                            int (&D_)[RCAP], int &n, float &lx, float &lv, float xv,
-                                            float vv, int dv) {
+                                            uint32_t (&D2_)[RCAP2], int &n, float &lx, float &lv,
+                                            float xv, float vv, int dv) {
 #pragma unroll
     for (int i = 0; i < RCAP; i++) {
         const bool here = i == n;
         X_[i] = here ? xv : X_[i];
         if constexpr (!kL) V_[i] = here ? vv : V_[i];
-        D_[i] = here ? dv : D_[i];
+    }
+#pragma unroll
+    for (int p = 0; p < RCAP2; p++) {
+        D2_[p] = 2 * p == n ? (uint32_t)dv : D2_[p];
+        D2_[p] = 2 * p + 1 == n ? (D2_[p] & 0xffffu) | ((uint32_t)dv << 16) : D2_[p];
     }
     if constexpr (kL) c.at(n) = vv;
     n++;
@@ -1120,12 +1144,12 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
 
     // ---- this thread's lane (registers) and origin queue
     const bool own = tid < NL;
-    const int l = tid, e = tid / 3, kf = tid - 3 * (tid / 3);
+    const int l = tid;  // (e = l / 3 and kf = l % 3 are derived inside the substep loop)
     constexpr bool kL = NT > 512;  // speeds in the LDS column (VColL)
     float X_[RCAP], V_[RCAP];
     VColL Vc{nullptr, 0, NT};
     if constexpr (kL) Vc.p = reinterpret_cast<float *>(dyn + reg_vcol_off(S.R, S.C, kFuse, LS)) + tid;
-    int D_[RCAP];
+    uint32_t D2_[RCAP2];
     int n = 0;
     float lx = 0.0f, lv = 0.0f;
     if (own) {
@@ -1142,7 +1166,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 if (sl >= cap) sl -= cap;
                 X_[i] = G.x[base + sl];
                 vset<kL>(V_, Vc, i, G.v[base + sl]);
-                D_[i] = G.dst[base + sl];
+                dset(D2_, i, G.dst[base + sl]);
             }
         }
         if (n > 0) {
@@ -1198,7 +1222,9 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         // held across the substeps (this kernel is at its register limit)
         if (tid < A) reinterpret_cast<int32_t *>(dyn + fl.mt_off)[tid] = my_act;
     }
-    const float len = own ? lane_length(T, e) : 0.0f;
+    // the lane's length: re-read from the topology table each substep (an LDS
+    // read) rather than held in a VGPR across the substeps (register limit)
+#define LANE_LEN() (own ? lane_length(T, e) : 0.0f)
 
     // TL at time t: natural phase advance (and the actuated gap-out of phase 0)
     auto tl_pass = [&](int t) {
@@ -1228,7 +1254,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             const int d_ = s_ins[l];                                    \
             if (d_ != -1) {                                             \
                 DMDQN_DBG(n < RCAP, DBG_SIM_RING);                      \
-                lane_append<kL>(X_, V_, Vc, D_, n, lx, lv, P.length, 0.0f, d_); \
+                lane_append<kL>(X_, V_, Vc, D2_, n, lx, lv, P.length, 0.0f, d_); \
                 s_ins[l] = -1;                                          \
             }                                                           \
         }                                                               \
@@ -1242,13 +1268,18 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
 #endif
     for (int k = 0; k < K; k++) {
         const int t = t0 + k;
+        // the lane ids again from an opaque thread id: expressions of them are
+        // then computed in the loop instead of hoisted above it and held --
+        // the 1024-thread fused kernel spilled 16 such invariants to scratch
+        const int l = opaque_tid(), e = l / 3, kf = l - 3 * (l / 3);
+        const float len = LANE_LEN();
         TAKE_INSERT();
         // ---- A: the front vehicle decides (route, target lane, IDM, request)
         int rq = -1;
         float fx = 0.0f, fv = 0.0f;
         if (own && n > 0) {
             const float x0 = X_[0], v0 = vget<kL>(V_, Vc, 0);
-            const int d0 = D_[0];
+            const int d0 = dget(D2_, 0);
             float acc;
             if (e >= 4 * A || on_final_edge(d0, e)) {  // exit edge or last edge: free road
                 acc = idm_free(v0, P);
@@ -1339,7 +1370,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                         lead_x_new = len;
                         fvn = 0.0f;
                     } else {
-                        s_mdst[l] = route_advance(D_[0]);
+                        s_mdst[l] = route_advance(dget(D2_, 0));
                     }
                 }
                 if (!pop) {
@@ -1379,10 +1410,8 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 }
                 if (pop) {
 #pragma unroll
-                    for (int i = 0; i < RCAP - 1; i++) {
-                        X_[i] = X_[i + 1];
-                        D_[i] = D_[i + 1];
-                    }
+                    for (int i = 0; i < RCAP - 1; i++) X_[i] = X_[i + 1];
+                    dpop(D2_);
                     vpop<kL>(V_, Vc);
                     n--;
                 }
@@ -1411,7 +1440,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 }
                 if (xe < 0.0f) xe = 0.0f;
                 DMDQN_DBG(n < cap && n < RCAP, DBG_SIM_RING);  // pass B granted only with room
-                lane_append<kL>(X_, V_, Vc, D_, n, lx, lv, xe, vin, dv);
+                lane_append<kL>(X_, V_, Vc, D2_, n, lx, lv, xe, vin, dv);
                 s_cnt[l] = n;
                 s_lx[l] = lx;
                 s_lv[l] = lv;
@@ -1448,6 +1477,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     }
     TAKE_INSERT();
 #undef TAKE_INSERT
+#undef LANE_LEN
     const int t = t0 + K;
     // ---- outputs: halting counts, signals, running / pending, done
     int run = own ? n : 0, pend = leader ? qend - qp : 0;
@@ -1482,7 +1512,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 if (i < n) {
                     G.x[base + i] = X_[i];
                     G.v[base + i] = vget<kL>(V_, Vc, i);
-                    G.dst[base + i] = D_[i];
+                    G.dst[base + i] = dget(D2_, i);
                 }
             }
         }

@@ -42,6 +42,15 @@ __host__ __device__ constexpr uint32_t green_lanes(uint32_t g) {
     return out;
 }
 
+// threadIdx.x behind an empty asm (the value the compiler cannot see through):
+// expressions of it are recomputed where they are used instead of being
+// hoisted out of a loop and held in (or spilled from) registers.
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 constexpr int kArrive = -2;
 enum { DIR_N = 0, DIR_S = 1, DIR_E = 2, DIR_W = 3 };
 enum { MV_R = 0, MV_S = 1, MV_L = 2, MV_U = 3 };
