@@ -154,12 +154,18 @@ def test_unmapped_and_unchanged_actions_let_the_program_run():
     env = SumoTrafficEnvironment(None, None, _ctl(ids, phases), max_simulation_time=400,
                                  env_config=EnvConfig(rows=2, cols=2, seed=6))
     assert env.get_action_size("J_0_1") == 2
-    seen = set()
     steps, info, _ = _drive(env, O.OracleEnv(2, 2, 6), 2, 2, 400, 1, seed=7,
-                            phase_of={0: 0, 1: 6}, seen=seen)
+                            phase_of={0: 0, 1: 6})
     assert steps == 400
-    shown = {p for _, p in seen}
-    assert {1, 2, 7, 8} & shown, shown  # yellow / all-red reached on their own
+    # always action 0: phase 0 is requested while it runs (no setPhase), so
+    # the program moves on to its yellow phase 1 after 25 s, then the next
+    # request sets phase 0 again
+    env2 = SumoTrafficEnvironment(None, None, _ctl(ids, phases), max_simulation_time=100,
+                                  env_config=EnvConfig(rows=2, cols=2, seed=6))
+    seen = set()
+    steps, info, _ = _drive(env2, O.OracleEnv(2, 2, 6), 2, 2, 100, 1, seed=7,
+                            phase_of={0: 0, 1: 6}, seen=seen, n_actions=1)
+    assert steps == 100 and {p for _, p in seen} == {0, 1}, seen
 
 
 def test_subset_of_junctions_controlled():
