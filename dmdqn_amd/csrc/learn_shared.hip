@@ -566,12 +566,6 @@ __device__ __forceinline__ half4v relu4(f32x4 c, half4v b) {
 //   G   dW3 (H2 own^T, DQ) ; dH1 own (dZ2 image) -> dZ1 own (over H2 own) ;
 //       dW2 (H1^T, dZ2 own) ; dW1 (X^T, dZ1 own)
 // Same rounding points as round 3's grad3 (Keras' mixed policy; same gradient bits).
-#ifndef SH_W3_PAD
-#define SH_W3_PAD 0  // padded [4][144] W3^T image (A/B: tools/build_exp.py)
-#endif
-#ifndef SH_GRAD_PAIR
-#define SH_GRAD_PAIR 0  // paired waves in the gradient phase (A/B: tools/build_exp.py)
-#endif
 namespace g4 {
 using gx::X_BYTES;
 using gx::IMG;
@@ -580,16 +574,12 @@ constexpr int OFF_H1 = 2 * X_BYTES;
 constexpr int OFF_Z2 = OFF_H1 + IMG;              // dZ2 [128][128], written by rows
 constexpr int OFF_H2 = OFF_Z2 + IMG;              // H2 own columns, then dZ1 own columns
 constexpr int OFF_DQ = OFF_H2 + IMG;              // [128][16]
-#if SH_W3_PAD
 // W3^T [4][W3LD] f16 (rows padded to 144 halves = 72 dwords, so the 4 rows start
 // 8 banks apart): lane (i, g) of the Q MFMA reads row i & 3 (lanes of equal
-// rows broadcast) and the dZ2 read takes row a -- both conflict-free.  The
+// rows broadcast) and the dZ2 read takes row a -- both conflict-free.  Round 4's
 // [16][128] image with repeated rows (rows 256 B apart, one bank set) made
 // both reads 8-way / 4-way bank conflicts (tools/lds_banks.py).
 constexpr int W3LD = H + 16, W3ROWS = NACT;
-#else
-constexpr int W3LD = H, W3ROWS = 16;              // W3^T [16][128], row m = W3^T[m & 3]
-#endif
 constexpr int OFF_W3 = OFF_DQ + B_ * 16 * 2;
 constexpr int OFF_SC = OFF_W3 + W3ROWS * W3LD * 2;  // sloss [8]
 constexpr int LDS = OFF_SC + 32;
@@ -680,7 +670,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
     const int c0 = 16 * wv;  // own column block
     const int bW = hoff(i, (c0 & 16) + 4 * g) + 256 * (c0 >> 5);
     const int trO = hsplit(8 * (g & 1) + (i >> 2), (c0 & 16) + 4 * (i & 3), g >> 1, 0) + 256 * (c0 >> 5);
-#if SH_GRAD_PAIR
     // the partner wave's column tile (w ^ 1) and this wave's half of the row
     // tiles: dW2 j-tiles 4hh..4hh+3, dW1 f-tiles 3hh..3hh+2 (hh = w & 1)
     const int cP = 16 * (wv ^ 1), hh = wv & 1;
@@ -696,7 +685,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         const int ft = 3 * hh + ff;
         xB[ff] = (ft & 1 ? trX[1] : trX[0]) + 256 * (ft >> 1);
     }
-#endif
     const bool stager = threadIdx.x < 256;
     int agent = blockIdx.x;
     if (agent < a.NA && stager) {
@@ -866,27 +854,34 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             }
         }
         SH_STAMP(agent, 5, threadIdx.x);
-        // ---- dW2[j][k own] and db2 ; dW1[f][j own] and db1 (K = rows)
-#if SH_GRAD_PAIR
-        // paired waves: waves 2p and 2p+1 share their two column tiles (k of dW2,
+        // ---- dW2[j][k] and db2 ; dW1[f][j] and db1 (K = rows), paired waves
+        // (round 5): waves 2p and 2p+1 share their two column tiles (k of dW2,
         // j of dW1) and split the row tiles (j of dW2, f of dW1) in halves, so a
         // wave reads 4 H1 + 3 X + 4 own / partner fragments per K-step for 16
-        // MFMAs instead of 8 + 6 + 2; every gradient element is the same MFMA
-        // chain as the unpaired order (bit-identical slabs)
+        // MFMAs instead of 8 + 6 + 2 (round 4: every wave read all eight H1 and
+        // six X fragments for its one column tile).  Every gradient element is
+        // the same MFMA chain as before: the slabs are bit-identical.
+        // dW2 first: dZ2 (both column tiles) is complete since B3
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             const half8 bqA = frag_tr_p(Z2I + trO + 2 * 16 * H * s);
-            const half8 bvA = frag_tr_p(H2I + trO + 2 * 16 * H * s);
             const half8 bqB = frag_tr_p(Z2I + trP + 2 * 16 * H * s);
-            const half8 bvB = frag_tr_p(H2I + trP + 2 * 16 * H * s);
             GB2 = mfma(ones, bqA, GB2);
-            GB1 = mfma(ones, bvA, GB1);
 #pragma unroll
             for (int jj = 0; jj < 4; jj++) {
                 const half8 av = frag_tr_p(H1I + hB[jj] + 2 * 16 * H * s);
                 G2[2 * jj] = mfma(av, bqA, G2[2 * jj]);
                 G2[2 * jj + 1] = mfma(av, bqB, G2[2 * jj + 1]);
             }
+        }
+        // the partner's dZ1 columns (written over its H2 columns in its dH1
+        // phase) are complete only after this barrier
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const half8 bvA = frag_tr_p(H2I + trO + 2 * 16 * H * s);
+            const half8 bvB = frag_tr_p(H2I + trP + 2 * 16 * H * s);
+            GB1 = mfma(ones, bvA, GB1);
 #pragma unroll
             for (int ff = 0; ff < 3; ff++) {
                 const half8 xv = frag_tr_p(X + xB[ff] + 2 * 16 * DP * s);
@@ -894,21 +889,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
                 G1[2 * ff + 1] = mfma(xv, bvB, G1[2 * ff + 1]);
             }
         }
-#else
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const half8 bq = frag_tr_p(Z2I + trO + 2 * 16 * H * s);
-            const half8 bv = frag_tr_p(H2I + trO + 2 * 16 * H * s);
-            GB2 = mfma(ones, bq, GB2);
-            GB1 = mfma(ones, bv, GB1);
-#pragma unroll
-            for (int jt = 0; jt < 8; jt++)
-                G2[jt] = mfma(frag_tr_p(H1I + trH[jt & 1] + 256 * (jt >> 1) + 2 * 16 * H * s), bq, G2[jt]);
-#pragma unroll
-            for (int ft = 0; ft < 6; ft++)
-                G1[ft] = mfma(frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s), bv, G1[ft]);
-        }
-#endif
         yv = yn;
         avl = an;
         SH_STAMP(agent, 6, threadIdx.x);
@@ -918,7 +898,9 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
     // partial sums of this workgroup, kernel layout (every index written once)
     float *G = slab + (size_t)blockIdx.x * L::P;
     const int n0 = 16 * w, n = n0 + i;  // this lane's neuron (C-tile column)
-#if SH_GRAD_PAIR
+    if (i < NACT)  // G3: rows k = n0 + 4g + e, column a = i
+        *reinterpret_cast<float4 *>(G + L::oW3T + i * H + n0 + 4 * g) =
+            make_float4(G3[0], G3[1], G3[2], G3[3]);
     {
         const int hh = w & 1, nB = 16 * (w ^ 1) + i;  // the partner's column
 #pragma unroll
@@ -945,21 +927,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             }
         }
     }
-#else
-    if (i < NACT)  // G3: rows k = n0 + 4g + e, column a = i
-        *reinterpret_cast<float4 *>(G + L::oW3T + i * H + n0 + 4 * g) =
-            make_float4(G3[0], G3[1], G3[2], G3[3]);
-#pragma unroll
-    for (int jt = 0; jt < 8; jt++)  // G2[jt]: fan-in j = 16jt + 4g + e, fan-out k = n
-        *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(n, 16 * jt + 4 * g, H)) =
-            make_float4(G2[jt][0], G2[jt][1], G2[jt][2], G2[jt][3]);
-#pragma unroll
-    for (int ft = 0; ft < 6; ft++)  // G1[ft]: features 16ft + 4g + e, neuron n
-        if (ft < 5 || g < 2)
-            *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(n, 16 * ft + 4 * g)) =
-                make_float4(G1[ft][0], G1[ft][1], G1[ft][2], G1[ft][3]);
-    if (g == 2) G[L::oW1X + n] = G1[5][0];  // feature 88
-#endif
     if (g == 0) {
         G[L::ob2 + n] = GB2[0];
         G[L::ob1 + n] = GB1[0];
