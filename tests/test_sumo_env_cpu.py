@@ -55,3 +55,41 @@ def test_reference_defaults_and_signature():
     r = inspect.signature(S.SumoTrafficEnvironment.reset).parameters
     assert r["sumo_seed"].default == "random" and r["use_gui"].default is False
     assert os.path.exists(GOLDEN)
+
+
+def _bare_env(phases, controlled, current):
+    """A SumoTrafficEnvironment shell (no device) for the host-side action
+    mapping: ids of a 2x2 grid, `controlled` with their action_phases, the
+    simulator's current phase per signal."""
+    import torch
+    from types import SimpleNamespace
+    env = S.SumoTrafficEnvironment.__new__(S.SumoTrafficEnvironment)
+    ids = [f"J_{r}_{c}" for r in range(2) for c in range(2)]
+    env.env = SimpleNamespace(A=4, phase=torch.tensor([current], dtype=torch.int32))
+    env.traffic_light_ids = {j: j for j in controlled}
+    env.action_to_sumo_phase = {j: phases for j in controlled}
+    env._phase_of = {j: {a: S._phase_index(p) for a, p in phases.items() if isinstance(p, int) or p}
+                     for j in controlled}
+    env._signal = {j: ids.index(j) for j in controlled}
+    return env
+
+
+def test_apply_actions_follows_the_reference_rules(capsys):
+    """sumo_env.py:491-530 on the host: an unknown id, an unmapped action and a
+    string the program lacks are skipped (the last with the reference's
+    warning); setPhase is skipped when the signal is already in the phase;
+    signals without an action keep their program (-1 = no setPhase)."""
+    P = S.TL_PROGRAM_STATES
+    phases = {0: P[0], 1: P[6], 2: "G" * 24, 3: ""}
+    env = _bare_env(phases, ["J_0_0", "J_0_1", "J_1_0"], current=[0, 3, 6, 9])
+    ph = env._apply_actions({"J_0_0": 0,      # already in phase 0: skipped
+                             "J_0_1": 1,      # phase 6
+                             "J_1_0": 2,      # string not in the program: warning, skipped
+                             "J_1_1": 1,      # not controlled: skipped
+                             "nope": 0})
+    assert ph.tolist() == [[-1, 6, -1, -1]]
+    assert "not found for TL J_1_0" in capsys.readouterr().out
+    ph = env._apply_actions({"J_0_0": 3, "J_0_1": 7, "J_1_0": 0})  # "" and unmapped: skipped
+    assert ph.tolist() == [[-1, -1, 0, -1]]
+    assert env._apply_actions({"J_1_0": 1}).tolist() == [[-1, -1, -1, -1]]  # 6 already runs
+    assert S._phase_index(P[6]) == 6 and S.NO_SET_PHASE == -1
