@@ -299,17 +299,31 @@ __device__ __forceinline__ void load_w2(const T *Wg, Frags &f) {
     f.b2 = ld_bias4_h(Wg + L::ob2 + 16 * w + 4 * lg);
 }
 
-// Stage W3T (f16) and b3 of one network into LDS (threads 0..127; caller syncs).
+// The output layer (W3T f16 image + b3) of one network into LDS, in two
+// halves: the loads (into registers, issued early) and the LDS stores (once
+// they land; the caller syncs).  Thread t < 128: W3T[4t..4t+3]; t in 128..131:
+// b3[t - 128] (in v.x).
+struct OutStage {
+    float4 v;
+};
+
 template <typename T>
-__device__ __forceinline__ void stage_out(const T *Wg, h16 *w3, float *b3) {
+__device__ __forceinline__ OutStage stage_out_load(const T *Wg) {
+    const int t = threadIdx.x;
+    OutStage o{make_float4(0.f, 0.f, 0.f, 0.f)};
+    if (t < NACT * H / 4) o.v = ld_bias4(Wg + L::oW3T + 4 * t);
+    else if (t < NACT * H / 4 + NACT) o.v.x = (float)(h16)Wg[L::ob3 + t - NACT * H / 4];
+    return o;
+}
+
+__device__ __forceinline__ void stage_out_store(const OutStage &o, h16 *w3, float *b3) {
     const int t = threadIdx.x;
     if (t < NACT * H / 4) {
-        const float4 v = ld_bias4(Wg + L::oW3T + 4 * t);
         half4v hv;
-        hv[0] = (h16)v.x; hv[1] = (h16)v.y; hv[2] = (h16)v.z; hv[3] = (h16)v.w;
+        hv[0] = (h16)o.v.x; hv[1] = (h16)o.v.y; hv[2] = (h16)o.v.z; hv[3] = (h16)o.v.w;
         *reinterpret_cast<half4v *>(w3 + 4 * t) = hv;
     } else if (t < NACT * H / 4 + NACT) {
-        b3[t - NACT * H / 4] = (float)(h16)Wg[L::ob3 + t - NACT * H / 4];
+        b3[t - NACT * H / 4] = o.v.x;
     }
 }
 
@@ -691,11 +705,17 @@ __device__ __forceinline__ void commit_x(h16 *R, const RowsT<XF> &g) {
     }
 }
 
+// The batch's deque positions (thread tid < 128: position tid).  Loaded first
+// in the kernel: the slot computation then waits only for them (vmcnt is
+// in-order, so a load issued after the weight fragments would wait for those).
+__device__ __forceinline__ int batch_pos(const dmdqn_learn_args &a, int agent) {
+    return threadIdx.x < B_ ? a.idx[(size_t)agent * B_ + threadIdx.x] : 0;
+}
+
 // Ring slots of the batch (deque positions -> slots).  Ends with a barrier.
-__device__ __forceinline__ void batch_slots(const dmdqn_learn_args &a, int agent, const Scratch &S) {
+__device__ __forceinline__ void batch_slots(const dmdqn_learn_args &a, int pos, const Scratch &S) {
     const int tid = threadIdx.x;
     if (tid < B_) {
-        int pos = a.idx[(size_t)agent * B_ + tid];
         DMDQN_DBG(pos >= 0 && pos < a.cap, DBG_LEARN_IDX);
 #ifdef DMDQN_DEBUG_BOUNDS
         if (pos < 0 || pos >= a.cap) pos = 0;
@@ -775,13 +795,15 @@ __device__ __forceinline__ void zscore(const Scratch &S) {
 
 // Slots, then the s' rows -> X(S') in R2 plus the metadata, then the z-score.
 // X(S') is visible to every thread on return (zscore's barriers).  XF: float
-// rows, the metadata from the per-slot arrays.
-template <bool XF = false>
-__device__ __forceinline__ void batch_head(const dmdqn_learn_args &a, int agent, h16 *R2,
-                                           const Scratch &S) {
-    batch_slots(a, agent, S);
+// rows, the metadata from the per-slot arrays.  issued() runs once the row
+// loads are in flight (the caller's LDS stores of earlier loads).
+template <bool XF = false, typename Issued>
+__device__ __forceinline__ void batch_head(const dmdqn_learn_args &a, int agent, int pos, h16 *R2,
+                                           const Scratch &S, Issued issued) {
+    batch_slots(a, pos, S);
     RowsT<XF> gn;
     gather_x<XF>(a, agent, true, S.slot, gn);
+    issued();
     if constexpr (XF) {
         const int tid = threadIdx.x;
         if (tid < B_) {
@@ -984,15 +1006,26 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, f
     const AdamC AK{a.alpha, a.c1, a.c2, a.eps, SYNC && !GOUT, TH, GOUT,
                    GOUT ? gout + agent * Pz : nullptr};
     STAMP(0);
+    // Issue order (vmcnt is in-order): the deque positions, the output layers,
+    // then the target's fragments -- so the slot computation waits only for
+    // the positions and the S' row gather goes out while the fragments land
+    // (round 4 stored the output layers to LDS right after issuing the
+    // fragments: the head then waited for every fragment before the gather)
+    const int pos = batch_pos(a, agent);
+    const OutStage so_on = stage_out_load(Wp);
+    OutStage so_tg;
+    if (TH) so_tg = stage_out_load(TH);
+    else so_tg = stage_out_load(Tp);
     Frags fr;
     if (TH) load_frags(TH, fr);  // in flight during the z-score + gather
     else load_frags(a.target + agent * Pz, fr);
-    stage_out(Wp, W3L, B3L);  // synced by the metadata barrier below
-    if (TH) stage_out(TH, W3L + NACT * H, B3L + NACT);
-    else stage_out(Tp, W3L + NACT * H, B3L + NACT);
 
-    // ---- slots, X(S') + metadata from the s' rows, z-score
-    batch_head<XF>(a, agent, R2, S);
+    // ---- slots, X(S') + metadata from the s' rows, z-score (the output
+    // layers' LDS images are synced by its barriers)
+    batch_head<XF>(a, agent, pos, R2, S, [&]() {
+        stage_out_store(so_on, W3L, B3L);
+        stage_out_store(so_tg, W3L + NACT * H, B3L + NACT);
+    });
     STAMP(1);
     STAMP(2);
     // ---- target(S') -> z3 ; online(S') -> Q ; y

@@ -5,7 +5,9 @@ build of tools/build_exp.py (or the product library) called through the C ABI
 with the args of one product learn.  Prints per library the median / min of
 all its launches (ms) and the sha1 of the weights after one launch from the
 same starting weights (a timing-only variant differs there, by design).
-usage: python tools/ab_learn_lib.py [--rounds R] [--reps N] lib.so [lib.so ...]"""
+usage: python tools/ab_learn_lib.py [--rounds R] [--reps N] [--envs E --agents A] [--bf16]
+       lib.so [lib.so ...]   (default C3: 1024 envs x 16 agents, fp16; C2: --envs 256
+       --agents 4 --bf16)"""
 import ctypes as C
 import hashlib
 import json
@@ -29,9 +31,13 @@ def _opt(name, default):
 
 
 R, N = _opt("--rounds", 6), _opt("--reps", 20)
+E, A = _opt("--envs", 1024), _opt("--agents", 16)
+PREC = "fp16"
+if "--bf16" in sys.argv:
+    sys.argv.remove("--bf16")
+    PREC = "bf16"
 libs = sys.argv[1:]
-E, A = 1024, 16
-ag = BatchedDQN(E, A, AgentConfig(precision="fp16", seed=0, replay_buffer_size=1000))
+ag = BatchedDQN(E, A, AgentConfig(precision=PREC, seed=0, replay_buffer_size=1000))
 g = torch.Generator(device="cuda").manual_seed(0)
 for t in range(200):
     s = torch.randint(-1, 24, (E, A, 89), device="cuda", generator=g).float()
