@@ -209,30 +209,30 @@ __device__ __forceinline__ half8 wfrag(const h16 *WT, int ld, int n0, int k0, in
 // 89..95 are zero weights, not stored).
 __device__ __forceinline__ half8 w1frag(const float *W1, int n0, int s) {
     const int l = threadIdx.x & 63, lg = l >> 4, n = n0 + (l & 15);
+    const bool tile = s < 2 || lg < 3;
+    // branch-free: every lane loads a valid tile address (fragment 2's lane
+    // group 3 re-reads group 2's) and, for fragment 2, the feature-88 column;
+    // the select follows (a branch around the loads made the head wait)
+    const float4 *p = reinterpret_cast<const float4 *>(W1 + qn_w1<H>(n, 32 * s + 8 * (tile ? lg : 2)));
+    const float4 x = p[0], y = p[1];
+    const float c = s == 2 ? W1[qn_w1<H>(n, QN_DT)] : 0.0f;
     half8 r;
-    if (s < 2 || lg < 3) {
-        const float4 *p = reinterpret_cast<const float4 *>(W1 + qn_w1<H>(n, 32 * s + 8 * lg));
-        float4 x = p[0], y = p[1];
-        r[0] = (h16)x.x; r[1] = (h16)x.y; r[2] = (h16)x.z; r[3] = (h16)x.w;
-        r[4] = (h16)y.x; r[5] = (h16)y.y; r[6] = (h16)y.z; r[7] = (h16)y.w;
-    } else {
-#pragma unroll
-        for (int e = 1; e < 8; e++) r[e] = (h16)0.0f;
-        r[0] = (h16)W1[qn_w1<H>(n, QN_DT)];
-    }
+    r[0] = (h16)(tile ? x.x : c); r[1] = (h16)(tile ? x.y : 0.0f);
+    r[2] = (h16)(tile ? x.z : 0.0f); r[3] = (h16)(tile ? x.w : 0.0f);
+    r[4] = (h16)(tile ? y.x : 0.0f); r[5] = (h16)(tile ? y.y : 0.0f);
+    r[6] = (h16)(tile ? y.z : 0.0f); r[7] = (h16)(tile ? y.w : 0.0f);
     return r;
 }
 
 __device__ __forceinline__ half8 w1frag(const h16 *W1, int n0, int s) {
     const int l = threadIdx.x & 63, lg = l >> 4, n = n0 + (l & 15);
+    const bool tile = s < 2 || lg < 3;
+    const half8 t = *reinterpret_cast<const half8 *>(W1 + qn_w1<H>(n, 32 * s + 8 * (tile ? lg : 2)));
+    const h16 c = s == 2 ? W1[qn_w1<H>(n, QN_DT)] : (h16)0.0f;
     half8 r;
-    if (s < 2 || lg < 3) {
-        r = *reinterpret_cast<const half8 *>(W1 + qn_w1<H>(n, 32 * s + 8 * lg));
-    } else {
+    r[0] = tile ? t[0] : c;
 #pragma unroll
-        for (int e = 1; e < 8; e++) r[e] = (h16)0.0f;
-        r[0] = W1[qn_w1<H>(n, QN_DT)];
-    }
+    for (int e = 1; e < 8; e++) r[e] = tile ? t[e] : (h16)0.0f;
     return r;
 }
 
@@ -303,16 +303,20 @@ __device__ __forceinline__ void load_w2(const T *Wg, Frags &f) {
 // halves: the loads (into registers, issued early) and the LDS stores (once
 // they land; the caller syncs).  Thread t < 128: W3T[4t..4t+3]; t in 128..131:
 // b3[t - 128] (in v.x).
+// The loads are issued by every thread at valid addresses (no divergent
+// branch around a load: the wait-count insertion is conservative at control
+// flow, and a branch there made the head wait for each load in turn).
 struct OutStage {
     float4 v;
+    float b;
 };
 
 template <typename T>
 __device__ __forceinline__ OutStage stage_out_load(const T *Wg) {
     const int t = threadIdx.x;
-    OutStage o{make_float4(0.f, 0.f, 0.f, 0.f)};
-    if (t < NACT * H / 4) o.v = ld_bias4(Wg + L::oW3T + 4 * t);
-    else if (t < NACT * H / 4 + NACT) o.v.x = (float)(h16)Wg[L::ob3 + t - NACT * H / 4];
+    OutStage o;
+    o.v = ld_bias4(Wg + L::oW3T + 4 * (t & (NACT * H / 4 - 1)));
+    o.b = (float)(h16)Wg[L::ob3 + (t & (NACT - 1))];
     return o;
 }
 
@@ -323,7 +327,7 @@ __device__ __forceinline__ void stage_out_store(const OutStage &o, h16 *w3, floa
         hv[0] = (h16)o.v.x; hv[1] = (h16)o.v.y; hv[2] = (h16)o.v.z; hv[3] = (h16)o.v.w;
         *reinterpret_cast<half4v *>(w3 + 4 * t) = hv;
     } else if (t < NACT * H / 4 + NACT) {
-        b3[t - NACT * H / 4] = o.v.x;
+        b3[t - NACT * H / 4] = o.b;
     }
 }
 
@@ -709,21 +713,21 @@ __device__ __forceinline__ void commit_x(h16 *R, const RowsT<XF> &g) {
 // in the kernel: the slot computation then waits only for them (vmcnt is
 // in-order, so a load issued after the weight fragments would wait for those).
 __device__ __forceinline__ int batch_pos(const dmdqn_learn_args &a, int agent) {
-    return threadIdx.x < B_ ? a.idx[(size_t)agent * B_ + threadIdx.x] : 0;
+    return a.idx[(size_t)agent * B_ + (threadIdx.x & (B_ - 1))];
 }
 
 // Ring slots of the batch (deque positions -> slots).  Ends with a barrier.
 __device__ __forceinline__ void batch_slots(const dmdqn_learn_args &a, int pos, const Scratch &S) {
-    const int tid = threadIdx.x;
-    if (tid < B_) {
-        DMDQN_DBG(pos >= 0 && pos < a.cap, DBG_LEARN_IDX);
+    // every thread stores (the 4 lane groups of 128 store the same values):
+    // a store under tid < B_ let the compiler sink the idx load into that
+    // branch, behind the fragment loads, and wait for all of them
+    DMDQN_DBG(pos >= 0 && pos < a.cap, DBG_LEARN_IDX);
 #ifdef DMDQN_DEBUG_BOUNDS
-        if (pos < 0 || pos >= a.cap) pos = 0;
+    if (pos < 0 || pos >= a.cap) pos = 0;
 #endif
-        int s = a.start + pos;
-        if (s >= a.cap) s -= a.cap;
-        S.slot[tid] = s;
-    }
+    int s = a.start + pos;
+    if (s >= a.cap) s -= a.cap;
+    S.slot[threadIdx.x & (B_ - 1)] = s;
     __syncthreads();
 }
 
@@ -993,7 +997,11 @@ __device__ __forceinline__ void bwd_dz1(h16 *R1, const uint32_t *mask, const f32
 // gradient entry goes to gout[agent][P] (the 16-bit value Adam would receive)
 // and dmdqn_adam_agents applies the identical Adam step in a second launch,
 // which can share the chip with the next step's side-stream work.
-template <bool QSTATS, bool SYNC, bool GOUT, bool XF = false>
+// TS: the 16-bit target shadow is given (a.target_h != NULL, the normal case):
+// a compile-time choice, because a run-time branch between the two fragment
+// sources made the loaded registers meet at a control-flow merge, where the
+// compiler waits for every load (round 5).
+template <bool QSTATS, bool SYNC, bool GOUT, bool XF = false, bool TS = true>
 __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, float *gout) {
     LEARN_SMEM_SETUP;
     const int agent = blockIdx.x;
@@ -1002,7 +1010,7 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, f
     float *Wp = a.params + agent * Pz, *Mp = a.adam_m + agent * Pz, *Vp = a.adam_v + agent * Pz;
     float *Tp = a.target + agent * Pz;
     const size_t Ph = (Pz + 7) / 8 * 8;
-    h16 *TH = a.target_h ? reinterpret_cast<h16 *>(a.target_h) + agent * Ph : nullptr;
+    h16 *TH = TS ? reinterpret_cast<h16 *>(a.target_h) + agent * Ph : nullptr;
     const AdamC AK{a.alpha, a.c1, a.c2, a.eps, SYNC && !GOUT, TH, GOUT,
                    GOUT ? gout + agent * Pz : nullptr};
     STAMP(0);
@@ -1014,11 +1022,11 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, f
     const int pos = batch_pos(a, agent);
     const OutStage so_on = stage_out_load(Wp);
     OutStage so_tg;
-    if (TH) so_tg = stage_out_load(TH);
+    if constexpr (TS) so_tg = stage_out_load(TH);
     else so_tg = stage_out_load(Tp);
     Frags fr;
-    if (TH) load_frags(TH, fr);  // in flight during the z-score + gather
-    else load_frags(a.target + agent * Pz, fr);
+    if constexpr (TS) load_frags(TH, fr);  // in flight during the z-score + gather
+    else load_frags(Tp, fr);
 
     // ---- slots, X(S') + metadata from the s' rows, z-score (the output
     // layers' LDS images are synced by its barriers)
@@ -1236,6 +1244,13 @@ __global__ void __launch_bounds__(256) H16_ADAM_KERNEL(float *W, float *M, float
 
 DMDQN_DBG_READER(dbg_flags)
 
+// The kernel instance for a run-time target-shadow flag (TS above).
+template <bool QSTATS, bool SYNC, bool GOUT, bool XF>
+void (*pick_learn(bool ts))(dmdqn_learn_args, float *) {
+    return ts ? H16_LEARN_KERNEL<QSTATS, SYNC, GOUT, XF, true>
+              : H16_LEARN_KERNEL<QSTATS, SYNC, GOUT, XF, false>;
+}
+
 }  // namespace H16K
 
 int H16_LAUNCH(const dmdqn_learn_args *a, hipStream_t s) {
@@ -1243,15 +1258,16 @@ int H16_LAUNCH(const dmdqn_learn_args *a, hipStream_t s) {
                   "dmdqn_learn: precision %d (" H16_NAME ") needs hidden=128 (P=%d)", a->precision,
                   H16K::L::P);
     using namespace H16K;
-    auto kern = a->qstats ? (a->sync_target ? H16_LEARN_KERNEL<true, true, false>
-                                            : H16_LEARN_KERNEL<true, false, false>)
-                          : (a->sync_target ? H16_LEARN_KERNEL<false, true, false>
-                                            : H16_LEARN_KERNEL<false, false, false>);
+    const bool ts = a->target_h != nullptr;
+    auto kern = a->qstats ? (a->sync_target ? pick_learn<true, true, false, false>(ts)
+                                            : pick_learn<true, false, false, false>(ts))
+                          : (a->sync_target ? pick_learn<false, true, false, false>(ts)
+                                            : pick_learn<false, false, false, false>(ts));
     if (a->row_format == DMDQN_ROWS_F32)  // float rows (the drop-in surface): X from a.xs / a.xn
-        kern = a->qstats ? (a->sync_target ? H16_LEARN_KERNEL<true, true, false, true>
-                                           : H16_LEARN_KERNEL<true, false, false, true>)
-                         : (a->sync_target ? H16_LEARN_KERNEL<false, true, false, true>
-                                           : H16_LEARN_KERNEL<false, false, false, true>);
+        kern = a->qstats ? (a->sync_target ? pick_learn<true, true, false, true>(ts)
+                                           : pick_learn<true, false, false, true>(ts))
+                         : (a->sync_target ? pick_learn<false, true, false, true>(ts)
+                                           : pick_learn<false, false, false, true>(ts));
     hipLaunchKernelGGL(kern, dim3(a->NA), dim3(512), 0, s, *a, (float *)nullptr);
     DMDQN_LAUNCH_CHECK("k_learn_" H16_NAME);
     return DMDQN_OK;
@@ -1264,7 +1280,9 @@ int H16_LAUNCH_GRAD(const dmdqn_learn_args *a, float *grad, hipStream_t s) {
                   a->precision, H16K::L::P);
     using namespace H16K;
     DMDQN_REQUIRE(a->row_format == DMDQN_ROWS_I8, "dmdqn_learn_grad: int8 replay rows only");
-    auto kern = a->qstats ? H16_LEARN_KERNEL<true, false, true> : H16_LEARN_KERNEL<false, false, true>;
+    const bool ts = a->target_h != nullptr;
+    auto kern = a->qstats ? pick_learn<true, false, true, false>(ts)
+                          : pick_learn<false, false, true, false>(ts);
     hipLaunchKernelGGL(kern, dim3(a->NA), dim3(512), 0, s, *a, grad);
     DMDQN_LAUNCH_CHECK("k_learn_" H16_NAME " (gradient)");
     return DMDQN_OK;
