@@ -346,10 +346,8 @@ struct NoHook {
 // packed v_pk_add_f16; bf16: an f32 add rounded once, the same value).
 __device__ __forceinline__ half4v relu_h4(f32x4 acc, half4v b) {
     const half4v z = __builtin_convertvector(acc, half4v) + b;
-    half4v hv;
-#pragma unroll
-    for (int e = 0; e < 4; e++) hv[e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
-    return hv;
+    const half4v zero = {(h16)0.0f, (h16)0.0f, (h16)0.0f, (h16)0.0f};
+    return z > zero ? z : zero;  // vector select (packed max; the build has no SLP)
 }
 
 struct NoHook0 {

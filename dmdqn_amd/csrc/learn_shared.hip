@@ -213,13 +213,23 @@ __device__ __forceinline__ void x_issue(const int8_t *row, XTile &x) {
     for (int s = 0; s < 3; s++) x.raw[s] = reinterpret_cast<const uint2 *>(row)[4 * s + g];
 }
 
+// int8 -> f16 exactly, two values per v_perm + v_pk_add (as gx::xrows_commit):
+// the byte b ^ 0x80 = v + 128 under a high byte 0x64 is the half 1024 + v + 128;
+// subtracting 1152 leaves v.
 __device__ __forceinline__ void x_frags(const XTile &x, half8 bx[3]) {
+    typedef h16 h2v __attribute__((ext_vector_type(2)));
+    const h2v bias = {(h16)-1152.0f, (h16)-1152.0f};
 #pragma unroll
     for (int s = 0; s < 3; s++)
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            bx[s][e] = (h16)(float)(int8_t)(x.raw[s].x >> (8 * e));
-            bx[s][e + 4] = (h16)(float)(int8_t)(x.raw[s].y >> (8 * e));
+        for (int q = 0; q < 2; q++) {
+            const uint32_t wv = (q ? x.raw[s].y : x.raw[s].x) ^ 0x80808080u;
+            const h2v a0 = __builtin_bit_cast(h2v, __builtin_amdgcn_perm(0x64646464u, wv, 0x07010700u)) + bias;
+            const h2v a1 = __builtin_bit_cast(h2v, __builtin_amdgcn_perm(0x64646464u, wv, 0x07030702u)) + bias;
+            bx[s][4 * q + 0] = a0[0];
+            bx[s][4 * q + 1] = a0[1];
+            bx[s][4 * q + 2] = a1[0];
+            bx[s][4 * q + 3] = a1[1];
         }
 }
 
@@ -228,8 +238,10 @@ __device__ __forceinline__ void x_frags(const XTile &x, half8 bx[3]) {
 // elements 4 (t & 1) .. +3.
 __device__ __forceinline__ void dense_out(f32x4 c, half4v b, int t, half8 *ops) {
     const half4v z = __builtin_convertvector(c, half4v) + b;
+    const half4v zero = {(h16)0.0f, (h16)0.0f, (h16)0.0f, (h16)0.0f};
+    const half4v r = z > zero ? z : zero;  // vector select: two v_pk_max_f16
 #pragma unroll
-    for (int e = 0; e < 4; e++) ops[t >> 1][4 * (t & 1) + e] = z[e] > (h16)0.0f ? z[e] : (h16)0.0f;
+    for (int e = 0; e < 4; e++) ops[t >> 1][4 * (t & 1) + e] = r[e];
 }
 
 __device__ __forceinline__ half4v bias4(const h16 *bias, int t) {
