@@ -331,9 +331,6 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
 // ---------------------------------------------------------------- pass 1: S'
 // LDS: both nets (2 x 58,896 B) + per wave: rewards f64 [128], ring slots
 // [128], transition word (a | done << 8) [128].
-#ifndef SH_GRAD
-#define SH_GRAD 4  // gradient pass: 4 = k_shared_grad4 (8 waves), 6 = k_shared_grad6 (4 waves)
-#endif
 #ifndef NEXT_NT
 #define NEXT_NT 2  // 16-row tiles per weight read in k_shared_next
 #endif
@@ -389,13 +386,13 @@ __global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_
 #pragma unroll
         for (int n = 0; n < NEXT_NT; n++)
             x_issue(base + (size_t)ring_slot(a, pt[n]) * DMDQN_ROW_BYTES, xt[n]);
-        const int nxt = agent + stride;
-        if (nxt < a.NA) {
-            p0 = a.idx[(size_t)nxt * B_ + l];
-            p1 = a.idx[(size_t)nxt * B_ + l + 64];
+        // the next agent's positions, branch-free (the last agent's when none:
+        // a branch here made later waits conservative, as in gx::pos3)
+        const int nxt = agent + stride < a.NA ? agent + stride : a.NA - 1;
+        p0 = a.idx[(size_t)nxt * B_ + l];
+        p1 = a.idx[(size_t)nxt * B_ + l + 64];
 #pragma unroll
-            for (int n = 0; n < NEXT_NT; n++) pt[n] = a.idx[(size_t)nxt * B_ + 16 * n + i];
-        }
+        for (int n = 0; n < NEXT_NT; n++) pt[n] = a.idx[(size_t)nxt * B_ + 16 * n + i];
         slots[l] = s0;
         slots[l + 64] = s1;
         tw[l] = m0.x;
@@ -493,7 +490,9 @@ __device__ __forceinline__ void row_loss(int kind, float diff, float &term, floa
 // ---------------------------------------------------------------- pass 2: shared helpers
 // (The round-3 neuron-owning gradient pass, k_shared_grad3, was an A/B
 // template here until round 4; it lives on in git history -- rebuild it for a
-// same-box A/B with tools/build_rev.py 2d71bef <name> -DSH_GRAD=3.)
+// same-box A/B with tools/build_rev.py 2d71bef <name> -DSH_GRAD=3.  Round 5's
+// one-wave-per-SIMD variant k_shared_grad6 (4 waves, two neuron tiles each;
+// slower): tools/build_rev.py 21344f7 <name> -DSH_GRAD=6.)
 namespace gx {
 constexpr int X_BYTES = B_ * DP * 2;             // [128][96] f16
 constexpr int IMG = B_ * H * 2;                  // [128][128] f16
@@ -540,8 +539,14 @@ __device__ __forceinline__ void xrows_commit(const XRows &x, h16 *X, int part) {
     }
 }
 
+// Deque position of the row of staging part `part` (2 parts per row) of
+// `agent`, loaded unconditionally at a valid address (agent clamped to the last
+// one, part wrapped): the look-ahead loads of the next agents sit on no branch,
+// since the wait-count insertion is conservative at control-flow merges (a
+// branch around them made the L1 phase wait for the next agent's X rows).
 __device__ __forceinline__ int pos3(const dmdqn_learn_args &a, int agent, int part) {
-    return agent < a.NA && part < 2 * B_ ? a.idx[(size_t)agent * B_ + (part >> 1)] : 0;
+    const int ag = agent < a.NA ? agent : a.NA - 1;
+    return a.idx[(size_t)ag * B_ + ((part >> 1) & (B_ - 1))];
 }
 
 __device__ __forceinline__ float pickf4(float q0, float q1, float q2, float q3, int k) {
@@ -720,14 +725,14 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         SH_STAMP(agent, 0, threadIdx.x);
         const h16 *X = reinterpret_cast<const h16 *>(smem + OFF_X + buf * X_BYTES);
         const int nxt = agent + gridDim.x;
+        // look-ahead loads for the next agent, branch-free (pos3): every thread
+        // loads (threads >= 256 repeat the first half's X parts), at the last
+        // agent's rows when there is no next agent
+        const int nxc = nxt < a.NA ? nxt : a.NA - 1;
         gx::XRows xn;
-        float yn = 0.0f;
-        int an = 0;
-        if (nxt < a.NA && stager) gx::xrows_issue<NTH>(a, nxt, npos, threadIdx.x, xn);
-        if (nxt < a.NA) {
-            yn = y_in[(size_t)nxt * B_ + row];
-            an = act_in[(size_t)nxt * B_ + row];
-        }
+        gx::xrows_issue<NTH>(a, nxc, npos, threadIdx.x & 255, xn);
+        const float yn = y_in[(size_t)nxc * B_ + row];
+        const int an = act_in[(size_t)nxc * B_ + row];
         npos = gx::pos3(a, nxt + gridDim.x, threadIdx.x);
         // ---- L1: own neuron tile, row tiles in passes of RH -> H1 image
 #pragma unroll
@@ -951,368 +956,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
 
 }  // namespace g4
 
-// ---------------------------------------------------------------- pass 2, v6
-// One wave per SIMD (4 waves, up to 512 registers per lane): wave w owns the
-// two neuron tiles 2w, 2w + 1 (neurons 32w..32w+31) with both weight slices in
-// registers, so every activation / dZ fragment read from LDS feeds two MFMAs
-// (grad4: one), and the rows of the RQ phase are row tiles 2w, 2w + 1.  The
-// dW1 phase reads only the wave's own dZ1 columns (no partner, no mid-phase
-// barrier): four barriers per agent.  Per gradient element the MFMA chains
-// and rounding points are grad4's, so the slabs are bit-identical.
-namespace g6 {
-using g4::OFF_X;
-using g4::OFF_H1;
-using g4::OFF_Z2;
-using g4::OFF_H2;
-using g4::OFF_DQ;
-using g4::OFF_W3;
-using g4::W3LD;
-using g4::W3ROWS;
-using g4::row16_sum;
-using gx::X_BYTES;
-constexpr int NW = 4, NTH = 64 * NW;
-constexpr int OFF_SC = g4::OFF_SC;  // sloss [8] (one per 16-row tile, summed in grad4's order)
-constexpr int LDS = g4::LDS;
-
-struct WSlice6 {
-    half8 w1[2][3], w2[2][4], w2b[2][4];
-    half4v b1[2], b2[2], b3;
-};
-
-__device__ __forceinline__ void load_slice6(const h16 *WH, int w, WSlice6 &S) {
-    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int t = 2 * w + u, j = 16 * t + i;
-#pragma unroll
-        for (int s = 0; s < 3; s++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const int f = 32 * s + 8 * g + e;
-                S.w1[u][s][e] = f < QN_D ? WH[L::oW1T + qn_w1<H>(j, f)] : (h16)0.0f;
-            }
-#pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const int c = 32 * s + 8 * g + e;
-                S.w2[u][s][e] = WH[L::oW2T + qn_wt(j, c, H)];
-                S.w2b[u][s][e] = WH[L::oW2T + qn_wt(c, j, H)];
-            }
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int k = 16 * t + 4 * g + e;
-            S.b1[u][e] = WH[L::ob1 + k];
-            S.b2[u][e] = WH[L::ob1 + H + k];
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < 4; e++) S.b3[e] = WH[L::ob1 + 2 * H + e];
-}
-
-template <bool QSTATS>
-__global__ void __launch_bounds__(NTH, 1) k_shared_grad6(dmdqn_learn_args a, const float *y_in,
-                                                       const uint8_t *act_in, float *slab) {
-    constexpr int RH = 4;  // row tiles per pass of L1 / L2 / dH1
-    __shared__ __attribute__((aligned(16))) char smem[LDS];
-    h16 *H1I = reinterpret_cast<h16 *>(smem + OFF_H1), *Z2I = reinterpret_cast<h16 *>(smem + OFF_Z2);
-    h16 *H2I = reinterpret_cast<h16 *>(smem + OFF_H2), *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
-    h16 *W3I = reinterpret_cast<h16 *>(smem + OFF_W3);
-    float *sloss = reinterpret_cast<float *>(smem + OFF_SC);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
-    WSlice6 W;
-    load_slice6(WH, w, W);
-    for (int k = threadIdx.x; k < W3ROWS * H; k += NTH)
-        W3I[(k / H) * W3LD + (k % H)] = WH[L::oW3T + (k & (NACT * H - 1))];
-    half8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
-    // G1[u][f]: dW1 of own tile u, feature tile f; G2[u][j]: dW2 of own k tile u,
-    // fan-in tile j; G3[u]: dW3 rows of own tile u
-    f32x4 G1[2][6], G2[2][8], G3[2], GB1[2], GB2[2], GB3;
-    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-#pragma unroll
-        for (int f = 0; f < 6; f++) G1[u][f] = z4;
-#pragma unroll
-        for (int j = 0; j < 8; j++) G2[u][j] = z4;
-        G3[u] = GB1[u] = GB2[u] = z4;
-    }
-    GB3 = z4;
-    for (int k = threadIdx.x; k < B_ * 16; k += NTH) DQI[k] = (h16)0.0f;
-    int wv = w;
-    asm volatile("" : "+v"(wv));
-    const int bR = hoff(i, 8 * g), bX = hoff<DP>(i, 8 * g);
-    const int trH[2] = {hsplit(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    const int trX[2] = {hsplit<DP>(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit<DP>(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    // own column tiles 2w (u = 0, image columns 32w..+15) and 2w + 1 (32w+16..):
-    // the two share the 32-column block 32w and differ in the XOR'd chunk bits
-    const int bW[2] = {hoff(i, 4 * g) + 256 * wv, hoff(i, 16 + 4 * g) + 256 * wv};
-    const int trO[2] = {trH[0] + 256 * wv, trH[1] + 256 * wv};
-    int agent = blockIdx.x;
-    if (agent < a.NA) {
-        gx::XRows x0;
-        gx::xrows_issue<NTH>(a, agent, gx::pos3(a, agent, threadIdx.x), threadIdx.x, x0);
-        gx::xrows_commit(x0, reinterpret_cast<h16 *>(smem + OFF_X), threadIdx.x);
-    }
-    int npos = gx::pos3(a, agent + gridDim.x, threadIdx.x);
-    float yv[2] = {0.0f, 0.0f};
-    int avl[2] = {0, 0};
-    if (agent < a.NA) {
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            yv[u] = y_in[(size_t)agent * B_ + 32 * w + 16 * u + i];
-            avl[u] = act_in[(size_t)agent * B_ + 32 * w + 16 * u + i];
-        }
-    }
-    __syncthreads();
-    int buf = 0;
-    for (; agent < a.NA; agent += gridDim.x, buf ^= 1) {
-        SH_STAMP(agent, 0, threadIdx.x);
-        const h16 *X = reinterpret_cast<const h16 *>(smem + OFF_X + buf * X_BYTES);
-        const int nxt = agent + gridDim.x;
-        gx::XRows xn;
-        float yn[2] = {0.0f, 0.0f};
-        int an[2] = {0, 0};
-        if (nxt < a.NA) {
-            gx::xrows_issue<NTH>(a, nxt, npos, threadIdx.x, xn);
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                yn[u] = y_in[(size_t)nxt * B_ + 32 * w + 16 * u + i];
-                an[u] = act_in[(size_t)nxt * B_ + 32 * w + 16 * u + i];
-            }
-        }
-        npos = gx::pos3(a, nxt + gridDim.x, threadIdx.x);
-        // ---- L1: own tiles, row tiles in passes of RH -> H1 image
-#pragma unroll
-        for (int hf = 0; hf < 8 / RH; hf++) {
-            f32x4 c[2][RH];
-#pragma unroll
-            for (int r = 0; r < RH; r++) c[0][r] = c[1][r] = z4;
-#pragma unroll
-            for (int s = 0; s < 3; s++) {
-                half8 xb[RH];
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    xb[r] = *reinterpret_cast<const half8 *>(X + bX + 16 * DP * (RH * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < RH; r++) {
-                    c[0][r] = mfma(W.w1[0][s], xb[r], c[0][r]);
-                    c[1][r] = mfma(W.w1[1][s], xb[r], c[1][r]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 2; u++)
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    *reinterpret_cast<half4v *>(H1I + bW[u] + 16 * H * (RH * hf + r)) =
-                        gx::relu4(c[u][r], W.b1[u]);
-        }
-        SH_STAMP(agent, 1, threadIdx.x);
-        __syncthreads();  // B1: H1 image
-        // ---- L2: own tiles -> H2 image
-#pragma unroll
-        for (int hf = 0; hf < 8 / RH; hf++) {
-            f32x4 c[2][RH];
-#pragma unroll
-            for (int r = 0; r < RH; r++) c[0][r] = c[1][r] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 hb[RH];
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    hb[r] = *reinterpret_cast<const half8 *>(H1I + bR + 16 * H * (RH * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < RH; r++) {
-                    c[0][r] = mfma(W.w2[0][s], hb[r], c[0][r]);
-                    c[1][r] = mfma(W.w2[1][s], hb[r], c[1][r]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 2; u++)
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    *reinterpret_cast<half4v *>(H2I + bW[u] + 16 * H * (RH * hf + r)) =
-                        gx::relu4(c[u][r], W.b2[u]);
-        }
-        SH_STAMP(agent, 2, threadIdx.x);
-        __syncthreads();  // B2: H2 image
-        // ---- RQ: row tiles 2w + u (rows 32w + 16u + i), as grad4's RQ per tile
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int rt = 2 * wv + u, row = 16 * rt + i;
-            half8 h2r[4];
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                h2r[s] = *reinterpret_cast<const half8 *>(H2I + bR + 16 * H * rt + 256 * s);
-            f32x4 cq = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                cq = mfma(*reinterpret_cast<const half8 *>(W3I + (i % W3ROWS) * W3LD + 32 * s + 8 * g),
-                          h2r[s], cq);
-            float q[4];
-#pragma unroll
-            for (int e = 0; e < 4; e++) q[e] = r16(r16(cq[e]) + (float)W.b3[e]);
-            const float qa = gx::pickf4(q[0], q[1], q[2], q[3], avl[u]);
-            float term, dq;
-            row_loss(a.loss_kind, __fsub_rn(qa, yv[u]), term, dq);
-            dq = r16(dq);
-            if (g == 0) {
-                half4v d;
-#pragma unroll
-                for (int e = 0; e < 4; e++) d[e] = e == avl[u] ? (h16)dq : (h16)0.0f;
-                *reinterpret_cast<half4v *>(DQI + row * 16) = d;
-            }
-            if (QSTATS) {
-                const float s1 = row16_sum((q[0] + q[1]) + (q[2] + q[3]));
-                const float s2 = row16_sum((q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]));
-                if (l == 0) {
-                    atomicAdd(a.qstats + (size_t)agent * 6 + 0, s1);
-                    atomicAdd(a.qstats + (size_t)agent * 6 + 1, s2);
-                }
-#pragma unroll
-                for (int e = 0; e < NACT; e++) {
-                    const float cnt = (float)__popcll(__ballot(g == 0 && avl[u] == e));
-                    if (l == 0) atomicAdd(a.qstats + (size_t)agent * 6 + 2 + e, cnt);
-                }
-            }
-            term = row16_sum(term);
-            if (l == 0) sloss[2 * w + u] = term;
-            half8 w3[4];
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                w3[s] = *reinterpret_cast<const half8 *>(W3I + avl[u] * W3LD + 32 * s + 8 * g);
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 o;
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                    o[e] = h2r[s][e] > (h16)0.0f ? (h16)(dq * (float)w3[s][e]) : (h16)0.0f;
-                *reinterpret_cast<half8 *>(Z2I + bR + 16 * H * rt + 256 * s) = o;
-            }
-        }
-        if (nxt < a.NA)
-            gx::xrows_commit(xn, reinterpret_cast<h16 *>(smem + OFF_X + (buf ^ 1) * X_BYTES), threadIdx.x);
-        SH_STAMP(agent, 3, threadIdx.x);
-        __syncthreads();  // B3: DQ, dZ2 image, loss partials, next X
-        if (threadIdx.x == 0 && a.loss) {
-            float ls = sloss[0];
-            for (int v = 1; v < 8; v++) ls += sloss[v];
-            a.loss[agent] = ls / (float)B_;
-        }
-        // ---- dW3 (own k tiles) and db3 (wave 0)
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const half8 dqf = frag_tr(DQI, 16, 32 * s, 0);
-#pragma unroll
-            for (int u = 0; u < 2; u++) G3[u] = mfma(frag_tr_p(H2I + trO[u] + 2 * 16 * H * s), dqf, G3[u]);
-            if (w == 0) GB3 = mfma(ones, dqf, GB3);
-        }
-        SH_STAMP(agent, 4, threadIdx.x);
-        // ---- dH1 (own j tiles) -> dZ1 own -> image (over the wave's H2 columns)
-#pragma unroll
-        for (int hf = 0; hf < 8 / RH; hf++) {
-            f32x4 c[2][RH];
-#pragma unroll
-            for (int r = 0; r < RH; r++) c[0][r] = c[1][r] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 zb[RH];
-#pragma unroll
-                for (int r = 0; r < RH; r++)
-                    zb[r] = *reinterpret_cast<const half8 *>(Z2I + bR + 16 * H * (RH * hf + r) + 256 * s);
-#pragma unroll
-                for (int r = 0; r < RH; r++) {
-                    c[0][r] = mfma(W.w2b[0][s], zb[r], c[0][r]);
-                    c[1][r] = mfma(W.w2b[1][s], zb[r], c[1][r]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 2; u++)
-#pragma unroll
-                for (int r = 0; r < RH; r++) {
-                    const int rt = RH * hf + r;
-                    half4v o;
-                    const half4v hv = *reinterpret_cast<const half4v *>(H1I + bW[u] + 16 * H * rt);
-#pragma unroll
-                    for (int e = 0; e < 4; e++) o[e] = hv[e] > (h16)0.0f ? (h16)c[u][r][e] : (h16)0.0f;
-                    *reinterpret_cast<half4v *>(H2I + bW[u] + 16 * H * rt) = o;
-                }
-        }
-        SH_STAMP(agent, 5, threadIdx.x);
-        // ---- dW2[j][k] (k = own tiles, j = all 8 tiles) and db2
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            half8 bq[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                bq[u] = frag_tr_p(Z2I + trO[u] + 2 * 16 * H * s);
-                GB2[u] = mfma(ones, bq[u], GB2[u]);
-            }
-#pragma unroll
-            for (int jt = 0; jt < 8; jt++) {
-                const half8 av = frag_tr_p(H1I + trH[jt & 1] + 256 * (jt >> 1) + 2 * 16 * H * s);
-                G2[0][jt] = mfma(av, bq[0], G2[0][jt]);
-                G2[1][jt] = mfma(av, bq[1], G2[1][jt]);
-            }
-        }
-        // ---- dW1[f][j] (j = own tiles: the wave's own dZ1 columns, written above) and db1
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            half8 bv[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                bv[u] = frag_tr_p(H2I + trO[u] + 2 * 16 * H * s);
-                GB1[u] = mfma(ones, bv[u], GB1[u]);
-            }
-#pragma unroll
-            for (int ft = 0; ft < 6; ft++) {
-                const half8 xv = frag_tr_p(X + trX[ft & 1] + 256 * (ft >> 1) + 2 * 16 * DP * s);
-                G1[0][ft] = mfma(xv, bv[0], G1[0][ft]);
-                G1[1][ft] = mfma(xv, bv[1], G1[1][ft]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            yv[u] = yn[u];
-            avl[u] = an[u];
-        }
-        SH_STAMP(agent, 6, threadIdx.x);
-        __syncthreads();  // B4: the images are rewritten by the next agent
-        SH_STAMP(agent, 7, threadIdx.x);
-    }
-    // partial sums of this workgroup, kernel layout (every index written once)
-    float *G = slab + (size_t)blockIdx.x * L::P;
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int n0 = 16 * (2 * w + u), n = n0 + i;  // this lane's neuron (C-tile column)
-        if (i < NACT)
-            *reinterpret_cast<float4 *>(G + L::oW3T + i * H + n0 + 4 * g) =
-                make_float4(G3[u][0], G3[u][1], G3[u][2], G3[u][3]);
-#pragma unroll
-        for (int jt = 0; jt < 8; jt++)
-            *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(n, 16 * jt + 4 * g, H)) =
-                make_float4(G2[u][jt][0], G2[u][jt][1], G2[u][jt][2], G2[u][jt][3]);
-#pragma unroll
-        for (int ft = 0; ft < 6; ft++) {
-            if (ft < 5 || g < 2)
-                *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(n, 16 * ft + 4 * g)) =
-                    make_float4(G1[u][ft][0], G1[u][ft][1], G1[u][ft][2], G1[u][ft][3]);
-            if (ft == 5 && g == 2) G[L::oW1X + n] = G1[u][ft][0];  // feature 88
-        }
-        if (g == 0) {
-            G[L::ob2 + n] = GB2[u][0];
-            G[L::ob1 + n] = GB1[u][0];
-        }
-    }
-    if (w == 0 && g == 0 && i < NACT) G[L::ob3 + i] = GB3[0];
-}
-
-}  // namespace g6
 
 
 
@@ -1326,13 +969,8 @@ int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *s
     const int next_blocks = next_wg < n_slabs ? next_wg : n_slabs;
     hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(64 * NEXT_WAVES), 0, s, *a, y, act);
     DMDQN_LAUNCH_CHECK("k_shared_next");
-#if SH_GRAD == 6
-    auto k = a->qstats ? g6::k_shared_grad6<true> : g6::k_shared_grad6<false>;
-    hipLaunchKernelGGL(k, dim3(n_slabs), dim3(g6::NTH), 0, s, *a, y, act, slab);
-#else
     auto k = a->qstats ? g4::k_shared_grad4<true> : g4::k_shared_grad4<false>;
     hipLaunchKernelGGL(k, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
-#endif
     DMDQN_LAUNCH_CHECK("k_shared_grad");
     return DMDQN_OK;
 }
