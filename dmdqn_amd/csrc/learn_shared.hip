@@ -157,38 +157,74 @@ __device__ __forceinline__ Net net_at(char *p) {
 }
 
 // Stage one network from its f16 device-layout copy WH (qnet_layout.hpp) into
-// LDS at p.  Every thread of the block takes part; the caller syncs.
+// LDS at p.  Every thread of the (NTH-thread) block takes part; the caller
+// syncs.  Vector loads (an aligned group of 8 fan-in values is 16 contiguous
+// bytes, a kperm run of 4 is 8), every one issued before the LDS stores and
+// none under a branch (a per-element gather with a wait per entry made the
+// prologue ~14 serial L2 round trips long).
+template <int NTH>
 __device__ void stage_net(const h16 *WH, char *p) {
-    const int nt = blockDim.x;
+    constexpr int N1 = 8 * 3 * 64, N2 = 8 * 4 * 64;
+    static_assert(N1 % NTH == 0 && N2 % NTH == 0, "stage_net: whole entries per thread");
     half8 *w1 = reinterpret_cast<half8 *>(p);
     half8 *w2 = reinterpret_cast<half8 *>(p + W1_BYTES);
     half8 *w3 = reinterpret_cast<half8 *>(p + W1_BYTES + W2_BYTES);
     h16 *bb = reinterpret_cast<h16 *>(p + W1_BYTES + W2_BYTES + W3_BYTES);
-    for (int ent = threadIdx.x; ent < 8 * 3 * 64; ent += nt) {
+    const int tid = threadIdx.x;
+    half8 v1[N1 / NTH];
+    half4v v2[N2 / NTH][2];
+#pragma unroll
+    for (int k = 0; k < N1 / NTH; k++) {
+        const int ent = tid + NTH * k;
         const int t = ent / 192, s = (ent / 64) % 3, l = ent & 63, i = l & 15, g = l >> 4;
-        half8 v;
+        const int n = 16 * t + i;
+        const bool tile = s < 2 || g < 3;  // features 88..95: only 88 exists (the column)
+        const half8 x = *reinterpret_cast<const half8 *>(WH + L::oW1T + qn_w1<H>(n, 32 * s + 8 * (tile ? g : 2)));
+        const h16 c = WH[L::oW1X + n];
+        v1[k][0] = tile ? x[0] : c;
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            const int k = 32 * s + 8 * g + e;
-            v[e] = k < QN_D ? WH[L::oW1T + qn_w1<H>(16 * t + i, k)] : (h16)0.0f;
-        }
-        w1[ent] = v;
+        for (int e = 1; e < 8; e++) v1[k][e] = tile ? x[e] : (h16)0.0f;
     }
-    for (int ent = threadIdx.x; ent < 8 * 4 * 64; ent += nt) {
+#pragma unroll
+    for (int k = 0; k < N2 / NTH; k++) {
+        const int ent = tid + NTH * k;
         const int t = ent / 256, s = (ent / 64) & 3, l = ent & 63, i = l & 15, g = l >> 4;
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+            v2[k][h] = *reinterpret_cast<const half4v *>(WH + L::oW2T + qn_wt(16 * t + i, kperm(s, g, 4 * h), H));
+    }
+    // W3 (64 entries) and the biases (264 halves): threads tid < 64 / tid < 264,
+    // loads at clamped (valid) addresses by every thread, stores masked
+    const int e3 = tid & 63, s3 = e3 >> 4, g3 = (e3 >> 2) & 3, i3 = e3 & 3;
+    half4v v3[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+        v3[h] = *reinterpret_cast<const half4v *>(WH + L::oW3T + i3 * H + kperm(s3, g3, 4 * h));
+    const int jb = tid < 2 * H + NACT ? tid : 0;
+    const h16 vb = WH[L::ob1 + jb];
+#pragma unroll
+    for (int k = 0; k < N1 / NTH; k++) w1[tid + NTH * k] = v1[k];
+#pragma unroll
+    for (int k = 0; k < N2 / NTH; k++) {
         half8 v;
 #pragma unroll
-        for (int e = 0; e < 8; e++) v[e] = WH[L::oW2T + qn_wt(16 * t + i, kperm(s, g, e), H)];
-        w2[ent] = v;
+        for (int e = 0; e < 4; e++) {
+            v[e] = v2[k][0][e];
+            v[e + 4] = v2[k][1][e];
+        }
+        w2[tid + NTH * k] = v;
     }
-    for (int ent = threadIdx.x; ent < 4 * 4 * 4; ent += nt) {
-        const int s = ent >> 4, g = (ent >> 2) & 3, i = ent & 3;
+    if (tid < 64) {
         half8 v;
 #pragma unroll
-        for (int e = 0; e < 8; e++) v[e] = WH[L::oW3T + i * H + kperm(s, g, e)];
-        w3[ent] = v;
+        for (int e = 0; e < 4; e++) {
+            v[e] = v3[0][e];
+            v[e + 4] = v3[1][e];
+        }
+        w3[tid] = v;
     }
-    for (int j = threadIdx.x; j < 2 * H + NACT; j += nt) bb[j] = WH[L::ob1 + j];
+    if (tid < 2 * H + NACT) bb[tid] = vb;
+    static_assert(NTH >= 2 * H + NACT, "stage_net: one bias per thread");
 }
 
 // Diagnostics (tools/stamp_shared.py): when a stamps buffer is passed, lane 0
@@ -353,8 +389,8 @@ __device__ __forceinline__ int ring_slot(const dmdqn_learn_args &a, int pos) {
 __global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_args a, float *y_out,
                                                         uint8_t *act_out) {
     __shared__ __attribute__((aligned(16))) char smem[NEXT_LDS];
-    stage_net(reinterpret_cast<const h16 *>(a.params_h), smem);
-    stage_net(reinterpret_cast<const h16 *>(a.target_h), smem + NET_BYTES);
+    stage_net<64 * NEXT_WAVES>(reinterpret_cast<const h16 *>(a.params_h), smem);
+    stage_net<64 * NEXT_WAVES>(reinterpret_cast<const h16 *>(a.target_h), smem + NET_BYTES);
     __syncthreads();
     const Net on = net_at(smem), tg = net_at(smem + NET_BYTES);
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
