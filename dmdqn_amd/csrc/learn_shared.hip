@@ -335,7 +335,9 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
             bn = bias4(N.b2, t + 1);
         } else {
 #pragma unroll
-            for (int s = 0; s < 4; s++) nxt[s] = i < NACT ? N.w3[(s * 4 + g) * 4 + i] : zero8();
+            // lanes i >= 4 read row i & 3 (rows 4..15 of A only feed rows 4..15 of
+            // the product, which no lane uses): no zero fill, no masked read
+            for (int s = 0; s < 4; s++) nxt[s] = N.w3[(s * 4 + g) * 4 + (i & (NACT - 1))];
         }
         f32x4 c[NT];
 #pragma unroll
@@ -358,22 +360,24 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
     for (int s = 0; s < 4; s++)  // layer 3 (cur = W3 fragments)
 #pragma unroll
         for (int n = 0; n < NT; n++) c[n] = mfma(cur[s], hb2[n][s], c[n]);
+    // Q = h16(h16(acc) + b3) (a packed f16 add is the f32 add rounded once);
+    // meaningful on lanes g = 0 (the callers read only those)
+    const half4v b3 = *reinterpret_cast<const half4v *>(N.b3);
 #pragma unroll
     for (int n = 0; n < NT; n++)
-#pragma unroll
-        for (int e = 0; e < 4; e++) q[n][e] = g == 0 ? r16(r16(c[n][e]) + (float)N.b3[e]) : 0.0f;
+        q[n] = __builtin_convertvector(__builtin_convertvector(c[n], half4v) + b3, f32x4);
 }
 
 // ---------------------------------------------------------------- pass 1: S'
 // LDS: both nets (2 x 58,896 B) + per wave: rewards f64 [128], ring slots
-// [128], transition word (a | done << 8) [128].
+// [128], transition word (a | done << 8) [128], z-scored rewards f32 [128].
 #ifndef NEXT_NT
 #define NEXT_NT 2  // 16-row tiles per weight read in k_shared_next
 #endif
 #ifndef NEXT_WAVES
 #define NEXT_WAVES 8  // waves (agents in flight) per k_shared_next workgroup
 #endif
-constexpr int NEXT_WAVE_BYTES = B_ * 8 + B_ * 4 + B_ * 4;
+constexpr int NEXT_WAVE_BYTES = B_ * 8 + B_ * 4 + B_ * 4 + B_ * 4;  // + the z-scored rewards
 constexpr int NEXT_LDS = 2 * NET_BYTES + NEXT_WAVES * NEXT_WAVE_BYTES;
 static_assert(NEXT_LDS <= 160 * 1024, "k_shared_next LDS");
 
@@ -398,6 +402,7 @@ __global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_
     double *r64 = reinterpret_cast<double *>(wsc);
     int *slots = reinterpret_cast<int *>(wsc + B_ * 8);
     uint32_t *tw = reinterpret_cast<uint32_t *>(wsc + B_ * 12);
+    float *rnf = reinterpret_cast<float *>(wsc + B_ * 16);
     const int stride = gridDim.x * NEXT_WAVES;
     int agent = blockIdx.x * NEXT_WAVES + w;
     constexpr int RT = 16 * NEXT_NT;
@@ -469,6 +474,12 @@ __global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_
                                                                     __dadd_rn(p[6], p[7])))),
                                  128.0)),
             1e-8);
+        // the z-scored rewards of rows l and l + 64, by every lane (one f64
+        // division per lane and row instead of per row in each tile's epilogue)
+        rnf[l] = (float)__ddiv_rn(__dsub_rn(r64[l], mean), sd);
+        rnf[l + 64] = (float)__ddiv_rn(__dsub_rn(r64[l + 64], mean), sd);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the stores landed
+        __builtin_amdgcn_wave_barrier();
         SH_STAMP(agent, 11, l);
 #pragma unroll 1
         for (int rp = 0; rp < B_ / RT; rp++) {  // RT rows: NEXT_NT tiles share every weight read
@@ -495,7 +506,7 @@ __global__ void __launch_bounds__(64 * NEXT_WAVES, 1) k_shared_next(dmdqn_learn_
                     if (qo[n][3] > bq) { best = 3; }
                     const float tq = best == 0 ? qt[n][0] : best == 1 ? qt[n][1] : best == 2 ? qt[n][2] : qt[n][3];
                     const uint32_t m = tw[b];
-                    const float rn = (float)__ddiv_rn(__dsub_rn(r64[b], mean), sd);
+                    const float rn = rnf[b];
                     const float dn = ((m >> 8) & 0xffu) ? 1.0f : 0.0f;
                     const float gd = __fmul_rn(a.gamma, __fsub_rn(1.0f, dn));
                     y_out[(size_t)agent * B_ + b] = __fadd_rn(rn, __fmul_rn(gd, tq));
