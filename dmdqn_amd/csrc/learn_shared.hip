@@ -165,17 +165,17 @@ __device__ __forceinline__ Net net_at(char *p) {
 template <int NTH>
 __device__ void stage_net(const h16 *WH, char *p) {
     constexpr int N1 = 8 * 3 * 64, N2 = 8 * 4 * 64;
-    static_assert(N1 % NTH == 0 && N2 % NTH == 0, "stage_net: whole entries per thread");
+    constexpr int K1 = (N1 + NTH - 1) / NTH, K2 = (N2 + NTH - 1) / NTH;  // entries per thread
     half8 *w1 = reinterpret_cast<half8 *>(p);
     half8 *w2 = reinterpret_cast<half8 *>(p + W1_BYTES);
     half8 *w3 = reinterpret_cast<half8 *>(p + W1_BYTES + W2_BYTES);
     h16 *bb = reinterpret_cast<h16 *>(p + W1_BYTES + W2_BYTES + W3_BYTES);
     const int tid = threadIdx.x;
-    half8 v1[N1 / NTH];
-    half4v v2[N2 / NTH][2];
+    half8 v1[K1];
+    half4v v2[K2][2];
 #pragma unroll
-    for (int k = 0; k < N1 / NTH; k++) {
-        const int ent = tid + NTH * k;
+    for (int k = 0; k < K1; k++) {
+        const int ent = min(tid + NTH * k, N1 - 1);  // (a clamped entry is loaded, not stored)
         const int t = ent / 192, s = (ent / 64) % 3, l = ent & 63, i = l & 15, g = l >> 4;
         const int n = 16 * t + i;
         const bool tile = s < 2 || g < 3;  // features 88..95: only 88 exists (the column)
@@ -186,8 +186,8 @@ __device__ void stage_net(const h16 *WH, char *p) {
         for (int e = 1; e < 8; e++) v1[k][e] = tile ? x[e] : (h16)0.0f;
     }
 #pragma unroll
-    for (int k = 0; k < N2 / NTH; k++) {
-        const int ent = tid + NTH * k;
+    for (int k = 0; k < K2; k++) {
+        const int ent = min(tid + NTH * k, N2 - 1);
         const int t = ent / 256, s = (ent / 64) & 3, l = ent & 63, i = l & 15, g = l >> 4;
 #pragma unroll
         for (int h = 0; h < 2; h++)
@@ -203,9 +203,11 @@ __device__ void stage_net(const h16 *WH, char *p) {
     const int jb = tid < 2 * H + NACT ? tid : 0;
     const h16 vb = WH[L::ob1 + jb];
 #pragma unroll
-    for (int k = 0; k < N1 / NTH; k++) w1[tid + NTH * k] = v1[k];
+    for (int k = 0; k < K1; k++)
+        if (N1 % NTH == 0 || tid + NTH * k < N1) w1[tid + NTH * k] = v1[k];
 #pragma unroll
-    for (int k = 0; k < N2 / NTH; k++) {
+    for (int k = 0; k < K2; k++) {
+        if (N2 % NTH != 0 && tid + NTH * k >= N2) continue;
         half8 v;
 #pragma unroll
         for (int e = 0; e < 4; e++) {
