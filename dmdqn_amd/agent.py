@@ -57,6 +57,9 @@ _lib.register({
     "dmdqn_adam": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                    C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
                    C.c_int, C.c_void_p],
+    "dmdqn_adam_slabs": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                         C.c_void_p, C.c_int, C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_float,
+                         C.c_float, C.c_float, C.c_float, C.c_int, C.c_void_p],
     "dmdqn_target_sync": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                           C.c_void_p],
 })
@@ -573,13 +576,21 @@ class BatchedDQN:
         all-reduced (sum, RCCL) across ranks, then one Adam step with 1/world."""
         import torch.distributed as dist
         ring, cfg = self.ring, self.cfg
-        self._ops.learn_shared_grad(ring.s, ring.n, ring.a, ring.d, ring.r, self.idx, self.params,
-                                    self.target, self.target_h, self.params_h, self.loss,
-                                    ring.start, cfg.gamma, LOSSES[cfg.loss], qstats, self.rn_out,
-                                    self.slab, self.grad, 1.0 / self.NA, work=self.shared_work)
         world = 1
         if dist.is_available() and dist.is_initialized():
             world = dist.get_world_size()
+        # one rank: the slab reduction and the Adam step as one launch
+        # (dmdqn_adam_slabs, the same bits); more ranks: reduce, all-reduce, Adam
+        self._ops.learn_shared_grad(ring.s, ring.n, ring.a, ring.d, ring.r, self.idx, self.params,
+                                    self.target, self.target_h, self.params_h, self.loss,
+                                    ring.start, cfg.gamma, LOSSES[cfg.loss], qstats, self.rn_out,
+                                    self.slab, self.grad if world > 1 else None, 1.0 / self.NA,
+                                    work=self.shared_work)
+        if world == 1:
+            self._ops.adam_slabs(self.params, self.adam_m, self.adam_v, self.target, self.target_h,
+                                 self.params_h, self.slab, self.grad, 1.0 / self.NA, 1.0, alpha,
+                                 c1, c2, eps, sync)
+            return
         if world > 1:
             # one flat 114 KB buffer per learn, bounded (dist.BoundedAllReduce:
             # the host runs a few learns ahead; a stalled peer raises DistError)

@@ -76,7 +76,7 @@ extern "C" int dmdqn_get_option(int opt) {
 }
 
 extern "C" const char *dmdqn_last_error(void) { return dmdqn::g_err; }
-extern "C" int dmdqn_version(void) { return 2; }  // include/dmdqn.h
+extern "C" int dmdqn_version(void) { return 3; }  // include/dmdqn.h
 
 // A HIP stream whose kernels run only on the CUs set in `mask` (n_words
 // 32-bit words, CU i = bit i % 32 of word i / 32): the trainer's side stream

@@ -26,6 +26,7 @@ ENTRY_POINTS = {
     "dmdqn_learn_grad": "learn_step", "dmdqn_adam_agents": "learn_step",
     "dmdqn_replay_store_f32": "replay_store_f32", "dmdqn_replay_gather_f32": "replay_gather_f32",
     "dmdqn_learn_shared_grad": "learn_shared_grad", "dmdqn_adam": "adam",
+    "dmdqn_adam_slabs": "adam_slabs",
     "dmdqn_target_sync": "target_sync", "dmdqn_q_argmax": "q_argmax",
     "dmdqn_q_argmax_shared": "q_argmax",
 }

@@ -392,7 +392,7 @@ void learn_shared_grad(const Tensor &ring_s, const Tensor &ring_n, const Tensor 
                        const Tensor &params, const Tensor &target, const Tensor &target_h,
                        const Tensor &params_h, Tensor &loss, int64_t start, double gamma,
                        int64_t loss_kind, const OptT &qstats, const OptT &rn_out, Tensor &slab,
-                       Tensor &grad, double scale, const OptT &work) {
+                       const OptT &grad, double scale, const OptT &work) {
     const int64_t NA = loss.numel();
     Tensor p = params, t = target;  // read-only here: the Adam step is a separate op
     dmdqn_learn_args a = make_learn(ring_s, ring_n, ring_a, ring_d, ring_r, idx, p, std::nullopt,
@@ -402,7 +402,7 @@ void learn_shared_grad(const Tensor &ring_s, const Tensor &ring_n, const Tensor 
     TORCH_CHECK(slab.numel() % a.P == 0, "slab must be [n_slabs, P]");
     const int n_slabs = (int)(slab.numel() / a.P);
     auto sl = dptr<float>(slab, at::kFloat, "slab");
-    auto gr = dptr<float>(grad, at::kFloat, "grad", a.P);
+    auto gr = optr<float>(grad, at::kFloat, "grad", a.P);  // None: dmdqn_adam_slabs reduces
     auto wk = optr<uint8_t>(work, at::kByte, "work",
                             (int64_t)dmdqn_learn_shared_work_bytes((int)NA));
     c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
@@ -425,6 +425,26 @@ void adam(Tensor &params, Tensor &adam_m, Tensor &adam_v, Tensor &target, const 
                      int32_of(n, "n"), (float)gscale, (float)alpha, (float)c1, (float)c2,
                      (float)eps, sync ? 1 : 0, stream_of(params)),
           "dmdqn_adam");
+}
+
+void adam_slabs(Tensor &params, Tensor &adam_m, Tensor &adam_v, Tensor &target,
+                const OptT &target_h, const OptT &params_h, const Tensor &slab, Tensor &grad,
+                double scale, double gscale, double alpha, double c1, double c2, double eps,
+                bool sync) {
+    const int64_t n = params.numel();
+    auto w = dptr<float>(params, at::kFloat, "params");
+    auto m = dptr<float>(adam_m, at::kFloat, "adam_m", n);
+    auto v = dptr<float>(adam_v, at::kFloat, "adam_v", n);
+    auto t = dptr<float>(target, at::kFloat, "target", n);
+    auto gr = dptr<float>(grad, at::kFloat, "grad", n);
+    TORCH_CHECK(slab.numel() % n == 0, "slab must be [n_slabs, P]");
+    auto sl = dptr<float>(slab, at::kFloat, "slab");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
+    check(dmdqn_adam_slabs(w, m, v, t, h16ptr(target_h, "target_h", 1, n),
+                           h16ptr(params_h, "params_h", 1, n), sl, int32_of(slab.numel() / n, "n_slabs"),
+                           gr, (float)scale, int32_of(n, "n"), (float)gscale, (float)alpha,
+                           (float)c1, (float)c2, (float)eps, sync ? 1 : 0, stream_of(params)),
+          "dmdqn_adam_slabs");
 }
 
 void target_sync(const Tensor &params, Tensor &target, const OptT &target_h, int64_t precision) {
@@ -488,8 +508,11 @@ void learn_step_meta(const Tensor &, const Tensor &, const Tensor &, const Tenso
 void learn_shared_grad_meta(const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                             const Tensor &, const Tensor &, Tensor &, int64_t, double, int64_t,
-                            const OptT &, const OptT &, Tensor &, Tensor &, double,
+                            const OptT &, const OptT &, Tensor &, const OptT &, double,
                             const OptT &) {}
+void adam_slabs_meta(Tensor &, Tensor &, Tensor &, Tensor &, const OptT &, const OptT &,
+                     const Tensor &, Tensor &, double, double, double, double, double, double,
+                     bool) {}
 void adam_meta(Tensor &, Tensor &, Tensor &, Tensor &, const OptT &, const OptT &, const Tensor &,
                double, double, double, double, double, bool) {}
 void target_sync_meta(const Tensor &, Tensor &, const OptT &, int64_t) {}
@@ -546,8 +569,12 @@ TORCH_LIBRARY(dmdqn, m) {
     m.def("learn_shared_grad(Tensor ring_s, Tensor ring_n, Tensor ring_a, Tensor ring_d, "
           "Tensor ring_r, Tensor idx, Tensor params, Tensor target, Tensor target_h, "
           "Tensor params_h, Tensor(a!) loss, int start, float gamma, int loss_kind, "
-          "Tensor(b!)? qstats, Tensor(c!)? rn_out, Tensor(d!) slab, Tensor(e!) grad, "
+          "Tensor(b!)? qstats, Tensor(c!)? rn_out, Tensor(d!) slab, Tensor(e!)? grad, "
           "float scale, Tensor(f!)? work=None) -> ()");
+    // C5, one rank: the slab reduction and the Keras-3 Adam step in one launch
+    m.def("adam_slabs(Tensor(a!) params, Tensor(b!) adam_m, Tensor(c!) adam_v, Tensor(d!) target, "
+          "Tensor(e!)? target_h, Tensor(f!)? params_h, Tensor slab, Tensor(g!) grad, float scale, "
+          "float gscale, float alpha, float c1, float c2, float eps, bool sync) -> ()");
     // Keras-3 Adam (dqn_agent.py:357, A-11) on a flat gradient
     m.def("adam(Tensor(a!) params, Tensor(b!) adam_m, Tensor(c!) adam_v, Tensor(d!) target, "
           "Tensor(e!)? target_h, Tensor(f!)? params_h, Tensor grad, float gscale, float alpha, "
@@ -574,6 +601,7 @@ TORCH_LIBRARY_IMPL(dmdqn, CUDA, m) {
     m.impl("learn_step", &learn_step);
     m.impl("learn_shared_grad", &learn_shared_grad);
     m.impl("adam", &adam);
+    m.impl("adam_slabs", &adam_slabs);
     m.impl("target_sync", &target_sync);
     m.impl("q_argmax", &q_argmax);
 }
@@ -593,6 +621,7 @@ TORCH_LIBRARY_IMPL(dmdqn, Meta, m) {
     m.impl("learn_step", &learn_step_meta);
     m.impl("learn_shared_grad", &learn_shared_grad_meta);
     m.impl("adam", &adam_meta);
+    m.impl("adam_slabs", &adam_slabs_meta);
     m.impl("target_sync", &target_sync_meta);
     m.impl("q_argmax", &q_argmax_meta);
 }

@@ -52,7 +52,9 @@ extern "C" {
 #define DMDQN_ROWS_F32 1
 
 const char *dmdqn_last_error(void);
-/* ABI version.  2 (round 4/5): the replay ring arguments `cap` of the learn,
+/* ABI version.  3 (round 5): dmdqn_adam_slabs (the slab reduction and the
+ * Adam step of the shared net in one launch) and dmdqn_learn_shared_grad with
+ * grad == NULL (the slabs left for it).  2 (round 4/5): the replay ring arguments `cap` of the learn,
  * gather and store entry points are the PHYSICAL slot count of the ring -- a
  * deque of maxlen N lives in N + 1 slots (position p at slot (start + p) %
  * (N + 1), the next store in the one slot no position maps to), so a caller
@@ -442,7 +444,8 @@ int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, int pr
  * (one workgroup per CU: n_slabs = 256 on MI355X).  precision must be 1.
  * work: device scratch of dmdqn_learn_shared_work_bytes(NA) bytes (each batch
  * row's TD target and action between the kernel's two passes: the S' pass
- * with both nets resident in LDS, then the gradient pass); required. */
+ * with both nets resident in LDS, then the gradient pass); required.
+ * grad == NULL: the slabs are left unreduced for dmdqn_adam_slabs (one rank). */
 int dmdqn_learn_shared_grad(const dmdqn_learn_args *args, float *slab, int n_slabs, float *grad,
                             float scale, void *work, void *stream);
 size_t dmdqn_learn_shared_work_bytes(int NA);
@@ -454,6 +457,16 @@ size_t dmdqn_learn_shared_work_bytes(int NA);
 int dmdqn_adam(float *params, float *adam_m, float *adam_v, float *target, uint16_t *target_h,
                uint16_t *params_h, const float *grad, int n, float gscale, float alpha, float c1,
                float c2, float eps, int sync, void *stream);
+
+/* The slab reduction of dmdqn_learn_shared_grad (grad = scale * sum of the
+ * n_slabs slabs, same order, written to grad) followed by dmdqn_adam on it, in
+ * one launch: for one rank, where no all-reduce comes between the two.  n must
+ * be the shared net's parameter count; results bit-identical to
+ * dmdqn_learn_shared_grad(grad) + dmdqn_adam. */
+int dmdqn_adam_slabs(float *params, float *adam_m, float *adam_v, float *target,
+                     uint16_t *target_h, uint16_t *params_h, const float *slab, int n_slabs,
+                     float *grad, float scale, int n, float gscale, float alpha, float c1,
+                     float c2, float eps, int sync, void *stream);
 
 #ifdef __cplusplus
 }

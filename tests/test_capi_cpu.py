@@ -68,7 +68,7 @@ def test_torch_ops_registered_without_gpu(lib):
 
 
 def test_version_and_error_string(lib):
-    assert lib.dmdqn_version() == 2  # cap = physical ring slots (include/dmdqn.h)
+    assert lib.dmdqn_version() == 3  # dmdqn_adam_slabs; cap = physical ring slots (include/dmdqn.h)
     import ctypes
     lib.dmdqn_learn_shared_work_bytes.restype = ctypes.c_size_t
     assert lib.dmdqn_learn_shared_work_bytes(16384) == 16384 * 128 * 5

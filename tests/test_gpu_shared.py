@@ -120,3 +120,34 @@ def test_shared_many_agents_across_slabs():
     call("dmdqn_learn_shared_grad", C.byref(a), ptr(slab1), 1, ptr(g_one), C.c_float(1.0 / ag.NA),
          ptr(ag.shared_work), stream_of())
     torch.testing.assert_close(g_one, g1, rtol=1e-4, atol=1e-6 * float(g1.abs().max()))
+
+
+def test_shared_fused_reduce_adam_bit_identical_to_separate_launches():
+    """One rank: BatchedDQN's C5 learn reduces the slabs and steps Adam in one
+    launch (dmdqn_adam_slabs).  Same inputs through dmdqn_learn_shared_grad
+    (grad) + dmdqn_adam: every output bit-identical -- gradient, weights, Adam
+    slots, f16 shadow and, on a sync learn, the target and its shadow."""
+    from dmdqn_amd.agent import LOSSES
+    outs = []
+    for fused in (True, False):
+        ag = _shared(3, 4, freq=2, cap=300)
+        _fill(ag, 260, np.random.RandomState(11))
+        for k in range(2):  # learn 2 syncs the target
+            if fused:
+                ag.learn()
+                continue
+            assert ag.learn_begin()
+            alpha, c1, c2, eps, sync, qstats = ag._last_learn
+            ring, cfg = ag.ring, ag.cfg
+            ag._ops.learn_shared_grad(ring.s, ring.n, ring.a, ring.d, ring.r, ag.idx, ag.params,
+                                      ag.target, ag.target_h, ag.params_h, ag.loss, ring.start,
+                                      cfg.gamma, LOSSES[cfg.loss], qstats, ag.rn_out, ag.slab,
+                                      ag.grad, 1.0 / ag.NA, work=ag.shared_work)
+            ag._ops.adam(ag.params, ag.adam_m, ag.adam_v, ag.target, ag.target_h, ag.params_h,
+                         ag.grad, 1.0, alpha, c1, c2, eps, sync)
+        torch.cuda.synchronize()
+        outs.append({n: getattr(ag, n).cpu().clone() for n in
+                     ("grad", "params", "adam_m", "adam_v", "target", "target_h", "params_h",
+                      "loss")})
+    for n in outs[0]:
+        assert torch.equal(outs[0][n], outs[1][n]), n
