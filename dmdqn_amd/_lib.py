@@ -29,6 +29,7 @@ SIGNATURES = {
     "dmdqn_observe": [i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "dmdqn_replay_store": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dmdqn_replay_sample": [vp, i32, i32, i32, i32, vp, vp],
+    "dmdqn_replay_sample_budget": [vp, i32, i32, i32, i32, C.c_size_t, vp, vp],
     "dmdqn_replay_store_f32": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dmdqn_replay_gather_f32": [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp],
     "dmdqn_stream_create_cumask": [u32, vp, vp],
@@ -82,9 +83,16 @@ def load(path=None):
     lib.dmdqn_debug_status.argtypes = []
     lib.dmdqn_debug_build.restype = C.c_int
     lib.dmdqn_debug_build.argtypes = []
+    lib.dmdqn_learn_shared_lds_bytes.restype = C.c_size_t
+    lib.dmdqn_learn_shared_lds_bytes.argtypes = []
     _apply(lib, SIGNATURES)
     _LIB = lib
     return lib
+
+
+def learn_shared_lds_bytes():
+    """LDS of one workgroup of the shared learn's S' pass (include/dmdqn.h)."""
+    return int(load().dmdqn_learn_shared_lds_bytes())
 
 
 def call(name, *args):

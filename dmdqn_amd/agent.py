@@ -541,20 +541,22 @@ class BatchedDQN:
                       None if self._xs is None else self._xs.data_ptr(),
                       None if self._xn is None else self._xn.data_ptr())
 
-    def presample(self, n):
+    def presample(self, n, lds_budget=0):
         """Draw the next learn's replay indices now (ReplayBuffer.sample,
         dqn_agent.py:59-63) for a ring of n transitions, into the index buffer
         the current learn does not read, on the current stream.  The draws
         depend only on the CPython stream and n, never on the ring contents, so
         they may run before the store that brings the ring to n (trainer
-        overlap).  The next learn() must see len(ring) == n."""
+        overlap).  The next learn() must see len(ring) == n.  lds_budget:
+        kernels.replay_sample's (the sampler beside the shared learn)."""
         if n < self.cfg.batch_size:
             return False
         if self._presampled is not None:
             raise RuntimeError("presample called twice before a learn")
         self._idx_i = (self._idx_i + 1) % self.OUT_BUFS
         buf = self._idx_bufs[self._idx_i]
-        K.replay_sample(self.py_state, self.A, n, self.cfg.batch_size, out=buf)
+        K.replay_sample(self.py_state, self.A, n, self.cfg.batch_size, out=buf,
+                        lds_budget=lds_budget)
         self._presampled = (n, buf)
         return True
 

@@ -651,7 +651,8 @@ constexpr int OFF_DQ = OFF_H2 + IMG;              // [128][16]
 constexpr int W3LD = H + 16, W3ROWS = NACT;
 constexpr int OFF_W3 = OFF_DQ + B_ * 16 * 2;
 constexpr int OFF_SC = OFF_W3 + W3ROWS * W3LD * 2;  // sloss [8]
-constexpr int LDS = OFF_SC + 32;
+constexpr int OFF_QS = OFF_SC + 32;                // Q statistics per row tile [8][6]
+constexpr int LDS = OFF_QS + 8 * 6 * 4;
 static_assert(LDS <= 160 * 1024, "k_shared_grad4 LDS");
 static_assert(OFF_W3 % 16 == 0, "aligned W3 image");
 
@@ -709,6 +710,7 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
     h16 *H2I = reinterpret_cast<h16 *>(smem + OFF_H2), *DQI = reinterpret_cast<h16 *>(smem + OFF_DQ);
     h16 *W3I = reinterpret_cast<h16 *>(smem + OFF_W3);
     float *sloss = reinterpret_cast<float *>(smem + OFF_SC);
+    float *sqs = reinterpret_cast<float *>(smem + OFF_QS);
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
     const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
     WSlice4 W;
@@ -850,17 +852,17 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             for (int e = 0; e < 4; e++) d[e] = e == avl ? (h16)dq : (h16)0.0f;
             *reinterpret_cast<half4v *>(DQI + row * 16) = d;
         }
-        if (QSTATS) {
+        if (QSTATS) {  // per row tile into LDS; summed in tile order after B3
             const float s1 = row16_sum((q[0] + q[1]) + (q[2] + q[3]));
             const float s2 = row16_sum((q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]));
             if (l == 0) {
-                atomicAdd(a.qstats + (size_t)agent * 6 + 0, s1);
-                atomicAdd(a.qstats + (size_t)agent * 6 + 1, s2);
+                sqs[w * 6 + 0] = s1;
+                sqs[w * 6 + 1] = s2;
             }
 #pragma unroll
             for (int e = 0; e < NACT; e++) {  // every lane takes part in the ballot
                 const float cnt = (float)__popcll(__ballot(g == 0 && avl == e));
-                if (l == 0) atomicAdd(a.qstats + (size_t)agent * 6 + 2 + e, cnt);
+                if (l == 0) sqs[w * 6 + 2 + e] = cnt;
             }
         }
         term = row16_sum(term);
@@ -888,6 +890,13 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
             float ls = sloss[0];
             for (int v = 1; v < 8; v++) ls += sloss[v];
             a.loss[agent] = ls / (float)B_;
+        }
+        if (QSTATS && threadIdx.x < 6) {
+            // the agent's Q statistics in row-tile order (one writer per agent:
+            // deterministic, unlike float atomics from the eight waves)
+            float t = sqs[threadIdx.x];
+            for (int v = 1; v < 8; v++) t += sqs[v * 6 + threadIdx.x];
+            a.qstats[(size_t)agent * 6 + threadIdx.x] += t;
         }
         // ---- dW3 (own k) and db3 (wave 0)
 #pragma unroll
@@ -1009,6 +1018,10 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
 
 
 }  // namespace shk
+
+// LDS of the S' pass's workgroup (one per CU): what it leaves of a CU's 160 KB
+// is the budget of a sampler block running beside it (include/dmdqn.h).
+extern "C" size_t dmdqn_learn_shared_lds_bytes(void) { return shk::NEXT_LDS; }
 
 // Launch of the two passes (called by dmdqn_learn_shared_grad, learn_f16.hip).
 int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *slab, int n_slabs,

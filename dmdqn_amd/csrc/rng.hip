@@ -396,8 +396,8 @@ extern "C" int dmdqn_act_uniform(uint32_t *np_state, int E, int A, int n_actions
     return DMDQN_OK;
 }
 
-extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int k,
-                                   int32_t *idx, void *stream) {
+extern "C" int dmdqn_replay_sample_budget(uint32_t *py_state, int E, int A, int n, int k,
+                                          size_t lds_budget, int32_t *idx, void *stream) {
     DMDQN_REQUIRE(py_state && idx && E > 0 && A > 0, "dmdqn_replay_sample: bad args");
     DMDQN_REQUIRE(k >= 1 && n >= k, "dmdqn_replay_sample: need 1 <= k <= n (k=%d n=%d)", k, n);
     uint32_t setsize = 21;
@@ -410,12 +410,17 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
     size_t lds = 2 * MT_N * sizeof(uint32_t) + aux_bytes;
     // set branch: the first-lane table, 2^tlog u32 entries: no more than n
     // needs, within 39 KB per block in all (four blocks per CU) when that
-    // leaves at least 4 KB for it, else up to 32 KB; DMDQN_OPT_SAMPLE_TLOG caps
-    // it (tests: collisions in every chunk)
+    // leaves at least 4 KB for it, else up to 32 KB; with lds_budget, within
+    // that (e.g. beside the shared learn's S' pass: the trainer's "learn"
+    // schedule); DMDQN_OPT_SAMPLE_TLOG caps it (tests: collisions in every
+    // chunk).  The table size changes only the speed, never the draws.
     int tlog = 0;
     if (!pool) {
-        const size_t quad = 39 * 1024;
-        const size_t room = (quad >= lds + 4096 + 4) ? quad - lds - 4 : 32 * 1024;
+        const size_t quad = lds_budget ? lds_budget : 39 * 1024;
+        DMDQN_REQUIRE(!lds_budget || quad >= lds + 16 + 4,
+                      "dmdqn_replay_sample: lds_budget %zu below the %zu B the set branch needs",
+                      lds_budget, lds + 20);
+        const size_t room = (quad >= lds + 4096 + 4 || lds_budget) ? quad - lds - 4 : 32 * 1024;
         while (tlog < 20 && ((size_t)4 << (tlog + 1)) <= room && (1u << tlog) < (uint32_t)n) tlog++;
         const int cap = option(DMDQN_OPT_SAMPLE_TLOG);
         if (cap < tlog) tlog = cap;
@@ -432,4 +437,9 @@ extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int 
                        (uint32_t)n, k, idx);
     DMDQN_LAUNCH_CHECK("k_sample");
     return DMDQN_OK;
+}
+
+extern "C" int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int k, int32_t *idx,
+                                   void *stream) {
+    return dmdqn_replay_sample_budget(py_state, E, A, n, k, 0, idx, stream);
 }

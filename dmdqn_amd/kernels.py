@@ -223,10 +223,13 @@ _RANGE_MSG = ("replay_store: an observation value is not an integer in [-128, 12
               "replay rows store this env's features exactly and refuse anything else")
 
 
-def replay_sample(py_state, A, n, k=128, out=None):
+def replay_sample(py_state, A, n, k=128, out=None, lds_budget=0):
+    """ReplayBuffer.sample for E x A agents (dmdqn_replay_sample); lds_budget
+    (bytes, 0 = default) bounds the sampler block's LDS, e.g. to run beside
+    the shared learn (trainer schedule "learn"); the draws do not depend on it."""
     E = py_state.shape[0]
     _check(py_state, torch.int32, (E, MT_WORDS), "py_state")
     if out is None:
         out = torch.empty((E * A, k), dtype=torch.int32, device=py_state.device)
-    _ops().replay_sample(py_state, A, int(n), int(k), out)
+    _ops().replay_sample(py_state, A, int(n), int(k), out, int(lds_budget))
     return out

@@ -21,6 +21,7 @@ ENTRY_POINTS = {
     "dmdqn_mt_draw_u32": "mt_draw_u32", "dmdqn_act": "act", "dmdqn_act_uniform": "act",
     "dmdqn_observe": "observe",
     "dmdqn_replay_store": "replay_store", "dmdqn_replay_sample": "replay_sample",
+    "dmdqn_replay_sample_budget": "replay_sample",
     "dmdqn_sim_reset": "sim_reset", "dmdqn_sim_reset_envs": "sim_reset",
     "dmdqn_sim_step": "sim_step", "dmdqn_env_step": "env_step", "dmdqn_learn": "learn_step",
     "dmdqn_learn_grad": "learn_step", "dmdqn_adam_agents": "learn_step",

@@ -193,13 +193,15 @@ void replay_gather_f32(const Tensor &rows_s, const Tensor &rows_n, const Tensor 
           "dmdqn_replay_gather_f32");
 }
 
-void replay_sample(Tensor &py_state, int64_t A, int64_t n, int64_t k, Tensor &idx) {
+void replay_sample(Tensor &py_state, int64_t A, int64_t n, int64_t k, Tensor &idx,
+                   int64_t lds_budget) {
     const int64_t E = py_state.numel() / MT;
     auto s = dptr<uint32_t>(py_state, at::kInt, "py_state", E * MT);
     auto o = dptr<int32_t>(idx, at::kInt, "idx", E * A * k);
+    TORCH_CHECK(lds_budget >= 0, "lds_budget must be >= 0");
     c10::hip::HIPGuardMasqueradingAsCUDA g(py_state.device());
-    check(dmdqn_replay_sample(s, (int)E, int32_of(A, "A"), int32_of(n, "n"), int32_of(k, "k"), o,
-                              stream_of(py_state)),
+    check(dmdqn_replay_sample_budget(s, (int)E, int32_of(A, "A"), int32_of(n, "n"),
+                                     int32_of(k, "k"), (size_t)lds_budget, o, stream_of(py_state)),
           "dmdqn_replay_sample");
 }
 
@@ -486,7 +488,7 @@ void observe_meta(int64_t, int64_t, const Tensor &, const Tensor &, const Tensor
                   const OptT &, const OptT &, const OptT &, const OptT &) {}
 void replay_store_meta(int64_t, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                        const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &) {}
-void replay_sample_meta(Tensor &, int64_t, int64_t, int64_t, Tensor &) {}
+void replay_sample_meta(Tensor &, int64_t, int64_t, int64_t, Tensor &, int64_t) {}
 void replay_store_f32_meta(int64_t, const Tensor &, const Tensor &, const Tensor &, const Tensor &,
                            const Tensor &, Tensor &, Tensor &, Tensor &, Tensor &, Tensor &) {}
 void replay_gather_f32_meta(const Tensor &, const Tensor &, const Tensor &, int64_t, Tensor &,
@@ -538,7 +540,8 @@ TORCH_LIBRARY(dmdqn, m) {
           "Tensor(a!) ring_s, Tensor(b!) ring_n, Tensor(c!) ring_a, Tensor(d!) ring_r, "
           "Tensor(e!) ring_d, Tensor(f!) err) -> ()");
     // random.sample(self.buffer, k) (dqn_agent.py:63)
-    m.def("replay_sample(Tensor(a!) py_state, int A, int n, int k, Tensor(b!) idx) -> ()");
+    m.def("replay_sample(Tensor(a!) py_state, int A, int n, int k, Tensor(b!) idx, "
+          "int lds_budget=0) -> ()");
     // ReplayBuffer.add / .sample on float rows (the per-agent drop-in, dqn_agent.py:39-64)
     m.def("replay_store_f32(int slot, Tensor obs_s, Tensor obs_n, Tensor act, Tensor rew, "
           "Tensor done, Tensor(a!) rows_s, Tensor(b!) rows_n, Tensor(c!) ring_a, Tensor(d!) ring_r, "

@@ -48,6 +48,13 @@ sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
               side:  ... sample_{t+1} (ev_env) learn_{t+1}[NA-m, NA)
               main:  [wait ev_env] learn_{t+1}[0, NA-m)
 
+  "learn"   the replay draws of step t run on a side stream beside learn t-1
+            (everything else on one stream).  For the shared net (C5): its S'
+            pass leaves room on every CU for a sampler block, so the draws
+            (latency-bound, one block per env) hide behind the learn.
+              side:  [wait env_step_{t-1}] sample_t (ev_s)
+              main:  env_step_t [wait ev_s] learn_t
+
 What a step returns or exposes per step (obs, reward, loss, agent.actions,
 agent.idx) is fresh or double-buffered, so the caller may read it on its own
 stream between steps.  Persistent env/agent state (sim arrays, RNG streams) is
@@ -63,7 +70,8 @@ from .agent import AgentConfig, BatchedDQN
 from .env import EnvConfig, TrafficEnv
 
 
-SCHEDULES = ("none", "sample", "full", "env")
+SCHEDULES = ("none", "sample", "full", "env", "learn")
+LDS_PER_CU = 160 * 1024  # MI355X (gfx950)
 
 
 @dataclass
@@ -88,9 +96,16 @@ class Trainer:
         if overlap != "none":
             self.side = side_stream if side_stream is not None else torch.cuda.Stream(self.env.device)
         self._ev_store = self._ev_learn = None
+        self._ev_env_prev = None  # overlap "learn": the last env step
         self._join = True  # the side stream's first work waits for everything before it
         self.agent = BatchedDQN(self.env.E, self.env.A, agent_cfg or AgentConfig(), device=device,
                                 env_seeds=self.env.seeds)
+        # overlap "learn": the sampler's LDS is what the shared learn's S' pass
+        # leaves of a CU, so one sampler block runs beside each S' workgroup
+        # (with the default four-blocks-per-CU budget the two serialise)
+        self._sampler_lds = 0
+        if overlap == "learn" and self.agent.shared:
+            self._sampler_lds = LDS_PER_CU - _lib.learn_shared_lds_bytes()
         # split_learn (agent.set_split_learn): the learn as two launches so its
         # Adam half can share the chip with the next step's side-stream work
         # (overlap "full").  Off by default: measured at C2 (round 3), the
@@ -147,6 +162,8 @@ class Trainer:
             return self._step_env_beside_learn(collect_stats)
         if self.overlap == "sample":
             return self._step_side_sample(collect_stats)
+        if self.overlap == "learn":
+            return self._step_sample_beside_learn(collect_stats)
         env, agent = self.env, self.agent
         next_obs, reward, done, info = self._env_side()
         loss = agent.learn(collect_stats=collect_stats)
@@ -186,6 +203,34 @@ class Trainer:
         loss = agent.learn(collect_stats=collect_stats)
         self._ev_learn = torch.cuda.Event()
         self._ev_learn.record(main)
+        self.last_loss, self.last_reward = loss, reward
+        self.obs = self._after_step(done, next_obs, info)
+        return StepStats(loss is not None, done)
+
+    def _step_sample_beside_learn(self, collect_stats):
+        env, agent, side = self.env, self.agent, self.side
+        main = torch.cuda.current_stream(env.device)
+        if self._join:
+            side.wait_stream(main)
+            self._join = False
+        elif self._ev_env_prev is not None:
+            # env step t-1 done: these draws run beside learn t-1.  They read
+            # only the CPython stream and the ring length after this step's
+            # store; the index buffer they fill was last read three learns
+            # back (agent.OUT_BUFS rotation), before env step t-1
+            side.wait_event(self._ev_env_prev)
+        ev_s = None
+        with torch.cuda.stream(side):
+            if agent.presample(min(agent.ring.total + 1, agent.ring.cap),
+                               lds_budget=self._sampler_lds):
+                ev_s = torch.cuda.Event()
+                ev_s.record(side)
+        next_obs, reward, done, info = self._env_side()
+        self._ev_env_prev = torch.cuda.Event()
+        self._ev_env_prev.record(main)
+        if ev_s is not None:
+            main.wait_event(ev_s)
+        loss = agent.learn(collect_stats=collect_stats)
         self.last_loss, self.last_reward = loss, reward
         self.obs = self._after_step(done, next_obs, info)
         return StepStats(loss is not None, done)

@@ -53,8 +53,9 @@ extern "C" {
 
 const char *dmdqn_last_error(void);
 /* ABI version.  3 (round 5): dmdqn_adam_slabs (the slab reduction and the
- * Adam step of the shared net in one launch) and dmdqn_learn_shared_grad with
- * grad == NULL (the slabs left for it).  2 (round 4/5): the replay ring arguments `cap` of the learn,
+ * Adam step of the shared net in one launch), dmdqn_learn_shared_grad with
+ * grad == NULL (the slabs left for it), dmdqn_replay_sample_budget and
+ * dmdqn_learn_shared_lds_bytes.  2 (round 4/5): the replay ring arguments `cap` of the learn,
  * gather and store entry points are the PHYSICAL slot count of the ring -- a
  * deque of maxlen N lives in N + 1 slots (position p at slot (start + p) %
  * (N + 1), the next store in the one slot no position maps to), so a caller
@@ -211,6 +212,13 @@ int dmdqn_replay_gather_f32(const float *rows_s, const float *rows_n, const int3
  * idx: int32 [E*A][k]. */
 int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int k,
                         int32_t *idx, void *stream);
+/* dmdqn_replay_sample with the sampler block's LDS held within lds_budget
+ * bytes (0: the default, four blocks per CU): its first-lane table shrinks to
+ * fit -- slower on collisions, the same draws.  E.g. 160 KB less
+ * dmdqn_learn_shared_lds_bytes() lets one sampler block per CU run beside the
+ * shared learn's S' pass (trainer schedule "learn"). */
+int dmdqn_replay_sample_budget(uint32_t *py_state, int E, int A, int n, int k, size_t lds_budget,
+                               int32_t *idx, void *stream);
 
 /* ------------------------------------------------------------------ simulator
  * Vectorised grid microsimulation that replaces SUMO behind train.py:225-236
@@ -449,6 +457,8 @@ int dmdqn_q_argmax_shared(const float *params, int NA, int P, int hidden, int pr
 int dmdqn_learn_shared_grad(const dmdqn_learn_args *args, float *slab, int n_slabs, float *grad,
                             float scale, void *work, void *stream);
 size_t dmdqn_learn_shared_work_bytes(int NA);
+/* The LDS of one workgroup of the shared learn's S' pass (one per CU). */
+size_t dmdqn_learn_shared_lds_bytes(void);
 
 /* Keras-3 Adam (dqn_agent.py:357, A-11) on n flat parameters with gradient
  * gscale * grad[i]; params_h (when not NULL) receives the f16 copy of every

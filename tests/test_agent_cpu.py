@@ -99,8 +99,9 @@ def test_bench_auto_schedule():
     """bench.py --overlap auto: C2 (1,024 independent agents, fused) runs the env
     step beside the learn on 64 CUs (or the --cu-split given), with one agent
     per side CU learned on the side stream (or the --side-learn given), at most
-    half the agents (a small grid must not crash the Trainer); C3,
-    C5 (shared), the unfused and split-learn paths stay on one stream."""
+    half the agents (a small grid must not crash the Trainer); C5
+    (shared) draws its next batches beside the learn ("learn"); C3, the
+    unfused and split-learn paths stay on one stream."""
     import bench
     assert bench.auto_schedule(2, 2, 256, False, False, False, None) == ("env", 64, 64)
     assert bench.auto_schedule(2, 2, 256, False, False, False, 48) == ("env", 48, 48)
@@ -108,7 +109,8 @@ def test_bench_auto_schedule():
     assert bench.auto_schedule(2, 2, 16, False, False, False, None) == ("env", 64, 32)
     assert bench.auto_schedule(1, 1, 1, False, False, False, None) == ("env", 64, 0)
     assert bench.auto_schedule(4, 4, 1024, False, False, False, None) == ("none", None, 0)
-    assert bench.auto_schedule(8, 8, 256, True, False, False, None) == ("none", None, 0)
+    assert bench.auto_schedule(8, 8, 256, True, False, False, None) == ("learn", None, 0)
+    assert bench.auto_schedule(8, 8, 256, True, True, False, None) == ("learn", None, 0)
     assert bench.auto_schedule(2, 2, 256, False, True, False, None) == ("none", None, 0)
     assert bench.auto_schedule(2, 2, 256, False, False, True, None) == ("none", None, 0)
     for rows, cols, envs in ((2, 2, 16), (1, 1, 3), (2, 2, 256), (1, 2, 7)):

@@ -42,7 +42,8 @@ def test_python_bindings_cover_header(lib):
     ctypes signature (the C-ABI tests' path)."""
     from dmdqn_amd import _lib, agent, env, ops  # noqa: F401  (agent registers its signatures)
     declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version", "dmdqn_debug_status",
-                                   "dmdqn_debug_build", "dmdqn_learn_shared_work_bytes"}
+                                   "dmdqn_debug_build", "dmdqn_learn_shared_work_bytes",
+                                   "dmdqn_learn_shared_lds_bytes"}
     host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy", "dmdqn_set_option",
                  "dmdqn_get_option", "dmdqn_timing_event_create", "dmdqn_event_record",
                  "dmdqn_event_synchronize", "dmdqn_event_elapsed_ms", "dmdqn_event_destroy",
@@ -72,6 +73,9 @@ def test_version_and_error_string(lib):
     import ctypes
     lib.dmdqn_learn_shared_work_bytes.restype = ctypes.c_size_t
     assert lib.dmdqn_learn_shared_work_bytes(16384) == 16384 * 128 * 5
+    from dmdqn_amd import _lib
+    # the S' pass's workgroup: both nets (2 x 58,896 B) + 8 waves' scratch
+    assert _lib.learn_shared_lds_bytes() == 2 * 58896 + 8 * 128 * 20
     assert isinstance(lib.dmdqn_last_error(), bytes)
 
 

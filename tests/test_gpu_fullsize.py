@@ -406,9 +406,12 @@ def test_c2_bench_schedule_steady_state_wrapped_rings():
     torch.cuda.empty_cache()
 
 
-def _run_schedule(kw, steps=420, cap=300, stats_every=7):
-    tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=256, seed=2),
-                 AgentConfig(precision="bf16", replay_buffer_size=cap, seed=2), **kw)
+def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), precision="bf16",
+                  shared=False):
+    R, C, E = grid
+    tr = Trainer(EnvConfig(rows=R, cols=C, num_envs=E, seed=2),
+                 AgentConfig(precision=precision, replay_buffer_size=cap, seed=2,
+                             shared_params=shared), **kw)
     losses, stats, obs = [], [], []
     for t in range(steps):
         st = tr.step(collect_stats=t % stats_every == 0)
@@ -447,6 +450,24 @@ def test_c2_bench_schedule_bit_identical_to_one_stream(fenced):
             got = _run_schedule(kw)
     finally:
         torch.cuda.synchronize()
+    assert ref.keys() == got.keys()
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
+
+
+def test_c5_bench_schedule_bit_identical_to_one_stream():
+    """The schedule bench.py --overlap auto times at C5 (8x8 x 256, shared
+    fp16): the next step's replay draws on a side stream beside the learn, the
+    sampler's LDS cut to what the S' pass leaves of a CU (trainer "learn").
+    Replay 300 (wrapped by step 300), 420 steps: losses, Q statistics,
+    observations, the network, Adam slots, target shadows, random streams and
+    rings bit-identical to the one-stream order."""
+    import bench
+    sched, cus, side_learn = bench.auto_schedule(8, 8, 256, True, False, False, None)
+    assert sched == "learn" and cus is None and side_learn == 0
+    cfg = dict(grid=(8, 8, 256), precision="fp16", shared=True)
+    ref = _run_schedule({}, **cfg)
+    got = _run_schedule({"overlap": sched}, **cfg)
     assert ref.keys() == got.keys()
     for k in ref:
         assert torch.equal(ref[k], got[k]), k

@@ -35,7 +35,7 @@ def _run(tr, n):
     return out
 
 
-@pytest.mark.parametrize("mode", ["sample", "full", "env"])
+@pytest.mark.parametrize("mode", ["sample", "full", "env", "learn"])
 @pytest.mark.parametrize("precision,shared,greedy", [
     ("fp16", False, False), ("fp32", False, False), ("bf16", False, False), ("fp16", True, False),
     ("fp16", False, True)])

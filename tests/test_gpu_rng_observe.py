@@ -99,6 +99,25 @@ def test_replay_sample_table_collisions(tlog, lib_option):
                 np.testing.assert_array_equal(idx[e, j], O.py_sample(refs[e], n, 128))
 
 
+@pytest.mark.parametrize("budget", ["beside_shared_learn", 6400, 14000])
+def test_replay_sample_lds_budget(budget):
+    """dmdqn_replay_sample_budget: the sampler block's LDS held to a budget (the
+    trainer's "learn" schedule gives it what the shared S' pass leaves of a
+    CU; 6,400 B leaves the set branch a 32-entry table at n = 10,000): the
+    draws are CPython's, whatever the table size."""
+    from dmdqn_amd import _lib
+    from dmdqn_amd.trainer import LDS_PER_CU
+    b = LDS_PER_CU - _lib.learn_shared_lds_bytes() if budget == "beside_shared_learn" else budget
+    seeds = [3, 4]
+    st = K.seed_streams(seeds, "py")
+    refs = [O.py_stream(s) for s in seeds]
+    for n in (200, 1046, 10000):
+        idx = K.replay_sample(st, 16, n, 128, lds_budget=b).cpu().numpy().reshape(len(seeds), 16, 128)
+        for e in range(len(seeds)):
+            for j in range(16):
+                np.testing.assert_array_equal(idx[e, j], O.py_sample(refs[e], n, 128))
+
+
 @pytest.mark.parametrize("grid", [(1, 1), (2, 2), (3, 3), (4, 4), (8, 8), (2, 3)])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_observe_reward(grid, mode):

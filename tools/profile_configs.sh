@@ -21,7 +21,7 @@ for CFG in "$@"; do
             SIMK="k_sim_step<true, false, false>"; ENVK="k_sim_step<true, false, true>" ;;
         c3) ARGS="--rows 4 --cols 4 --envs 1024 --precision fp16"; KEY=4x4x1024_fp16; LK=k_learn_f16
             SIMK="k_sim_step<true, false, false>"; ENVK="k_sim_step<true, false, true>" ;;
-        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK="k_shared_next|k_shared_grad|k_reduce_slabs|k_adam"
+        c5) ARGS="--shared --rows 8 --cols 8 --envs 256"; KEY=8x8x256_fp16_shared; LK="k_shared_next|k_shared_grad|k_reduce_adam"
             SIMK="k_sim_step_reg<1024, false>"; ENVK="k_sim_step_reg<1024, true>" ;;
         *) echo "unknown config $CFG"; exit 2 ;;
     esac
