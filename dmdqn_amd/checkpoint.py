@@ -73,6 +73,7 @@ def _cfg_dict(cfg):
 
 def trainer_state(tr, include_replay=True):
     """CPU copy of everything a resume needs (see module docstring)."""
+    tr.sync_outputs()  # the last side-stream learn's weights (schedule "env")
     ag, env = tr.agent, tr.env
     st = {"format": FORMAT,
           "env_cfg": _cfg_dict(env.cfg), "agent_cfg": _cfg_dict(ag.cfg),
