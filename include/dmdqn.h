@@ -213,8 +213,10 @@ int dmdqn_replay_gather_f32(const float *rows_s, const float *rows_n, const int3
 int dmdqn_replay_sample(uint32_t *py_state, int E, int A, int n, int k,
                         int32_t *idx, void *stream);
 /* dmdqn_replay_sample with the sampler block's LDS held within lds_budget
- * bytes (0: the default, four blocks per CU): its first-lane table shrinks to
- * fit -- slower on collisions, the same draws.  E.g. 160 KB less
+ * bytes (0: the default, four blocks per CU) in the set branch (n > setsize,
+ * the steady state): its first-lane table shrinks to fit -- slower on
+ * collisions, the same draws.  The pool branch (n <= setsize, while a ring
+ * fills) ignores the budget.  E.g. 160 KB less
  * dmdqn_learn_shared_lds_bytes() lets one sampler block per CU run beside the
  * shared learn's S' pass (trainer schedule "learn"). */
 int dmdqn_replay_sample_budget(uint32_t *py_state, int E, int A, int n, int k, size_t lds_budget,
