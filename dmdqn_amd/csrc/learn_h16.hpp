@@ -150,8 +150,8 @@ __device__ __forceinline__ int hoff(int r, int c) {
 
 // frag_row on a blocked image (r0 a multiple of 16, k0 of 32).
 template <int LD = H>
-__device__ __forceinline__ half8 frag_row_h(const h16 *img, int r0, int k0) {
-    const int l = threadIdx.x & 63;
+__device__ __forceinline__ half8 frag_row_h(const h16 *img, int r0, int k0, int tid = threadIdx.x) {
+    const int l = tid & 63;
     return *reinterpret_cast<const half8 *>(img + hoff<LD>(r0 + (l & 15), k0 + 8 * (l >> 4)));
 }
 
@@ -367,11 +367,14 @@ __device__ void forward_x(Frags &f, const OutL o, const h16 *X, h16 *H1b, h16 *H
                           S2k after_sync2 = {}) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
     const int n = 16 * w + 4 * lg;
+    // the X-row addresses from a fresh lane id: shared across the three
+    // forwards they were kept live through the kernel and spilled (round 5)
+    const int tx = fresh_tid();
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row_h<DP>(X, 16 * t, 32 * s), c);
+        for (int s = 0; s < 3; s++) c = mfma(f.w1[s], frag_row_h<DP>(X, 16 * t, 32 * s, tx), c);
         *reinterpret_cast<half4v *>(H1b + hoff(16 * t + lr, n)) = relu_h4(c, f.b1);
     }
     after_l1(f);
@@ -1146,7 +1149,8 @@ __global__ void __launch_bounds__(512, 4) H16_LEARN_KERNEL(dmdqn_learn_args a, f
                 __syncthreads();
                 w2t_image(P1, fr);
             });
-        if (lg == 0) adam1(Wp, Mp, Vp, Tp, L::ob2 + 16 * w + lr, gb[0], AK);
+        const int tx = fresh_tid();  // (16w + lr kept from the head spilled)
+        if ((tx & 63) < 16) adam1(Wp, Mp, Vp, Tp, L::ob2 + (tx >> 6) * 16 + (tx & 15), gb[0], AK);
     }
     __syncthreads();  // W2^T image complete
     f32x4 d1[8];
