@@ -4,7 +4,10 @@ trace's queue / stream id; for the last N launches of the learn kernel on
 the learn stream it prints, per step (learn start to the next learn start):
 the learn's duration, the gap before it, and what the other stream ran in
 that step (kernel, grid, start offset and duration, us).
-usage: python tools/stream_timeline.py run_kernel_trace.csv [learn-substring] [N]"""
+usage: python tools/stream_timeline.py run_kernel_trace.csv [learn-substring] [N] [skip]
+  skip: leave out the last `skip` learns (bench.py runs SIM_PROBE_STEPS = 10
+  untimed steps after its timed region, with a V-bar reduction on the learn
+  stream between them: pass 10 to see the timed steps only)"""
 import csv
 import json
 import statistics
@@ -13,6 +16,7 @@ import sys
 path = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else "k_learn"
 N = int(sys.argv[3]) if len(sys.argv) > 3 else 12
+SKIP = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 rows = list(csv.DictReader(open(path)))
 qkey = next((k for k in ("Stream_Id", "Queue_Id") if k in rows[0]), None)
 ks = sorted(({"name": r["Kernel_Name"].split("(")[0][-48:], "q": r.get(qkey, "?"),
@@ -22,7 +26,8 @@ learn = [k for k in ks if pat in k["name"]]
 # the learn stream: the queue of the biggest learn launches
 big = max(k["grid"] for k in learn)
 lq = next(k["q"] for k in learn if k["grid"] == big)
-main = [k for k in learn if k["q"] == lq and k["grid"] == big][-N - 1:]
+main = [k for k in learn if k["q"] == lq and k["grid"] == big]
+main = main[:len(main) - SKIP][-N - 1:]
 steps = []
 for a, b in zip(main, main[1:]):
     other = [{"name": k["name"], "q": k["q"], "grid": k["grid"], "start": round(k["t0"] - a["t0"], 1),
