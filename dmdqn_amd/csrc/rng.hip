@@ -288,13 +288,18 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
                 __syncthreads();
                 ep = 1;
             }
-            const uint32_t sl = pend ? slot : dummy;
-            atomicMax(&first[sl], pend ? (ep << ib) | (imask - inner) : 0u);
+            // only the pending lanes touch the table (round 4's form sent every
+            // other lane's max of 0 to the dummy entry: a same-address atomic
+            // serialised over up to 256 lanes in every round)
+            if (pend) atomicMax(&first[slot], (ep << ib) | (imask - inner));
             __syncthreads();
-            const uint32_t wi = imask - (first[sl] & imask);  // the winner's (r >> tlog, word)
-            const bool mine = pend && (wi >> 9) == (inner >> 9);  // same r
-            if (mine) dup = wi != inner;
-            pend = pend && !mine;
+            if (pend) {
+                const uint32_t wi = imask - (first[slot] & imask);  // the winner's (r >> tlog, word)
+                if ((wi >> 9) == (inner >> 9)) {  // same r: decided
+                    dup = wi != inner;
+                    pend = false;
+                }
+            }
             ep++;
             // the accepted count per wave, final in the round that leaves no lane
             // pending (the loop's barrier publishes it)
