@@ -780,6 +780,15 @@ __host__ __device__ inline size_t sim_lds_bytes(int R, int C, int cap) {
            (size_t)A * 16 + 16 + (size_t)(4 * A + 1) * 4 + (size_t)A * 48;  // q_off, last_det
 }
 
+// Sum over the wave (integer: exact in any order); the block totals below take
+// one LDS atomic per wave instead of one per thread at a single address, which
+// the LDS serialises lane by lane (up to 1024-way in the 8x8 register path).
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return x;
+}
+
 // One RL step per env (block).  kLDS: the env's state is staged into LDS for
 // the K substeps (every pass is then an LDS-latency loop instead of an L2 one:
 // pass C walks each lane's vehicles front to back); only occupied positions
@@ -946,8 +955,12 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
         }
     }
     for (int e = tid; e < 4 * A; e += nt) pend += V.q_off[e + 1] - V.qptr[e];
-    atomicAdd(&s_running, run);
-    atomicAdd(&s_pending, pend);
+    run = wave_sum(run);
+    pend = wave_sum(pend);
+    if ((tid & 63) == 0) {
+        atomicAdd(&s_running, run);
+        atomicAdd(&s_pending, pend);
+    }
     for (int a = tid; a < A; a += nt) {
         phase_out[(size_t)blockIdx.x * A + a] = V.phase[a];
         tspent[(size_t)blockIdx.x * A + a] = t - V.ts[a];
@@ -1491,8 +1504,12 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             if constexpr (kFuse) s_halt[l] = hc;
         }
     }
-    atomicAdd(&s_stats[2], run);
-    atomicAdd(&s_stats[3], pend);
+    run = wave_sum(run);
+    pend = wave_sum(pend);
+    if ((tid & 63) == 0) {
+        atomicAdd(&s_stats[2], run);
+        atomicAdd(&s_stats[3], pend);
+    }
     for (int a = tid; a < A; a += NT) {
         phase_out[(size_t)blockIdx.x * A + a] = s_phase[a];
         tspent[(size_t)blockIdx.x * A + a] = t - s_ts[a];
