@@ -226,8 +226,8 @@ __global__ void __launch_bounds__(64) k_sample(uint32_t *py_state, int A, uint32
 // wave on one stream is issue-bound: ~250 instructions per 128 words).  Same
 // decisions as k_sample's set branch word for word: out-of-range and
 // already-selected words (LDS bitmap) are rejected, a repeat within the chunk
-// is rejected by the first-lane table (block-wide: atomicMin, barrier, read,
-// barrier, reset), positions come from the block prefix of the accepted
+// is rejected by the first-lane table (block-wide, pending lanes only:
+// atomicMax, barrier, read, barrier), positions come from the block prefix of the accepted
 // flags, and the agent whose k-th pick falls inside the chunk consumes it up
 // to that word.
 template <int NW>
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(64 * NW) k_sample_set(uint32_t *py_state, int 
     // tempered as they are read, so a chunk is always 64*NW words long
     uint32_t *cur = smem, *nxt = smem + MT_N, *bm = smem + 2 * MT_N;
     const uint32_t words = (n + 31u) >> 5, kb = bitlen(n);
-    uint32_t *first = bm + words;  // [T + 1]: entry T is the dummy
+    uint32_t *first = bm + words;  // [T + 1]: entry T, the dummy slot of non-candidates, is never touched
     const uint32_t tmask = (1u << tlog) - 1u, dummy = tmask + 1u;
     // first-lane table entries: (round << ib) | (imask - ((r >> tlog) << 9 | tid)),
     // taken with atomicMax: the current round's entries beat every older one
