@@ -246,8 +246,11 @@ def _step_roofline(value, K, vbar, A, P, shared, NA):
 # --overlap auto: C2 (1,024 agents) runs 3.35 M steps/s on one
 # stream, 4.03 M with the env step of t+1 beside learn t, 4.41 M with that side
 # stream on 64 CUs -- the CUs C2's 256 env blocks (four per CU) fill in one round
-# (48: 3.99 M, 80: 4.00 M); C3 gains 1-3 % with a slower learn kernel, so it and
-# C5 stay on one stream (profiles/r04/c2_schedules, c2_cusplit_end, c3_schedules)
+# (48: 3.99 M, 80: 4.00 M); C3 gains 1-3 % from that with a slower learn kernel,
+# so it does not use it (profiles/r04/c2_schedules, c2_cusplit_end, c3_schedules).
+# C3 draws its replay batches beside its own env step instead (trainer "sample":
+# the sampler blocks take the CUs the env step's last blocks leave, the learn
+# runs alone): 5.63-5.64 -> 5.67-5.68 M, learn unchanged (profiles/r05/c3_sample)
 AUTO_ENV_MAX_AGENTS = 4096
 AUTO_ENV_CU_SPLIT = 64
 # with it, the side stream learns one agent per side CU behind its env step
@@ -263,17 +266,21 @@ AUTO_SIDE_LEARN_PER_CU = 1
 def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split, side_learn=None):
     """--overlap auto -> (schedule, side-stream CUs, side-stream agents): "env"
     on AUTO_ENV_CU_SPLIT CUs (unless --cu-split names a count) for independent
-    nets of at most AUTO_ENV_MAX_AGENTS agents on the fused path; "learn" (the
-    draws beside the learn) for the shared net; else one stream.  Under "env"
+    nets of at most AUTO_ENV_MAX_AGENTS agents on the fused path; "sample" (the
+    draws beside the env step) for more of them; "learn" (the draws beside the
+    learn) for the shared net; else (the A/B flags) one stream.  Under "env"
     the side stream learns AUTO_SIDE_LEARN_PER_CU agents per side CU (unless
     --side-learn names a count), at most half the agents (Trainer needs
     0 <= side_learn < E*A); side_learn is 0 otherwise."""
     NA = rows * cols * envs
     if shared and not split_learn:
         return "learn", cu_split, 0 if side_learn is None else side_learn
-    small = (not shared and not no_fuse and not split_learn and NA <= AUTO_ENV_MAX_AGENTS)
-    if not small:
-        return "none", cu_split, 0 if side_learn is None else side_learn
+    indep = not shared and not no_fuse and not split_learn
+    if not (indep and NA <= AUTO_ENV_MAX_AGENTS):
+        # larger independent-net configs (C3, C4's shards): the replay draws on
+        # a side stream beside the env step (trainer "sample"), which fill the
+        # CUs the env step's last blocks leave; the learn runs alone
+        return ("sample" if indep else "none"), cu_split, 0 if side_learn is None else side_learn
     cus = AUTO_ENV_CU_SPLIT if cu_split is None else cu_split
     if side_learn is None:
         side_learn = min(AUTO_SIDE_LEARN_PER_CU * cus, NA // 2) if cus else 0

@@ -237,13 +237,33 @@ def test_c3_steady_state_wrapped_rings():
     indices bit-exact; at learns 3 and 5 steps after the wrap, for 8 agents,
     the device z-score bit-exact and the loss vs the Keras mixed-precision
     checker (pinned to the reference's own learn; rtol 2e-3, as at step 128)
-    and, as a sanity bound, the fp32 oracle "q-scaled" (_check_learn)."""
+    and, as a sanity bound, the fp32 oracle "q-scaled" (_check_learn).  Under
+    the schedule bench.py times at C3 (bench.auto_schedule: the replay draws on
+    a side stream beside the env step, trainer "sample")."""
     cap = 10000
-    tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap)
-    ring = tr.agent.ring
-    assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
-    del tr
+    work, kw = _bench_c3_schedule()
+    try:
+        with torch.cuda.stream(work):
+            tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap,
+                             trainer_kw=kw)
+            assert tr.overlap == "sample"
+            ring = tr.agent.ring
+            assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
+            del tr
+    finally:
+        torch.cuda.synchronize()
     torch.cuda.empty_cache()
+
+
+def _bench_c3_schedule():
+    """The schedule bench.py --overlap auto times at C3: the draws of step t
+    on a side stream beside env step t (after learn t-1), the learn alone."""
+    import bench
+    sched, cus, side_learn = bench.auto_schedule(4, 4, 1024, False, False, False, None)
+    assert (sched, cus, side_learn) == ("sample", None, 0)
+    work, side = bench.make_streams(torch.device(DEV), cus)
+    assert side is None  # the Trainer makes its side stream
+    return work, dict(overlap=sched)
 
 
 def test_c2_steady_state_wrapped_rings():
@@ -471,3 +491,45 @@ def test_c5_bench_schedule_bit_identical_to_one_stream():
     assert ref.keys() == got.keys()
     for k in ref:
         assert torch.equal(ref[k], got[k]), k
+
+
+def test_c3_bench_schedule_bit_identical_to_one_stream():
+    """The C3 schedule of bench.py (4x4 x 1024, fp16; draws beside the env
+    step) vs the one-stream order in the sampler's set branch with the rings
+    wrapped: replay 1,100 (n >= 1,046 from step 1,046 on), 1,160 steps.
+    Losses of every learn, Q statistics (collect_stats every 50th step), the
+    last observations, weights, Adam slots, target shadows, random streams and
+    rings bit-identical (compared on the device)."""
+    def run(kw):
+        tr = Trainer(EnvConfig(rows=4, cols=4, num_envs=1024, seed=2),
+                     AgentConfig(precision="fp16", replay_buffer_size=1100, seed=2), **kw)
+        losses, stats = [], []
+        for t in range(1160):
+            tr.step(collect_stats=t % 50 == 0)
+            if tr.last_loss is not None:
+                losses.append(tr.last_loss.clone())
+                if t % 50 == 0:
+                    stats.append(tr.agent.qstats.clone())
+        torch.cuda.synchronize()
+        ag = tr.agent
+        assert len(ag.ring) == 1100 and ag.ring.start == 60
+        out = dict(losses=torch.stack(losses), stats=torch.stack(stats), obs=tr.obs.clone(),
+                   **{k: getattr(ag, k).clone() for k in ("params", "target", "adam_m", "adam_v",
+                                                          "target_h", "np_state", "py_state")},
+                   **{"ring_" + k: getattr(ag.ring, k).clone() for k in ("s", "n", "a", "r", "d")})
+        del tr, ag
+        torch.cuda.empty_cache()
+        return out
+
+    ref = run({})
+    work, kw = _bench_c3_schedule()
+    try:
+        with torch.cuda.stream(work):
+            got = run(kw)
+    finally:
+        torch.cuda.synchronize()
+    assert ref.keys() == got.keys()
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
+    del ref, got
+    torch.cuda.empty_cache()
