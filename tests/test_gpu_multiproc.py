@@ -110,20 +110,24 @@ def test_c5_shared_allreduce_equals_union_batch():
     np.testing.assert_allclose(res[0]["params"], one["params"], rtol=0, atol=2e-6)
 
 
-@pytest.mark.parametrize("shared,ranks", [(False, 2), (True, 2), (False, 4)])
-def test_bench_multi_rank_launch(shared, ranks):
+@pytest.mark.parametrize("shared,ranks,grid", [(False, 2, (2, 2, 64)), (True, 2, (8, 8, 64)),
+                                               (False, 4, (2, 2, 64)), (False, 2, (4, 4, 320))])
+def test_bench_multi_rank_launch(shared, ranks, grid):
     """The launch the driver's multi-GPU bench uses (torch.distributed.run,
     one rank per GPU, max-over-ranks timing), rehearsed with 2 and 4 ranks on
     this one GPU (DMDQN_DEVICE_OVERRIDE=0, gloo: RCCL needs a device per rank):
     rank 0 prints one JSON line with n_gpus = ranks, the whole-job value over
     every rank's replicas, "weak" scaling; the shared run goes through the C5
-    gradient all-reduce every learn."""
+    gradient all-reduce every learn.  The schedules --overlap auto picks: the
+    env step beside the learn (2x2), the draws beside the learn (8x8 shared),
+    the draws beside the env step (4x4 x 320: 5,120 agents per rank, C4's
+    per-GPU schedule)."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    E = 64
-    args = ["--rows", "8", "--cols", "8", "--shared"] if shared else ["--rows", "2", "--cols", "2"]
+    R, C, E = grid
+    args = ["--rows", str(R), "--cols", str(C)] + (["--shared"] if shared else [])
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
            str(ranks), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(root, "bench.py"), "--gpus", str(ranks), "--envs", str(E), "--steps", "5",
@@ -135,8 +139,10 @@ def test_bench_multi_rank_launch(shared, ranks):
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
     out = json.loads(lines[0])
-    A = 64 if shared else 4
+    A = R * C
     assert out["n_gpus"] == ranks and out["scaling"] == "weak"
+    if R * C * E > 4096 and not shared:
+        assert out["config"]["schedule"].startswith("replay draws on a side stream beside act")
     assert out["config"]["global_envs"] == ranks * E
     assert out["steps"] == 5 and out["value"] > 0
     # value = agent-env steps of every rank / max-over-ranks wall time
