@@ -178,6 +178,16 @@ STREAM_PROBE_BYTES = 4 << 30  # bytes copied per launch by the HBM streaming pro
 STREAM_PROBE_REPS = 5
 
 
+def stream_probe_bytes(dev, want=STREAM_PROBE_BYTES):
+    """The probe's copy size: STREAM_PROBE_BYTES, cut to a sixth of the free
+    device memory (it holds 3 x n bytes) when the device is shared or short;
+    0 (skip) below 256 MiB."""
+    import torch
+    free, _ = torch.cuda.mem_get_info(dev)
+    n = min(int(want), int(free) // 6) // (1 << 20) * (1 << 20)
+    return n if n >= (256 << 20) else 0
+
+
 def stream_probe(stream, n_bytes=STREAM_PROBE_BYTES, reps=STREAM_PROBE_REPS):
     """This box's HBM streaming rate, in this process, on the learn's stream
     (dmdqn_stream_probe, csrc/probe.hip): a float4 copy of n_bytes (read n,
@@ -226,7 +236,8 @@ def stream_probe(stream, n_bytes=STREAM_PROBE_BYTES, reps=STREAM_PROBE_REPS):
     timed("copy_runtime", 2 * n_bytes, runtime_copy)
     del src, dst
     torch.cuda.empty_cache()
-    return {"copy_gbs": max(modes["copy"], modes["copy_nt"], modes["copy_runtime"]),
+    return {"n_bytes": int(n_bytes),
+            "copy_gbs": max(modes["copy"], modes["copy_nt"], modes["copy_runtime"]),
             "triad_gbs": max(modes["triad"], modes["triad_nt"]),
             "read_gbs": max(modes["read"], modes["read_nt"]), "modes": modes}
 
@@ -393,6 +404,7 @@ def main():
 
     from dmdqn_amd.agent import AgentConfig
     from dmdqn_amd.env import EnvConfig
+    from dmdqn_amd import _lib
     from dmdqn_amd.trainer import Trainer
 
     # all work on one dedicated stream: HIP events recorded on the legacy null
@@ -461,7 +473,7 @@ def main():
         tr.step()
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
     t_wait = KM.POLL_WAIT_S[0] - wait0  # ... of which blocked on the lagged replay check
-    torch.cuda.synchronize(dev)
+    tr.synchronize()  # the device, and (C5, RCCL) every outstanding all-reduce, bounded
     el = time.perf_counter() - t0
     D.barrier(args.dist_timeout)
     tr.agent.learn_hook = None
@@ -496,7 +508,16 @@ def main():
     sim_ms = [s0.elapsed_time(s1) / SIM_PROBE_STEPS]
     assert n_learn == args.steps, "learn must run in every timed step"
     learn_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    probe = stream_probe(work) if not args.no_stream_probe else None
+    probe = None
+    if not args.no_stream_probe:
+        # after the timed region, before the record: sized from free memory,
+        # and an allocation failure costs only the probe, never the bench line
+        try:
+            nb = stream_probe_bytes(dev)
+            probe = stream_probe(work, nb) if nb else {"skipped": "less than 1.5 GiB free"}
+        except torch.cuda.OutOfMemoryError as e:
+            torch.cuda.empty_cache()
+            probe = {"skipped": f"out of memory: {str(e).splitlines()[0][:120]}"}
     el_max = D.max_over_ranks(el, device=dev, timeout_s=args.dist_timeout)
     # every rank's GPU (PCI address, UUID): a multi-GPU record shows N distinct devices
     device_ids = D.gather_device_ids(dev, timeout_s=args.dist_timeout)
@@ -574,6 +595,11 @@ def main():
                                if args.side_learn else ""),
             },
             "cpu_baseline": cpu,
+            # the digest of the sources libdmdqn_hip.so / libdmdqn_torch.so were
+            # built from (embedded at build time; _lib.load() refuses a library
+            # whose digest is not the tree's, so this is also the tree's)
+            "lib_digest": _lib.LIB_DIGEST,
+            "lib_digest_matches_tree": bool(_lib.LIB_DIGEST_MATCHES),
             # secondary figures SURVEY 8d asks for next to the headline roofline
             # BASELINE.md's whole-step figure: canonical bytes of one agent-env step
             # (B_sim + B_obs + B_store + B_learn) x steps/s over 8 TB/s
@@ -604,7 +630,9 @@ def main():
             "bytes_per_launch": bpl,
             **timing,
         }
-        if probe:
+        if probe and "skipped" in probe:
+            hbm_roof["probe"] = probe
+        elif probe:
             # the same process's HBM streaming rate on this box (stream_probe)
             hbm_roof.update({
                 "copy_gbs": probe["copy_gbs"], "triad_gbs": probe["triad_gbs"],
@@ -613,7 +641,7 @@ def main():
                 "frac_of_triad": round(achieved / probe["triad_gbs"], 4),
                 "probe_modes_gbs": probe["modes"],
                 "probe": (f"dmdqn_stream_probe after the timed region, learn stream, "
-                          f"{STREAM_PROBE_BYTES >> 30} GiB: float4 copy (read + write), triad "
+                          f"{probe['n_bytes'] / (1 << 30):.2f} GiB: float4 copy (read + write), triad "
                           f"(2 reads + 1 write), read; plain and non-temporal; plus the "
                           f"runtime's D2D copy; best of each, median of {STREAM_PROBE_REPS} "
                           "launches")})

@@ -44,6 +44,7 @@ SIGNATURES = {
     "dmdqn_event_elapsed_ms": [vp, vp, vp],
     "dmdqn_event_destroy": [vp],
     "dmdqn_stream_probe": [vp, vp, C.c_size_t, i32, vp],
+    "dmdqn_device_lds_per_cu": [i32, vp],
 }
 
 
@@ -66,9 +67,47 @@ def _apply(lib, sigs):
         fn.restype = C.c_int
 
 
+def tree_digest(root=None):
+    """The digest of the sources in this tree (build.tree_digest)."""
+    from .build import tree_digest as td
+    return td(root)
+
+
+def verify_digest(lib, what, root=None, symbol="dmdqn_source_digest"):
+    """Raise DmdqnError unless the library `lib` (its path in `what`) was
+    built from the sources of this tree: the digest it embeds at build time
+    (include/dmdqn.h dmdqn_source_digest) against build.tree_digest().  A
+    prebuilt library that no longer matches its sources -- a kernel edited
+    after the build, a library from another revision -- never runs as the
+    current code.  Returns the digest.  DMDQN_ALLOW_FOREIGN_LIB=1 (same-box
+    A/B of another revision's library, tools/ab_swap.sh) turns the refusal
+    into a warning and records it in LIB_DIGEST_MATCHES (bench.py prints it)."""
+    fn = getattr(lib, symbol, None)
+    if fn is None:
+        raise DmdqnError(f"{what} has no {symbol}(): built before round 6; rebuild with "
+                         "`python -m dmdqn_amd.build`")
+    fn.restype, fn.argtypes = C.c_char_p, []
+    built = fn().decode()
+    tree = tree_digest(root)
+    global LIB_DIGEST_MATCHES
+    if built != tree:
+        if os.environ.get("DMDQN_ALLOW_FOREIGN_LIB") == "1":
+            import warnings
+            warnings.warn(f"{what}: digest {built} != tree {tree} (DMDQN_ALLOW_FOREIGN_LIB=1)")
+            LIB_DIGEST_MATCHES = False
+            return built
+        raise DmdqnError(f"{what} is stale: built from sources with digest {built}, this tree's "
+                         f"is {tree} -- rebuild with `python -m dmdqn_amd.build`")
+    return built
+
+
+LIB_DIGEST = None  # the loaded library's source digest (== the tree's)
+LIB_DIGEST_MATCHES = True  # False only under DMDQN_ALLOW_FOREIGN_LIB=1 with another build
+
+
 def load(path=None):
-    """Load the HIP library (raises if it is absent: no fallback path)."""
-    global _LIB
+    """Load the HIP library (raises if it is absent or stale: no fallback path)."""
+    global _LIB, LIB_DIGEST
     if _LIB is not None:
         return _LIB
     p = path or LIB_PATH
@@ -76,6 +115,7 @@ def load(path=None):
         raise DmdqnError(f"{p} not found: build it with `python -m dmdqn_amd.build` "
                          "(the HIP path has no CPU fallback)")
     lib = C.CDLL(p)
+    LIB_DIGEST = verify_digest(lib, p)
     lib.dmdqn_last_error.restype = C.c_char_p
     lib.dmdqn_last_error.argtypes = []
     lib.dmdqn_version.restype = C.c_int
@@ -88,6 +128,16 @@ def load(path=None):
     _apply(lib, SIGNATURES)
     _LIB = lib
     return lib
+
+
+def device_lds_per_cu(device=None):
+    """LDS bytes of one CU of `device` (dmdqn_device_lds_per_cu)."""
+    import torch
+    d = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    out = C.c_size_t()
+    call("dmdqn_device_lds_per_cu", idx, C.byref(out))
+    return int(out.value)
 
 
 def learn_shared_lds_bytes():

@@ -360,6 +360,10 @@ class BatchedDQN:
         self.stamps = None      # optional int64 [NA, 16] device tensor: phase timestamps
         self.rn_out = None      # optional f32 [NA, batch] device tensor: the z-scored rewards
         self._split_grad = None  # [NA, P] f32 scratch of the split learn (set_split_learn)
+        # the shared net's learns by launch sequence (tests assert which ran):
+        # "adam_slabs" = one rank's fused slab reduction + Adam; "allreduce" =
+        # k_reduce_slabs -> all-reduce over ranks -> k_adam(gscale = 1/world)
+        self.shared_paths = {"adam_slabs": 0, "allreduce": 0}
 
     def set_split_learn(self, on=True):
         """Run each independent-agent learn as two launches (dmdqn_learn_grad,
@@ -589,6 +593,7 @@ class BatchedDQN:
                                     self.slab, self.grad if world > 1 else None, 1.0 / self.NA,
                                     work=self.shared_work)
         if world == 1:
+            self.shared_paths["adam_slabs"] += 1
             self._ops.adam_slabs(self.params, self.adam_m, self.adam_v, self.target, self.target_h,
                                  self.params_h, self.slab, self.grad, 1.0 / self.NA, 1.0, alpha,
                                  c1, c2, eps, sync)
@@ -606,8 +611,16 @@ class BatchedDQN:
                 self.grad.copy_(g)
             else:
                 self._allreduce(self.grad)
+            self.shared_paths["allreduce"] += 1
         self._ops.adam(self.params, self.adam_m, self.adam_v, self.target, self.target_h,
                        self.params_h, self.grad, 1.0 / world, alpha, c1, c2, eps, sync)
+
+    def drain_collectives(self):
+        """Wait (bounded, dist.BoundedAllReduce.drain) for the shared net's
+        outstanding gradient all-reduces; a no-op without any."""
+        ar = getattr(self, "_allreduce", None)
+        if ar is not None:
+            ar.drain()
 
     def _refresh_params_h(self):
         if self.params_h is not None:

@@ -87,6 +87,55 @@ def source_digest(kind):
     return h.hexdigest()[:16]
 
 
+def tree_files(root=None):
+    """Every file the two libraries are built from, in a fixed order: the
+    kernels, headers and C ABI (csrc/), include/*.h and the torch operator
+    library's source.  root: another copy of the package directory (tests)."""
+    here = root or HERE
+    pats = [os.path.join(here, "csrc", "*"), os.path.join(here, "..", "include", "*.h"),
+            os.path.join(here, "torch_ext", "*.cpp")]
+    files = [p for pat in pats for p in glob.glob(pat)
+             if os.path.isfile(p) and p.endswith((".hip", ".hpp", ".cpp", ".h"))]
+    return sorted(files, key=lambda p: (os.path.basename(os.path.dirname(p)), os.path.basename(p)))
+
+
+def tree_digest(root=None):
+    """sha256 (hex, 16 chars) over tree_files() (names and contents) and the
+    common compile flags: what libdmdqn_hip.so / libdmdqn_torch.so embed at
+    build time (dmdqn_source_digest) and what _lib.load() checks them against,
+    so a library built from other sources than the tree's is refused."""
+    import hashlib
+    h = hashlib.sha256(" ".join(COMMON).encode())
+    for p in tree_files(root):
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _digest_object(variant, digest):
+    """The object that exports dmdqn_source_digest(): regenerated (and the
+    library relinked) whenever the tree digest changes."""
+    src = os.path.join(objdir(variant), "source_digest.cpp")
+    obj = src + ".o"
+    text = ("// generated by dmdqn_amd/build.py: the digest of the sources this library\n"
+            "// was built from (build.tree_digest; _lib.load() compares it with the tree)\n"
+            f'extern "C" const char *dmdqn_source_digest(void) {{ return "{digest}"; }}\n')
+    try:
+        with open(src) as f:
+            same = f.read() == text
+    except OSError:
+        same = False
+    if same and os.path.exists(obj):
+        return obj, False
+    with open(src, "w") as f:
+        f.write(text)
+    r = subprocess.run(["g++", "-O2", "-fPIC", "-c", src, "-o", obj], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"digest object failed:\n{r.stdout}\n{r.stderr}")
+    return obj, True
+
+
 def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
@@ -141,6 +190,7 @@ def build_torch_ext(force=False, verbose=True, variant=""):
     deps = [TORCH_EXT, os.path.join(LIBDIR, libname(variant))] + _headers()
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     flags = ["-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+             f'-DDMDQN_SOURCE_DIGEST="{tree_digest()}"',
              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{tdir}/include",
              f"-I{tdir}/include/torch/csrc/api/include", "-I/opt/rocm/include"]
     stamp = so + ".flags"
@@ -172,6 +222,7 @@ def build(force=False, verbose=True, variant=""):
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         results = list(ex.map(lambda s: _compile(s, force, variant), srcs))
     so = os.path.join(LIBDIR, libname(variant))
+    results.append(_digest_object(variant, tree_digest()))
     objs = [o for o, _ in results]
     if force or any(ch for _, ch in results) or not os.path.exists(so):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", so] + objs

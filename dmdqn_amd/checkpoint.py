@@ -99,7 +99,7 @@ def trainer_state(tr, include_replay=True):
 
 
 def save(path, tr, include_replay=True):
-    torch.cuda.synchronize(tr.env.device)
+    tr.synchronize()  # every stream, and (C5) the outstanding all-reduces, bounded
     tr.agent.ring.check()  # never persist a replay that holds a refused value
     torch.save(trainer_state(tr, include_replay), path)
 
@@ -148,6 +148,10 @@ def load(path, tr):
                              f"{_written(int(c['ring_total']), ag.ring)}")
         for k, v in st["replay"].items():
             plan("replay", getattr(ag.ring, k)[:, :n], v, k)
+    # the restore writes on the caller's stream: order it after everything the
+    # trainer queued on its side stream (the "env" schedule's side learn may
+    # still be updating its agents' weights and Adam slots -- ADVICE r5)
+    tr.quiesce()
     for dst, v in copies:
         dst.copy_(v.to(dst.device))
     env.local = st["env"]["local"].to(env.device)

@@ -76,7 +76,39 @@ extern "C" int dmdqn_get_option(int opt) {
 }
 
 extern "C" const char *dmdqn_last_error(void) { return dmdqn::g_err; }
-extern "C" int dmdqn_version(void) { return 3; }  // include/dmdqn.h
+extern "C" int dmdqn_version(void) { return 4; }  // include/dmdqn.h
+
+extern "C" int dmdqn_device_lds_per_cu(int device, size_t *out) {
+    DMDQN_REQUIRE(out && device >= 0, "dmdqn_device_lds_per_cu: bad args");
+    int v = 0;
+    const hipError_t e =
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device);
+    if (e != hipSuccess) {
+        dmdqn::set_error("hipDeviceGetAttribute(MaxSharedMemoryPerMultiprocessor): %s",
+                         hipGetErrorString(e));
+        return DMDQN_EHIP;
+    }
+    *out = (size_t)v;
+    return DMDQN_OK;
+}
+
+namespace dmdqn {
+// The current device's per-workgroup LDS limit, cached per device (the
+// sampler's budget is clamped to it); 160 KB if the query fails.
+size_t device_lds_per_block() {
+    static size_t cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 160 * 1024;
+    if (!cache[dev]) {
+        int v = 0;
+        cache[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) ==
+                                 hipSuccess && v > 0
+                         ? (size_t)v
+                         : 160 * 1024;
+    }
+    return cache[dev];
+}
+}  // namespace dmdqn
 
 // A HIP stream whose kernels run only on the CUs set in `mask` (n_words
 // 32-bit words, CU i = bit i % 32 of word i / 32): the trainer's side stream

@@ -355,6 +355,10 @@ DMDQN_DBG_READER(dbg_flags_rng)
 
 using namespace dmdqn;
 
+namespace dmdqn {
+size_t device_lds_per_block();  // capi.cpp: the current device's per-workgroup LDS
+}
+
 extern "C" int dmdqn_mt_seed_np(uint32_t *state, const uint64_t *seeds, int E, void *stream) {
     DMDQN_REQUIRE(state && seeds && E > 0, "dmdqn_mt_seed_np: null pointer or E<=0");
     hipLaunchKernelGGL(k_seed_np, dim3((E + 63) / 64), dim3(64), 0, as_stream(stream), state, seeds, E);
@@ -420,6 +424,8 @@ extern "C" int dmdqn_replay_sample_budget(uint32_t *py_state, int E, int A, int 
     // schedule); DMDQN_OPT_SAMPLE_TLOG caps it (tests: collisions in every
     // chunk).  The table size changes only the speed, never the draws.
     int tlog = 0;
+    const size_t lds_max = device_lds_per_block();
+    if (lds_budget > lds_max) lds_budget = lds_max;  // never more than a workgroup may hold
     if (!pool) {
         const size_t quad = lds_budget ? lds_budget : 39 * 1024;
         DMDQN_REQUIRE(!lds_budget || quad >= lds + 16 + 4,
@@ -431,7 +437,8 @@ extern "C" int dmdqn_replay_sample_budget(uint32_t *py_state, int E, int A, int 
         if (cap < tlog) tlog = cap;
         lds += ((size_t)4 << tlog) + 4;  // + the dummy entry first[T]
     }
-    DMDQN_REQUIRE(lds <= 160 * 1024, "dmdqn_replay_sample: n=%d too large for LDS", n);
+    DMDQN_REQUIRE(lds <= lds_max, "dmdqn_replay_sample: n=%d too large for LDS (%zu > %zu B)", n,
+                  lds, lds_max);
     if (!pool) {  // set branch: four waves per stream
         hipLaunchKernelGGL(k_sample_set<4>, dim3(E), dim3(256), lds, as_stream(stream), py_state, A,
                            (uint32_t)n, k, tlog, idx);

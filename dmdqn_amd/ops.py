@@ -44,6 +44,10 @@ def load():
         if not os.path.exists(TORCH_LIB_PATH):
             raise _lib.DmdqnError(f"{TORCH_LIB_PATH} not found: build it with "
                                   "`python -m dmdqn_amd.build` (no CPU fallback)")
+        # the operator library's build-time digest must be the tree's too
+        import ctypes
+        _lib.verify_digest(ctypes.CDLL(TORCH_LIB_PATH), TORCH_LIB_PATH,
+                           symbol="dmdqn_torch_source_digest")
         torch.ops.load_library(TORCH_LIB_PATH)
         _OPS = torch.ops.dmdqn
     return _OPS

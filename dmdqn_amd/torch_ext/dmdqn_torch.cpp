@@ -522,6 +522,10 @@ void q_argmax_meta(const Tensor &, int64_t, int64_t, const Tensor &, Tensor &, c
 
 }  // namespace
 
+// The tree digest this operator library was built from (build.py passes it as
+// a define; ops.load() compares it with the tree, like libdmdqn_hip.so's).
+extern "C" const char *dmdqn_torch_source_digest(void) { return DMDQN_SOURCE_DIGEST; }
+
 // Schemas: each op cites the reference call it replaces (include/dmdqn.h has
 // the argument meanings).
 TORCH_LIBRARY(dmdqn, m) {

@@ -73,7 +73,6 @@ from .env import EnvConfig, TrafficEnv
 
 
 SCHEDULES = ("none", "sample", "full", "env", "learn")
-LDS_PER_CU = 160 * 1024  # MI355X (gfx950)
 
 
 @dataclass
@@ -105,10 +104,13 @@ class Trainer:
                                 env_seeds=self.env.seeds)
         # overlap "learn": the sampler's LDS is what the shared learn's S' pass
         # leaves of a CU, so one sampler block runs beside each S' workgroup
-        # (with the default four-blocks-per-CU budget the two serialise)
+        # (with the default four-blocks-per-CU budget the two serialise); the
+        # CU's LDS is the device's (160 KB on gfx950), and the launcher clamps
+        # the budget to what one workgroup may hold
         self._sampler_lds = 0
         if overlap == "learn" and self.agent.shared:
-            self._sampler_lds = LDS_PER_CU - _lib.learn_shared_lds_bytes()
+            self._sampler_lds = max(0, _lib.device_lds_per_cu(self.env.device)
+                                    - _lib.learn_shared_lds_bytes())
         # split_learn (agent.set_split_learn): the learn as two launches so its
         # Adam half can share the chip with the next step's side-stream work
         # (overlap "full").  Off by default: measured at C2 (round 3), the
@@ -315,7 +317,8 @@ class Trainer:
             # all written on the side stream -- so an ordering-only event
             # (write after read: the store of t+2 after learn t's ring reads)
             # is enough.  A data hand-over main -> side takes a full event.
-            assert self._side_reads_nothing_from_main(), "ordering-only event with a RAW hazard"
+            if not self._side_reads_nothing_from_main():  # (not an assert: kept under -O)
+                raise RuntimeError("ordering-only learn event with a read-after-write hazard")
             ev = self._war_ring[self._war_i]
             self._war_i = (self._war_i + 1) % len(self._war_ring)
             ev.record(main)
@@ -398,11 +401,29 @@ class Trainer:
     def join_streams(self):
         """Call after changing trainer state on the caller's stream between
         steps (checkpoint restore, weight loads): the next step's side-stream
-        work then waits for it."""
+        work then waits for it.  Also orders the caller's stream after the
+        last side-stream learn (schedule "env" with side_learn), so later
+        caller-side writes cannot race it; call quiesce() BEFORE such writes."""
+        self.sync_outputs()
+        self._side_pending = None
         self._join = True
+
+    def quiesce(self):
+        """Order the caller's stream after every piece of trainer work queued
+        so far on any stream (the side stream's env step, draws and side
+        learn), so the caller may overwrite trainer state on it (checkpoint
+        restore).  No host block."""
+        self.sync_outputs()
+        self._side_pending = None
+        if self.side is not None:
+            torch.cuda.current_stream(self.env.device).wait_stream(self.side)
 
     def agent_env_steps(self, n_steps):
         return n_steps * self.env.E * self.env.A
 
     def synchronize(self):
+        """Wait for all device work, and (C5 over RCCL) first for every
+        outstanding gradient all-reduce, bounded: a peer that stalled on or
+        skipped one raises DistError instead of hanging the synchronize."""
+        self.agent.drain_collectives()
         torch.cuda.synchronize(self.env.device)

@@ -52,7 +52,9 @@ extern "C" {
 #define DMDQN_ROWS_F32 1
 
 const char *dmdqn_last_error(void);
-/* ABI version.  3 (round 5): dmdqn_adam_slabs (the slab reduction and the
+/* ABI version.  4 (round 6): version 3 plus dmdqn_source_digest and
+ * dmdqn_device_lds_per_cu; dmdqn_replay_sample_budget clamps lds_budget to the
+ * device's per-workgroup LDS.  3 (round 5): dmdqn_adam_slabs (the slab reduction and the
  * Adam step of the shared net in one launch), dmdqn_learn_shared_grad with
  * grad == NULL (the slabs left for it), dmdqn_replay_sample_budget and
  * dmdqn_learn_shared_lds_bytes.  2 (round 4/5): the replay ring arguments `cap` of the learn,
@@ -62,6 +64,18 @@ const char *dmdqn_last_error(void);
  * passes N + 1; dmdqn_learn_shared_grad requires `work`; dmdqn_sim_step takes
  * action < 0 as "no setPhase".  1: cap = maxlen, work optional. */
 int dmdqn_version(void);
+
+/* The digest of the sources this library was built from (16 hex chars:
+ * dmdqn_amd/build.py tree_digest over csrc/, the include/ headers and the operator
+ * library's source, plus the common compile flags), generated at build time.
+ * The Python loader refuses a library whose digest is not the tree's, so a
+ * stale prebuilt .so cannot run as current code. */
+const char *dmdqn_source_digest(void);
+
+/* The LDS of one CU of `device` (hipDeviceAttributeMaxSharedMemoryPerMultiprocessor):
+ * the trainer sizes a sampler block to run beside the shared learn's S' pass
+ * with it.  0 or DMDQN_EINVAL / DMDQN_EHIP. */
+int dmdqn_device_lds_per_cu(int device, size_t *out);
 
 /* Debug-bounds build (libdmdqn_hip_debug.so, -DDMDQN_DEBUG_BOUNDS): kernels
  * check the ring slots, edges, replay indices and stored actions they derive,

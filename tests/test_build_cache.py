@@ -60,3 +60,57 @@ def test_missing_flag_stamp_forces_rebuild(tmp_path, monkeypatch):
     assert build._compile(str(src), False)[1] is True
     assert (tmp_path / "k.hip.o.flags").read_text() == " ".join(
         build.COMMON + build.DEFAULT_FP)
+
+
+# ------------------------------------------------------------ source digest
+def _tree_copy(tmp_path):
+    """A copy of the sources the libraries are built from, laid out as in the
+    repository (dmdqn_amd/{csrc,torch_ext}, include/)."""
+    import shutil
+    pkg = tmp_path / "dmdqn_amd"
+    for d in ("csrc", "torch_ext"):
+        shutil.copytree(os.path.join(build.HERE, d), pkg / d)
+    shutil.copytree(os.path.join(build.HERE, "..", "include"), tmp_path / "include")
+    return str(pkg)
+
+
+def test_shipped_library_matches_tree():
+    """The built libraries embed the digest of the sources they were built
+    from (dmdqn_source_digest), and it is this tree's: load() accepts them."""
+    from dmdqn_amd import _lib, ops
+    _lib.load()
+    assert _lib.LIB_DIGEST == build.tree_digest() and _lib.LIB_DIGEST_MATCHES
+    ops.load()
+
+
+def test_stale_library_refused(tmp_path, monkeypatch):
+    """Touching a kernel source (here: one comment line in a copy of the tree)
+    changes the tree digest, and the library built before it is refused with
+    a message naming the rebuild command."""
+    import ctypes
+    import pytest
+    from dmdqn_amd import _lib
+    _lib.load()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    root = _tree_copy(tmp_path)
+    assert _lib.verify_digest(lib, "libdmdqn_hip.so", root=root) == build.tree_digest()
+    with open(os.path.join(root, "csrc", "learn_h16.hpp"), "a") as f:
+        f.write("// edited after the build\n")
+    assert build.tree_digest(root) != build.tree_digest()
+    monkeypatch.delenv("DMDQN_ALLOW_FOREIGN_LIB", raising=False)
+    with pytest.raises(_lib.DmdqnError, match=r"stale.*python -m dmdqn_amd\.build"):
+        _lib.verify_digest(lib, "libdmdqn_hip.so", root=root)
+    # the operator library carries the same digest
+    tl = ctypes.CDLL(os.path.join(os.path.dirname(_lib.LIB_PATH), "libdmdqn_torch.so"))
+    with pytest.raises(_lib.DmdqnError, match="stale"):
+        _lib.verify_digest(tl, "libdmdqn_torch.so", root=root, symbol="dmdqn_torch_source_digest")
+
+
+def test_digest_covers_every_source():
+    """Every kernel, header, C-ABI and operator source is in the digest."""
+    names = {os.path.basename(p) for p in build.tree_files()}
+    for d, ext in (("csrc", (".hip", ".hpp", ".cpp")), ("torch_ext", (".cpp",))):
+        for f in os.listdir(os.path.join(build.HERE, d)):
+            if f.endswith(ext):
+                assert f in names, f
+    assert "dmdqn.h" in names

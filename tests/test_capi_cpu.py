@@ -43,12 +43,13 @@ def test_python_bindings_cover_header(lib):
     from dmdqn_amd import _lib, agent, env, ops  # noqa: F401  (agent registers its signatures)
     declared = set(_declared()) - {"dmdqn_last_error", "dmdqn_version", "dmdqn_debug_status",
                                    "dmdqn_debug_build", "dmdqn_learn_shared_work_bytes",
-                                   "dmdqn_learn_shared_lds_bytes"}
+                                   "dmdqn_learn_shared_lds_bytes", "dmdqn_source_digest"}
     host_only = {"dmdqn_stream_create_cumask", "dmdqn_stream_destroy", "dmdqn_set_option",
                  "dmdqn_get_option", "dmdqn_timing_event_create", "dmdqn_event_record",
                  "dmdqn_event_synchronize", "dmdqn_event_elapsed_ms", "dmdqn_event_destroy",
                  "dmdqn_order_event_create", "dmdqn_stream_wait_event",
-                 "dmdqn_stream_probe"}  # bench.py's HBM probe, not on the path
+                 "dmdqn_stream_probe",  # bench.py's HBM probe, not on the path
+                 "dmdqn_device_lds_per_cu"}  # the trainer's sampler budget
     assert declared - host_only <= set(ops.ENTRY_POINTS), sorted(declared - host_only -
                                                                  set(ops.ENTRY_POINTS))
     ctypes_only = declared - {"dmdqn_sim_reset", "dmdqn_sim_reset_envs", "dmdqn_sim_step",
@@ -69,7 +70,9 @@ def test_torch_ops_registered_without_gpu(lib):
 
 
 def test_version_and_error_string(lib):
-    assert lib.dmdqn_version() == 3  # dmdqn_adam_slabs; cap = physical ring slots (include/dmdqn.h)
+    # 4: dmdqn_source_digest, dmdqn_device_lds_per_cu (3: dmdqn_adam_slabs;
+    # cap = physical ring slots; include/dmdqn.h)
+    assert lib.dmdqn_version() == 4
     import ctypes
     lib.dmdqn_learn_shared_work_bytes.restype = ctypes.c_size_t
     assert lib.dmdqn_learn_shared_work_bytes(16384) == 16384 * 128 * 5

@@ -89,8 +89,10 @@ def _shared_worker(rank, ws, port, q):
                            slab=torch.zeros((2, P)), grad=torch.zeros(P),
                            params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
                            target=torch.zeros(P), target_h=None, params_h=None, shared_work=None,
+                           shared_paths={"adam_slabs": 0, "allreduce": 0},
                            _ops=SimpleNamespace(learn_shared_grad=learn_shared_grad, adam=adam))
     AG.BatchedDQN._learn_shared(fake, 1e-3, 0.1, 1e-3, 1e-7, True, None)
+    seen["paths"] = dict(fake.shared_paths)
     q.put((rank, seen))
     dist.destroy_process_group()
 
@@ -111,6 +113,7 @@ def test_shared_param_gradient_allreduce_two_ranks():
         assert np.isclose(seen["scale"], 1 / 4)        # 1 / local agents
         assert np.allclose(seen["grad"], expect)       # identical on every rank
         assert np.isclose(seen["gscale"], 1 / ws)      # mean over ranks in Adam
+        assert seen["paths"] == {"adam_slabs": 0, "allreduce": 1}  # reduce, all-reduce, Adam
         assert seen["sync"] == 1
 
 
@@ -198,6 +201,7 @@ def _skipping_peer(rank, port, q):
                            slab=torch.zeros((2, P)), grad=torch.zeros(P),
                            params=torch.zeros(P), adam_m=torch.zeros(P), adam_v=torch.zeros(P),
                            target=torch.zeros(P), target_h=None, params_h=None, shared_work=None,
+                           shared_paths={"adam_slabs": 0, "allreduce": 0},
                            _ops=SimpleNamespace(learn_shared_grad=lambda *a, **k: None,
                                                 adam=lambda *a, **k: None))
     t0 = time.time()
@@ -266,3 +270,28 @@ def test_bounded_allreduce_lag_and_timeout(monkeypatch):
     with pytest.raises(D.DistError, match="all_reduce\\(SUM\\) of the shared-net gradient failed"):
         ar(t)  # the third incomplete one: blocks on the oldest, then times out
     assert 0.3 < time.monotonic() - t0 < 5
+
+
+def test_skipped_final_allreduce_raises_at_synchronize(monkeypatch):
+    """the last `lag` reductions of a run are still pending when it
+    ends.  Trainer.synchronize() / checkpoint.save() / bench's timed region
+    drain them first (agent.drain_collectives), bounded: a final reduction a
+    peer skipped raises DistError instead of hanging the device-wide sync."""
+    from dmdqn_amd import dist as D
+    from dmdqn_amd.agent import BatchedDQN
+    monkeypatch.setattr(D.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(D.dist, "get_world_size", lambda: 2)
+    monkeypatch.setattr(D.dist, "get_backend", lambda: "nccl")
+    monkeypatch.setattr(D.dist, "all_reduce",
+                        lambda t, op=None, async_op=False: _FakeWork(done_after=3600.0))
+    ag = BatchedDQN.__new__(BatchedDQN)  # only the collective state matters here
+    ag._allreduce = D.BoundedAllReduce(lag=4, timeout_s=0.4)
+    ag._allreduce(torch.zeros(3))  # the final reduction: its peer never joins
+    assert len(ag._allreduce._pending) == 1  # within the lag: the host ran on
+    import time
+    t0 = time.monotonic()
+    with pytest.raises(D.DistError, match="a peer rank stalled or skipped it"):
+        ag.drain_collectives()
+    assert time.monotonic() - t0 < 5
+    ag2 = BatchedDQN.__new__(BatchedDQN)
+    ag2.drain_collectives()  # no collectives: a no-op

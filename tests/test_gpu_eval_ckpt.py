@@ -204,3 +204,35 @@ def test_resume_mismatch_leaves_trainer_untouched(tmp_path):
     after = (tr2.agent.params, tr2.agent.adam_m, tr2.env.t_x, tr2.agent.ring.s,
              tr2.agent.np_state)
     assert all(torch.equal(a, b) for a, b in zip(before, after))
+
+
+def test_restore_into_running_side_learn_trainer(tmp_path):
+    """under the "env" schedule with side_learn the last
+    step's side-stream learn (agents [NA - side_learn, NA)) is waited for
+    lazily.  checkpoint.load() into a trainer that is still running it orders
+    its copies after that learn (Trainer.quiesce), so the restored weights and
+    Adam slots of the side agents are not overwritten by it: the restored run
+    continues bit-identically to the run the checkpoint was taken from."""
+    def make():
+        return Trainer(EnvConfig(rows=2, cols=2, num_envs=8, seed=5),
+                       AgentConfig(replay_buffer_size=300, target_update_frequency=7, seed=3,
+                                   precision="fp16"), overlap="env", side_learn=8)
+    tr = make()
+    _run(tr, 140)
+    path = os.path.join(str(tmp_path), "ck.pt")
+    CK.save(path, tr)
+    a = _run(tr, 15)
+    tr2 = make()
+    for _ in range(150):  # a different history, then restore with its last side learn in flight
+        tr2.step()
+    CK.load(path, tr2)
+    b = _run(tr2, 15)
+    for (la, oa, ra), (lb, ob, rb) in zip(a, b):
+        assert torch.equal(la, lb) and torch.equal(oa, ob) and torch.equal(ra, rb)
+    tr.sync_outputs()
+    tr2.sync_outputs()
+    torch.cuda.synchronize()
+    side = slice(tr.agent.NA - 8, tr.agent.NA)
+    for k in ("params", "adam_m", "adam_v", "target"):
+        assert torch.equal(getattr(tr.agent, k)[side], getattr(tr2.agent, k)[side]), k
+        assert torch.equal(getattr(tr.agent, k), getattr(tr2.agent, k)), k

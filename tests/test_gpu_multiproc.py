@@ -211,3 +211,138 @@ def test_rccl_one_rank_group_on_this_gpu():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert out == {"max": 1.25, "same": True, "finite": True}
+
+
+# ------------------------------------------------- the C5 bench schedule at 2 ranks
+C5_E_RANK = 16      # 8x8 x 16 envs per rank: 1,024 agents
+C5_STEPS = 420      # replay 300: the rings wrap at step 300
+C5_CAP = 300
+C5_STATS_EVERY = 7
+C5_EARLY_LEARNS = 8  # the union comparison's point (as test_c5_shared_allreduce_equals_union_batch)
+
+
+def _digest(h, t):
+    h.update(t.contiguous().view(torch.uint8).cpu().numpy().tobytes())
+
+
+def _run_c5_schedule(rank, ws, overlap):
+    """One rank of C5 under `overlap` ("learn" = what bench.auto_schedule picks
+    for the shared net), on bench.make_streams' dedicated learn stream.  Small
+    state comes back whole, large state (observations every step, rings,
+    random streams) as sha1 digests."""
+    import hashlib
+
+    import bench
+    from dmdqn_amd.agent import AgentConfig
+    from dmdqn_amd.env import EnvConfig
+    from dmdqn_amd.trainer import Trainer
+    E = C5_E_RANK if ws > 1 else 2 * C5_E_RANK  # one process: the union of 2 ranks
+    dev = torch.device("cuda", 0)
+    work, side = bench.make_streams(dev, None)
+    cfg = AgentConfig(precision="fp16", seed=2, shared_params=True, replay_buffer_size=C5_CAP)
+    out = {}
+    with torch.cuda.stream(work):
+        tr = Trainer(EnvConfig(rows=8, cols=8, num_envs=E, seed=2, env_offset=rank * E), cfg,
+                     device=dev, overlap=overlap, side_stream=side)
+        losses, stats, h_obs = [], [], hashlib.sha1()
+        for t in range(C5_STEPS):
+            st = tr.step(collect_stats=t % C5_STATS_EVERY == 0)
+            assert st.loss_launched == (t + 1 >= 128)
+            if tr.last_loss is not None:
+                losses.append(tr.last_loss.cpu().numpy().copy())
+                if t % C5_STATS_EVERY == 0:
+                    stats.append(tr.agent.qstats.cpu().numpy().copy())
+                if len(losses) == C5_EARLY_LEARNS:
+                    out["params_early"] = tr.agent.params.cpu().numpy().copy()
+            _digest(h_obs, tr.obs)
+        tr.synchronize()  # drains the bounded all-reduces first
+        ag = tr.agent
+        assert ag.ring.start != 0 and len(ag.ring) == C5_CAP
+        out.update(losses=np.stack(losses), stats=np.stack(stats), obs_sha1=h_obs.hexdigest(),
+                   paths=dict(ag.shared_paths), sampler_lds=tr._sampler_lds,
+                   **{k: getattr(ag, k).cpu().numpy().copy()
+                      for k in ("params", "target", "adam_m", "adam_v")},
+                   target_h=ag.target_h.float().cpu().numpy())
+        for k in ("np_state", "py_state"):
+            h = hashlib.sha1()
+            _digest(h, getattr(ag, k))
+            out[k + "_sha1"] = h.hexdigest()
+        for k in ("s", "n", "a", "r", "d"):
+            h = hashlib.sha1()
+            _digest(h, getattr(ag.ring, k))
+            out["ring_" + k + "_sha1"] = h.hexdigest()
+    return out
+
+
+def _c5_worker(rank, ws, port, q, overlap):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from dmdqn_amd import dist as D
+    D.init(backend="gloo", timeout_s=120)
+    torch.cuda.set_device(0)
+    try:
+        q.put((rank, _run_c5_schedule(rank, ws, overlap)))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _c5_two_ranks(overlap):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_c5_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=400) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_c5_bench_schedule_two_ranks_bit_identical_to_one_stream():
+    """the schedule bench.py --overlap auto picks for C5
+    ("learn": the next step's replay draws on a side stream beside the learn,
+    the sampler's LDS cut to what the S' pass leaves of a CU) at 2 ranks, where
+    the shared learn is k_shared_next + k_shared_grad -> k_reduce_slabs ->
+    all-reduce over ranks -> k_adam(1/world) instead of one rank's fused
+    k_reduce_adam.  8x8 x 16 envs per rank, replay 300 (wrapped at step 300),
+    420 steps, Q statistics every 7th step: per rank, losses, Q statistics,
+    observations, the network, Adam slots, the f16 target shadow, random
+    streams and rings are bit-identical to the same 2 ranks on one stream
+    (overlap "none"), and the network is identical on both ranks.  The
+    2-rank network after 8 learns equals one process over the union of the
+    replicas within 2e-6 (as test_c5_shared_allreduce_equals_union_batch);
+    the end-of-run difference is printed (f32 sums in another order, through
+    Adam's normalisation, ~290 learns)."""
+    import bench
+    sched, cus, side_learn = bench.auto_schedule(8, 8, C5_E_RANK, True, False, False, None)
+    assert (sched, cus, side_learn) == ("learn", None, 0)
+    got = _c5_two_ranks(sched)
+    ref = _c5_two_ranks("none")
+    n_learn = C5_STEPS - 127
+    for r in range(2):
+        assert got[r]["paths"] == {"adam_slabs": 0, "allreduce": n_learn}, got[r]["paths"]
+        assert ref[r]["paths"] == {"adam_slabs": 0, "allreduce": n_learn}, ref[r]["paths"]
+        assert got[r]["sampler_lds"] > 0 and ref[r]["sampler_lds"] == 0
+        assert got[r].keys() == ref[r].keys()
+        for k in ref[r]:
+            if k in ("paths", "sampler_lds"):
+                continue
+            a, b = ref[r][k], got[r][k]
+            if isinstance(a, np.ndarray):
+                np.testing.assert_array_equal(b, a, err_msg=f"rank {r} {k}")
+            else:
+                assert a == b, f"rank {r} {k}"
+    for k in ("params", "target", "adam_m", "adam_v", "target_h", "params_early"):
+        np.testing.assert_array_equal(got[0][k], got[1][k], err_msg=k)
+    one = _run_c5_schedule(0, 1, "none")
+    assert one["paths"] == {"adam_slabs": n_learn, "allreduce": 0}
+    d_early = np.abs(got[0]["params_early"] - one["params_early"]).max()
+    d_end = np.abs(got[0]["params"] - one["params"]).max()
+    print(f"C5 2-rank 'learn' vs union: max |dw| {d_early:.3g} after {C5_EARLY_LEARNS} learns, "
+          f"{d_end:.3g} after {n_learn}")
+    np.testing.assert_allclose(got[0]["params_early"], one["params_early"], rtol=0, atol=2e-6)

@@ -10,6 +10,7 @@ tag=$1 rounds=$2 bargs=$3; shift 3
 out=gpurun_out/$tag
 mkdir -p "$out"
 prod=dmdqn_amd/lib/libdmdqn_hip.so
+export DMDQN_ALLOW_FOREIGN_LIB=1  # the swapped-in libraries are other revisions (_lib.verify_digest)
 cp "$prod" "$out/_product.so"
 restore() { cp "$out/_product.so" "$prod"; rm -f "$out/_product.so"; }
 trap restore EXIT
