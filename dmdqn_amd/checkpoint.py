@@ -26,10 +26,11 @@ import os
 import numpy as np
 import torch
 
-# 7: replay rings of cap + 1 slots (kernels.ReplayRing), the written slots saved;
+# 8: replay rings of cap + 2 slots (kernels.ReplayRing.SPARE); 7: cap + 1 slots,
+# the written slots saved;
 # 6: + per-replica clocks and episode counters; 5: + the actuated-mode detector
 # times; 4: 128-B replay rows, unpadded W1T
-FORMAT = "dmdqn-ckpt-7"
+FORMAT = "dmdqn-ckpt-8"
 
 _ENV_TENSORS = ["t_x", "t_v", "t_dst", "t_head", "t_cnt", "t_phase_state", "t_ts", "t_qptr",
                 "t_stats", "t_last_det", "t_env", "halt", "phase", "tspent", "done_u8"]

@@ -87,22 +87,26 @@ class ReplayRing:
     """Device replay rings for NA agents (ReplayBuffer, dqn_agent.py:27-89).
 
     Each agent keeps the last `cap` transitions (the deque's maxlen) in
-    `slots` = cap + 1 physical ring slots: deque position p (0 = oldest) lives
-    in slot (start + p) % slots and the next store goes to the one slot no
-    position maps to, total % slots -- so the store of step t+1 never touches
-    a slot the learn of step t may read (trainer overlap "env").  All agents
-    add in lockstep, so one host-side counter describes every ring.
+    `slots` = cap + SPARE physical ring slots: deque position p (0 = oldest)
+    lives in slot (start + p) % slots and the next stores go to the SPARE
+    slots no position maps to, total % slots -- so the stores of steps t+1
+    and t+2 never touch a slot the learn of step t may read (trainer overlap
+    "env": the side stream's env step k waits only for learn k - 1 - SPARE,
+    and the learn stream records its ordering event every other learn).  All
+    agents add in lockstep, so one host-side counter describes every ring.
 
     row_format "int8" (the batched path): 128-byte int8 rows, exact for this
     environment's integer features, anything else raises.  "f32" (the
     per-agent drop-in surface): float32 rows of ROW_FLOATS, every value kept
     as the reference's buffer keeps it (dqn_agent.py:39-56)."""
 
+    SPARE = 2  # physical slots beyond the deque's maxlen (round 6; 1 before)
+
     def __init__(self, NA, cap, device="cuda", row_format="int8"):
         if row_format not in ("int8", "f32"):
             raise ValueError("row_format must be 'int8' or 'f32'")
         self.NA, self.cap, self.row_format = NA, cap, row_format
-        self.slots = S = cap + 1
+        self.slots = S = cap + self.SPARE
         z = dict(device=device)
         if row_format == "f32":
             self.s = torch.zeros((NA, S, ROW_FLOATS), dtype=torch.float32, **z)

@@ -35,12 +35,14 @@ sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
 
   "env"     the fused env step of step t+1 (act, sim, observe, remember) and
             the replay draws of learn t+1 run on a side stream beside learn t.
-            The ring has one spare slot (kernels.ReplayRing: cap + 1 slots for
-            a deque of maxlen cap), and the store of step t+1 goes to the one
-            slot learn t cannot sample; the store of step t+2 waits for learn
-            t (its slot is in learn t's window).  A greedy act (epsilon < 1)
-            waits for learn t's weights.
-              side:  [wait learn t-1] env_step_{t+1} sample_{t+1} (ev_env)
+            The ring has two spare slots (kernels.ReplayRing: cap + 2 slots
+            for a deque of maxlen cap), and the stores of steps t+1 and t+2 go
+            to slots learn t cannot sample; the store of step t+3 waits for
+            learn t (its slot is in learn t's window), or a later marked learn
+            (at fixed epsilon 1 the learn stream marks every other learn with
+            an ordering-only event).  A greedy act (epsilon < 1) waits for
+            learn t's weights.
+              side:  [wait learn t-2 or t-1] env_step_{t+1} sample_{t+1} (ev_env)
               main:  [wait ev_env of t] learn_t
             With a CU-masked side stream (bench --cu-split) the two split the
             chip.  side_learn=m runs the learn of the last m agents on the side
@@ -123,7 +125,6 @@ class Trainer:
         self.fused = bool(fused) and overlap != "full" and self.agent.ring.row_format == "int8"
         if overlap == "env" and not self.fused:
             raise ValueError('overlap "env" runs the fused env step (int8 replay rows, fused=True)')
-        self._ev_learn_prev = None  # overlap "env": the learn before the last one
         # overlap "env": the learn of the last `side_learn` agents runs on the
         # side stream behind the env step and the draws (its CUs idle
         # otherwise while the learn stream works), the rest on the learn
@@ -141,6 +142,18 @@ class Trainer:
         self._war_ring = ([_lib.OrderEvent() for _ in range(4)]
                           if war_events and overlap == "env" else None)
         self._war_i = 0
+        # overlap "env": (call index, event) of the learns the side stream may
+        # wait for, newest last.  The store of call k overwrites the slot of
+        # store k - slots, which the learns of calls up to k - 1 - spare read
+        # (kernels.ReplayRing.SPARE), so env step k waits for the newest marked
+        # learn of a call <= k - 2 -- never learn k - 1, beside which it runs.
+        # With 2 spare slots any learn of call k - 3 or k - 2 will do, so under
+        # ordering-only events the learn stream marks every other learn
+        # (a marker packet less per two steps between its kernels).
+        self._marks = []
+        self._calls = 0
+        self._first_learn = None  # the call of the first learn (always marked)
+        self.n_marks = 0  # learns marked for the side stream (tests: every other one)
         self.obs = self.env.reset()
         self.episode = 0
         self.step_count = 0
@@ -275,12 +288,21 @@ class Trainer:
         if self._join:  # first step, or the caller touched state on its stream
             side.wait_stream(main)
             self._join = False
-        if self._ev_learn_prev is not None:
-            # this store's slot is in the window of the learn two steps back
-            if isinstance(self._ev_learn_prev, _lib.OrderEvent):
-                self._ev_learn_prev.wait(side)
+        k = self._calls
+        self._calls += 1
+        spare = agent.ring.slots - agent.ring.cap
+        marks = [m for m in self._marks if m[0] <= k - 2]
+        if marks:
+            j, ev = marks[-1]
+            # every learn of a call <= k - 1 - spare must be covered (the main
+            # stream is in order: waiting for learn j covers every earlier one)
+            if j < k - 1 - spare and self._learned_at(k - 1 - spare, j):
+                raise RuntimeError(f"env schedule: no marked learn covers call {k - 1 - spare}")
+            if isinstance(ev, _lib.OrderEvent):
+                ev.wait(side)
             else:
-                side.wait_event(self._ev_learn_prev)
+                side.wait_event(ev)
+        self._marks = [m for m in self._marks if m[0] >= k - 3]
         if agent.current_epsilon() < 1.0 and self._ev_learn is not None:
             # greedy act reads the updated weights (recorded as a full event:
             # an ordering-only one is used only while epsilon is fixed at 1)
@@ -307,9 +329,14 @@ class Trainer:
         loss = None
         if learned:
             loss = agent.learn_range(0, agent.NA - self.side_learn)
-        self._ev_learn_prev = self._ev_learn
-        if (self._war_ring is not None and not agent.cfg.count_env_steps
-                and agent.current_epsilon() >= 1.0):
+        war = (self._war_ring is not None and not agent.cfg.count_env_steps
+               and agent.current_epsilon() >= 1.0)
+        if (learned and war and spare >= 2 and k % 2 and self._first_learn is not None
+                and self._first_learn != k):
+            # odd call under ordering-only events: no marker (the side stream's
+            # next waits are covered by the marks of calls k - 1 and k + 1)
+            pass
+        elif war:
             # epsilon cannot fall below 1 later (count_env_steps off): no act
             # will read this learn's weights through the side stream.  What the
             # side stream reads of main's work is then nothing: the side learn
@@ -323,9 +350,17 @@ class Trainer:
             self._war_i = (self._war_i + 1) % len(self._war_ring)
             ev.record(main)
             self._ev_learn = ev
+            if learned:
+                self._marks.append((k, ev))
+                self.n_marks += 1
         else:
             self._ev_learn = torch.cuda.Event()
             self._ev_learn.record(main)
+            if learned:
+                self._marks.append((k, self._ev_learn))
+                self.n_marks += 1
+        if learned and self._first_learn is None:
+            self._first_learn = k
         # the side learn's outputs (its agents' loss, stats and weights) for the
         # caller's stream.  The next learn needs no wait for them: the side
         # stream runs the next env step behind the side learn, and the next
@@ -359,6 +394,11 @@ class Trainer:
         weights read on it are complete.  A no-op otherwise."""
         if getattr(self, "_side_pending", None) is not None:
             torch.cuda.current_stream(self.env.device).wait_event(self._side_pending)
+
+    def _learned_at(self, call, newest_mark):
+        """Whether a learn ran at `call` that the mark of call `newest_mark`
+        does not cover (call > newest_mark and the learn had begun by then)."""
+        return self._first_learn is not None and newest_mark < call and self._first_learn <= call
 
     def _side_reads_nothing_from_main(self):
         """The "env" schedule's invariant for ordering-only learn events: no

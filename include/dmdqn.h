@@ -59,9 +59,9 @@ const char *dmdqn_last_error(void);
  * grad == NULL (the slabs left for it), dmdqn_replay_sample_budget and
  * dmdqn_learn_shared_lds_bytes.  2 (round 4/5): the replay ring arguments `cap` of the learn,
  * gather and store entry points are the PHYSICAL slot count of the ring -- a
- * deque of maxlen N lives in N + 1 slots (position p at slot (start + p) %
- * (N + 1), the next store in the one slot no position maps to), so a caller
- * passes N + 1; dmdqn_learn_shared_grad requires `work`; dmdqn_sim_step takes
+ * deque of maxlen N lives in N + k slots, k >= 1 (position p at slot (start +
+ * p) % (N + k), the next stores in the k slots no position maps to; the Python
+ * ring uses k = 2 since round 6, k = 1 before), so a caller passes N + k; dmdqn_learn_shared_grad requires `work`; dmdqn_sim_step takes
  * action < 0 as "no setPhase".  1: cap = maxlen, work optional. */
 int dmdqn_version(void);
 

@@ -71,28 +71,35 @@ def test_config_keys_match_reference_yaml():
 
 
 def test_replay_ring_spare_slot_arithmetic():
-    """ReplayRing keeps a deque of maxlen cap in cap + 1 slots: deque position
-    p -> slot (start + p) % (cap + 1), the next store goes to the slot no
-    position maps to, so the store of step t+1 never touches the window of
-    learn t (trainer overlap "env"), while the store of step t+2 may (it
-    waits for learn t)."""
+    """ReplayRing keeps a deque of maxlen cap in cap + 2 slots: deque position
+    p -> slot (start + p) % (cap + 2), the next stores go to the slots no
+    position maps to, so the stores of steps t+1 and t+2 never touch the
+    window of learn t (trainer overlap "env"), while the store of step t+3 may
+    (it waits for learn t, or a later marked one)."""
     from dmdqn_amd.kernels import ReplayRing
     cap = 5
+    S = cap + ReplayRing.SPARE
+    assert ReplayRing.SPARE == 2
     r = ReplayRing(2, cap, device="cpu")
-    assert r.slots == cap + 1 and tuple(r.a.shape) == (2, cap + 1)
-    prev_window = None
+    assert r.slots == S and tuple(r.a.shape) == (2, S)
+    windows = []
     for t in range(40):
         window = {int(s) for s in r.slots_of(np.arange(len(r)))}
         assert len(window) == len(r) and r.next_slot not in window
-        if prev_window is not None and len(prev_window) == cap:
-            # the window one learn back holds the next slot once the ring is full
-            assert r.next_slot in prev_window
-        prev_window = window
+        # store t: `window` is what learn t-1 reads (stores 0..t-1), windows[-1]
+        # learn t-2's; neither holds its slot (two spare slots), so store t
+        # waits for neither -- learn t-3's window (windows[-2]) holds it once
+        # the ring is full, so store t waits for learn t-3 (or a later one)
+        if windows:
+            assert r.next_slot not in windows[-1]
+        if len(windows) >= 2 and len(windows[-2]) == cap:
+            assert r.next_slot in windows[-2]
+        windows.append(window)
         # deque semantics: position 0 is the oldest kept transition
         if t >= cap:
-            assert int(r.slots_of(0)) == (t - cap) % (cap + 1)
+            assert int(r.slots_of(0)) == (t - cap) % S
         r.advance()
-    assert len(r) == cap and r.start == (40 - cap) % (cap + 1)
+    assert len(r) == cap and r.start == (40 - cap) % S
 
 
 def test_bench_auto_schedule():

@@ -427,7 +427,7 @@ def test_c2_bench_schedule_steady_state_wrapped_rings():
 
 
 def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), precision="bf16",
-                  shared=False):
+                  shared=False, marks=None):
     R, C, E = grid
     tr = Trainer(EnvConfig(rows=R, cols=C, num_envs=E, seed=2),
                  AgentConfig(precision=precision, replay_buffer_size=cap, seed=2,
@@ -443,6 +443,8 @@ def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), preci
         assert st.loss_launched == (t + 1 >= 128)
     torch.cuda.synchronize()
     assert tr.agent.ring.start != 0
+    if marks is not None:
+        marks.append((tr.n_marks, tr.agent.learn_launches))
     ag = tr.agent
     out = dict(losses=torch.stack(losses).cpu(), stats=torch.stack(stats).cpu(),
                obs=torch.stack(obs).cpu(),
@@ -465,11 +467,19 @@ def test_c2_bench_schedule_bit_identical_to_one_stream(fenced):
     ref = _run_schedule({})
     work, kw = _bench_c2_schedule()
     kw["war_events"] = not fenced
+    marks = []
     try:
         with torch.cuda.stream(work):
-            got = _run_schedule(kw)
+            got = _run_schedule(kw, marks=marks)
     finally:
         torch.cuda.synchronize()
+    # two spare ring slots: ordering-only events mark every other learn for
+    # the side stream (the first learn always); default events mark every one
+    n_marks, n_learns = marks[0]
+    if fenced:
+        assert n_marks == n_learns, (n_marks, n_learns)
+    else:
+        assert abs(n_marks - n_learns / 2) <= 1.5, (n_marks, n_learns)
     assert ref.keys() == got.keys()
     for k in ref:
         assert torch.equal(ref[k], got[k]), k

@@ -250,6 +250,8 @@ def _run_c5_schedule(rank, ws, overlap):
             assert st.loss_launched == (t + 1 >= 128)
             if tr.last_loss is not None:
                 losses.append(tr.last_loss.cpu().numpy().copy())
+                if len(losses) == 1:  # the first learn's reduced gradient (same weights everywhere)
+                    out["grad1"] = tr.agent.grad.cpu().numpy().copy()
                 if t % C5_STATS_EVERY == 0:
                     stats.append(tr.agent.qstats.cpu().numpy().copy())
                 if len(losses) == C5_EARLY_LEARNS:
@@ -313,11 +315,16 @@ def test_c5_bench_schedule_two_ranks_bit_identical_to_one_stream():
     420 steps, Q statistics every 7th step: per rank, losses, Q statistics,
     observations, the network, Adam slots, the f16 target shadow, random
     streams and rings are bit-identical to the same 2 ranks on one stream
-    (overlap "none"), and the network is identical on both ranks.  The
-    2-rank network after 8 learns equals one process over the union of the
-    replicas within 2e-6 (as test_c5_shared_allreduce_equals_union_batch);
-    the end-of-run difference is printed (f32 sums in another order, through
-    Adam's normalisation, ~290 learns)."""
+    (overlap "none"), and the network is identical on both ranks.
+    Against one process over the union of the replicas ("averaged
+    gradient equals the single-GPU gradient over the union batch"): the first
+    learn's gradient (same weights on both sides) -- the all-reduced sum over
+    2 ranks, halved by Adam's gscale -- equals the union's within 1e-5 of its
+    largest element (f32 sums in another order: per rank, then across ranks).
+    The weights after 8 learns agree within 2e-6 except where Adam's
+    normalisation m / (sqrt(v) + eps) turns an order-of-summation difference
+    in a near-zero gradient into a visible step: there the bound is Adam's own
+    step size, lr per learn (measured: 7 of 28,548 weights, 1.9e-5)."""
     import bench
     sched, cus, side_learn = bench.auto_schedule(8, 8, C5_E_RANK, True, False, False, None)
     assert (sched, cus, side_learn) == ("learn", None, 0)
@@ -341,8 +348,14 @@ def test_c5_bench_schedule_two_ranks_bit_identical_to_one_stream():
         np.testing.assert_array_equal(got[0][k], got[1][k], err_msg=k)
     one = _run_c5_schedule(0, 1, "none")
     assert one["paths"] == {"adam_slabs": n_learn, "allreduce": 0}
-    d_early = np.abs(got[0]["params_early"] - one["params_early"]).max()
+    g2, g1 = got[0]["grad1"] * 0.5, one["grad1"]  # the 2-rank sum x Adam's gscale 1/world
+    gmax = float(np.abs(g1).max())
+    dg = float(np.abs(g2 - g1).max())
+    d = np.abs(got[0]["params_early"] - one["params_early"])
     d_end = np.abs(got[0]["params"] - one["params"]).max()
-    print(f"C5 2-rank 'learn' vs union: max |dw| {d_early:.3g} after {C5_EARLY_LEARNS} learns, "
-          f"{d_end:.3g} after {n_learn}")
-    np.testing.assert_allclose(got[0]["params_early"], one["params_early"], rtol=0, atol=2e-6)
+    print(f"C5 2-rank 'learn' vs union: first gradient max |dg| {dg:.3g} (max |g| {gmax:.3g}); "
+          f"max |dw| {d.max():.3g} after {C5_EARLY_LEARNS} learns ({int((d > 2e-6).sum())} "
+          f"above 2e-6), {d_end:.3g} after {n_learn}")
+    assert dg <= 1e-5 * gmax
+    lr = 1e-3  # AgentConfig.learning_rate: Adam moves a weight at most ~lr per learn
+    assert (d > 2e-6).sum() <= 1e-3 * d.size and d.max() <= C5_EARLY_LEARNS * lr

@@ -153,13 +153,14 @@ def test_replay_store_roundtrip_and_range_check():
         ring.store(s.to(DEV), n.to(DEV), a.to(DEV), r.to(DEV), d.to(DEV))
         rows.append((s, n, a, r, d))
     ring.check()
-    # a deque of maxlen cap in cap + 1 slots: position p -> slot (start + p) % (cap + 1)
-    assert len(ring) == cap and ring.slots == cap + 1 and ring.start == (10 - cap) % (cap + 1)
+    # a deque of maxlen cap in cap + SPARE slots: position p -> slot (start + p) % slots
+    NS = cap + K.ReplayRing.SPARE
+    assert len(ring) == cap and ring.slots == NS and ring.start == (10 - cap) % NS
     S = ring.s.cpu().numpy()
     for p in range(cap):
         t = 10 - cap + p
         slot = int(ring.slots_of(p))
-        assert slot == t % (cap + 1)
+        assert slot == t % NS
         s, n, a, r, d = rows[t]
         np.testing.assert_array_equal(S[:, slot, :89].astype(np.float32), s.numpy())
         np.testing.assert_array_equal(S[:, slot, 89:], 0)
