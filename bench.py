@@ -371,6 +371,9 @@ def main():
     ap.add_argument("--fenced-events", action="store_true",
                     help="overlap env: order the side stream after the learns with default "
                          "(system-scope) events instead of ordering-only ones (A/B)")
+    ap.add_argument("--mark-every-learn", action="store_true",
+                    help="overlap env: record the learn stream's ordering event behind every learn "
+                         "(A/B; default every other one, which the ring's two spare slots allow)")
     ap.add_argument("--learn-priority", action="store_true",
                     help="with --overlap sample/full/env and no --cu-split: the learn stream at "
                          "the highest HIP stream priority, the side stream at the lowest")
@@ -426,7 +429,8 @@ def main():
                             shared_params=args.shared)
     tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side,
                  split_learn=args.split_learn, fused=not args.no_fuse,
-                 war_events=not args.fenced_events, side_learn=args.side_learn)
+                 war_events=not args.fenced_events, side_learn=args.side_learn,
+                 mark_every_learn=args.mark_every_learn)
     E, A = tr.env.E, tr.env.A
     NA = E * A
     prefill = agent_cfg.replay_buffer_size if args.prefill_steps is None else args.prefill_steps

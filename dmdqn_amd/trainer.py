@@ -86,7 +86,7 @@ class StepStats:
 class Trainer:
     def __init__(self, env_cfg: EnvConfig = None, agent_cfg: AgentConfig = None, device="cuda",
                  overlap="none", side_stream=None, split_learn=False, fused=True,
-                 war_events=True, side_learn=0):
+                 war_events=True, side_learn=0, mark_every_learn=False):
         self.env = TrafficEnv(env_cfg or EnvConfig(), device=device)
         if overlap is True or overlap is False:
             overlap = "full" if overlap else "none"
@@ -154,6 +154,7 @@ class Trainer:
         self._calls = 0
         self._first_learn = None  # the call of the first learn (always marked)
         self.n_marks = 0  # learns marked for the side stream (tests: every other one)
+        self._mark_every = bool(mark_every_learn)  # A/B: a marker behind every learn
         self.obs = self.env.reset()
         self.episode = 0
         self.step_count = 0
@@ -331,7 +332,8 @@ class Trainer:
             loss = agent.learn_range(0, agent.NA - self.side_learn)
         war = (self._war_ring is not None and not agent.cfg.count_env_steps
                and agent.current_epsilon() >= 1.0)
-        if (learned and war and spare >= 2 and k % 2 and self._first_learn is not None
+        if (learned and war and spare >= 2 and k % 2 and not self._mark_every
+                and self._first_learn is not None
                 and self._first_learn != k):
             # odd call under ordering-only events: no marker (the side stream's
             # next waits are covered by the marks of calls k - 1 and k + 1)
