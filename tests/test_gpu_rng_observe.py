@@ -99,15 +99,18 @@ def test_replay_sample_table_collisions(tlog, lib_option):
                 np.testing.assert_array_equal(idx[e, j], O.py_sample(refs[e], n, 128))
 
 
-@pytest.mark.parametrize("budget", ["beside_shared_learn", 6400, 14000])
+@pytest.mark.parametrize("budget", ["beside_shared_learn", 6400, 14000, 1 << 24])
 def test_replay_sample_lds_budget(budget):
     """dmdqn_replay_sample_budget: the sampler block's LDS held to a budget (the
-    trainer's "learn" schedule gives it what the shared S' pass leaves of a
-    CU; 6,400 B leaves the set branch a 32-entry table at n = 10,000): the
-    draws are CPython's, whatever the table size."""
+    trainer's "learn" schedule gives it what the shared S' pass leaves of the
+    device's CU, dmdqn_device_lds_per_cu: 160 KB on gfx950; 6,400 B leaves the
+    set branch a 32-entry table at n = 10,000; a budget beyond the device's
+    per-workgroup LDS is clamped to it): the draws are CPython's, whatever the
+    table size."""
     from dmdqn_amd import _lib
-    from dmdqn_amd.trainer import LDS_PER_CU
-    b = LDS_PER_CU - _lib.learn_shared_lds_bytes() if budget == "beside_shared_learn" else budget
+    assert _lib.device_lds_per_cu() == 160 * 1024  # MI355X (gfx950)
+    b = (_lib.device_lds_per_cu() - _lib.learn_shared_lds_bytes()
+         if budget == "beside_shared_learn" else budget)
     seeds = [3, 4]
     st = K.seed_streams(seeds, "py")
     refs = [O.py_stream(s) for s in seeds]
