@@ -259,9 +259,13 @@ def _step_roofline(value, K, vbar, A, P, shared, NA):
 # stream on 64 CUs -- the CUs C2's 256 env blocks (four per CU) fill in one round
 # (48: 3.99 M, 80: 4.00 M); C3 gains 1-3 % from that with a slower learn kernel,
 # so it does not use it (profiles/r04/c2_schedules, c2_cusplit_end, c3_schedules).
-# C3 draws its replay batches beside its own env step instead (trainer "sample":
-# the sampler blocks take the CUs the env step's last blocks leave, the learn
-# runs alone): 5.63-5.64 -> 5.67-5.68 M, learn unchanged (profiles/r05/c3_sample)
+# Larger independent-net configs (C3, C4's shards) run the same schedule
+# without the CU mask or side learns (round 6, VERDICT r5 item 6: chosen by
+# steps/s, same box, 3 alternating rounds, profiles/r06/c3_sched): "env"
+# 5.819-5.826 M steps/s against 5.649-5.668 M for round 5's default "sample"
+# (the draws beside the env step, learn after both) and 5.815-5.836 M with the
+# learn stream at high priority; the learn launch itself measured 2.62 ms under
+# "env" against 2.73 ms under "sample".
 AUTO_ENV_MAX_AGENTS = 4096
 AUTO_ENV_CU_SPLIT = 64
 # with it, the side stream learns one agent per side CU behind its env step
@@ -276,22 +280,23 @@ AUTO_SIDE_LEARN_PER_CU = 1
 
 def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split, side_learn=None):
     """--overlap auto -> (schedule, side-stream CUs, side-stream agents): "env"
-    on AUTO_ENV_CU_SPLIT CUs (unless --cu-split names a count) for independent
-    nets of at most AUTO_ENV_MAX_AGENTS agents on the fused path; "sample" (the
-    draws beside the env step) for more of them; "learn" (the draws beside the
-    learn) for the shared net; else (the A/B flags) one stream.  Under "env"
-    the side stream learns AUTO_SIDE_LEARN_PER_CU agents per side CU (unless
-    --side-learn names a count), at most half the agents (Trainer needs
-    0 <= side_learn < E*A); side_learn is 0 otherwise."""
+    for independent nets on the fused path -- on AUTO_ENV_CU_SPLIT CUs (unless
+    --cu-split names a count) with side learns for at most AUTO_ENV_MAX_AGENTS
+    agents, unmasked and without side learns for more; "learn" (the draws
+    beside the learn) for the shared net; else (the A/B flags) one stream.
+    Under the masked "env" the side stream learns AUTO_SIDE_LEARN_PER_CU agents
+    per side CU (unless --side-learn names a count), at most half the agents
+    (Trainer needs 0 <= side_learn < E*A); side_learn is 0 otherwise."""
     NA = rows * cols * envs
     if shared and not split_learn:
         return "learn", cu_split, 0 if side_learn is None else side_learn
     indep = not shared and not no_fuse and not split_learn
-    if not (indep and NA <= AUTO_ENV_MAX_AGENTS):
-        # larger independent-net configs (C3, C4's shards): the replay draws on
-        # a side stream beside the env step (trainer "sample"), which fill the
-        # CUs the env step's last blocks leave; the learn runs alone
-        return ("sample" if indep else "none"), cu_split, 0 if side_learn is None else side_learn
+    if not indep:
+        return "none", cu_split, 0 if side_learn is None else side_learn
+    if NA > AUTO_ENV_MAX_AGENTS:
+        # larger independent-net configs (C3, C4's shards): the env step of t+1
+        # and its draws beside learn t on an unmasked side stream
+        return "env", cu_split, 0 if side_learn is None else side_learn
     cus = AUTO_ENV_CU_SPLIT if cu_split is None else cu_split
     if side_learn is None:
         side_learn = min(AUTO_SIDE_LEARN_PER_CU * cus, NA // 2) if cus else 0
@@ -346,9 +351,9 @@ def main():
                     help="timed RL steps per replica of the CPU baseline")
     ap.add_argument("--overlap", default="auto", choices=["auto", "none", "sample", "full", "env", "learn"],
                     help="stream schedule (dmdqn_amd/trainer.py; all bit-identical): auto = "
-                         "env with the side stream on 64 CUs for independent nets of at most "
-                         f"{AUTO_ENV_MAX_AGENTS} agents per GPU (C2: the learn's compute phase "
-                         "leaves most of the chip idle), else none; none = one "
+                         "env for independent nets (the side stream on 64 CUs with side learns "
+                         f"at most {AUTO_ENV_MAX_AGENTS} agents per GPU, C2; unmasked above, "
+                         "C3), learn for the shared net, else none; none = one "
                          "stream; sample = replay draws on a side stream beside act/sim/observe/"
                          "store; full = step t+1's act/sim/observe/sample beside learn t; env = "
                          "step t+1's fused env step (store in the ring's spare slot) + draws "

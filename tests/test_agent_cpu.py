@@ -108,15 +108,16 @@ def test_bench_auto_schedule():
     per side CU learned on the side stream (or the --side-learn given), at most
     half the agents (a small grid must not crash the Trainer); C5
     (shared) draws its next batches beside the learn ("learn"); C3 (16,384
-    independent agents) draws beside the env step ("sample"); the unfused and
-    split-learn paths stay on one stream."""
+    independent agents) runs the env step beside the learn on an unmasked side
+    stream without side learns ("env", round 6); the unfused and split-learn
+    paths stay on one stream."""
     import bench
     assert bench.auto_schedule(2, 2, 256, False, False, False, None) == ("env", 64, 64)
     assert bench.auto_schedule(2, 2, 256, False, False, False, 48) == ("env", 48, 48)
     assert bench.auto_schedule(2, 2, 256, False, False, False, None, 12) == ("env", 64, 12)
     assert bench.auto_schedule(2, 2, 16, False, False, False, None) == ("env", 64, 32)
     assert bench.auto_schedule(1, 1, 1, False, False, False, None) == ("env", 64, 0)
-    assert bench.auto_schedule(4, 4, 1024, False, False, False, None) == ("sample", None, 0)
+    assert bench.auto_schedule(4, 4, 1024, False, False, False, None) == ("env", None, 0)
     assert bench.auto_schedule(4, 4, 1024, False, True, False, None) == ("none", None, 0)
     assert bench.auto_schedule(4, 4, 1024, False, False, True, None) == ("none", None, 0)
     assert bench.auto_schedule(8, 8, 256, True, False, False, None) == ("learn", None, 0)

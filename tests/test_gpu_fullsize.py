@@ -246,7 +246,7 @@ def test_c3_steady_state_wrapped_rings():
         with torch.cuda.stream(work):
             tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap,
                              trainer_kw=kw)
-            assert tr.overlap == "sample"
+            assert tr.overlap == "env" and tr.side_learn == 0
             ring = tr.agent.ring
             assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
             del tr
@@ -256,11 +256,11 @@ def test_c3_steady_state_wrapped_rings():
 
 
 def _bench_c3_schedule():
-    """The schedule bench.py --overlap auto times at C3: the draws of step t
-    on a side stream beside env step t (after learn t-1), the learn alone."""
+    """The schedule bench.py --overlap auto times at C3 (round 6): the fused
+    env step of t+1 and its draws on an unmasked side stream beside learn t."""
     import bench
     sched, cus, side_learn = bench.auto_schedule(4, 4, 1024, False, False, False, None)
-    assert (sched, cus, side_learn) == ("sample", None, 0)
+    assert (sched, cus, side_learn) == ("env", None, 0)
     work, side = bench.make_streams(torch.device(DEV), cus)
     assert side is None  # the Trainer makes its side stream
     return work, dict(overlap=sched)
@@ -504,8 +504,9 @@ def test_c5_bench_schedule_bit_identical_to_one_stream():
 
 
 def test_c3_bench_schedule_bit_identical_to_one_stream():
-    """The C3 schedule of bench.py (4x4 x 1024, fp16; draws beside the env
-    step) vs the one-stream order in the sampler's set branch with the rings
+    """The C3 schedule of bench.py (4x4 x 1024, fp16; the env step of t+1 and
+    its draws beside learn t, ring stores in the two spare slots) vs the
+    one-stream order in the sampler's set branch with the rings
     wrapped: replay 1,100 (n >= 1,046 from step 1,046 on), 1,160 steps.
     Losses of every learn, Q statistics (collect_stats every 50th step), the
     last observations, weights, Adam slots, target shadows, random streams and

@@ -120,8 +120,8 @@ def test_bench_multi_rank_launch(shared, ranks, grid):
     every rank's replicas, "weak" scaling; the shared run goes through the C5
     gradient all-reduce every learn.  The schedules --overlap auto picks: the
     env step beside the learn (2x2), the draws beside the learn (8x8 shared),
-    the draws beside the env step (4x4 x 320: 5,120 agents per rank, C4's
-    per-GPU schedule)."""
+    the env step beside the learn on an unmasked side stream (4x4 x 320:
+    5,120 agents per rank, C4's per-GPU schedule)."""
     import json
     import subprocess
     import sys
@@ -142,7 +142,8 @@ def test_bench_multi_rank_launch(shared, ranks, grid):
     A = R * C
     assert out["n_gpus"] == ranks and out["scaling"] == "weak"
     if R * C * E > 4096 and not shared:
-        assert out["config"]["schedule"].startswith("replay draws on a side stream beside act")
+        assert out["config"]["schedule"].startswith("the fused env step + replay draws of step t+1")
+        assert "CUs" not in out["config"]["schedule"]
     assert out["config"]["global_envs"] == ranks * E
     assert out["steps"] == 5 and out["value"] > 0
     # value = agent-env steps of every rank / max-over-ranks wall time
