@@ -1027,6 +1027,12 @@ constexpr int RCAP = 24;
 #ifndef SIM_STAGE_UNROLL
 #define SIM_STAGE_UNROLL 1  // 0: the round-5 staging / write-back loops (A/B)
 #endif
+#ifndef SIM_PASSC_UNROLL
+#define SIM_PASSC_UNROLL 1  // 0: pass C's rolled per-vehicle loop (A/B)
+#endif
+#ifndef SIM_PASSC_FENCE
+#define SIM_PASSC_FENCE 1  // a scheduling barrier per unrolled vehicle (1024-thread blocks)
+#endif
 #ifndef SIM_STAGE_CHUNK
 #define SIM_STAGE_CHUNK 8  // vehicles whose loads are in flight together
 #endif
@@ -1436,8 +1442,19 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 bool det = lead_x_new >= dp && lead_x_old0 < dpl;
                 float lead_x_old = lead_x_old0, lead_v_old = lead_v_old0;
                 float last_x = X_[0], last_v = vget<kL>(V_, Vc, 0);
+#if SIM_PASSC_UNROLL
+                // unrolled with constant register indices (no v_movrels /
+                // v_movreld per vehicle); the IDM terms of vehicle i + 1 do
+                // not depend on vehicle i's new position (only its clamp
+                // does), so the unrolled body overlaps them.  The loop leaves
+                // wave-uniformly past the wave's longest lane.
+#pragma unroll
+                for (int i = 1; i < RCAP; i++) {
+                    if (i < nm && i < n) {
+#else
                 for (int i = 1; i < nm; i++) {
                     if (i < n) {
+#endif
                         const float xi = X_[i], vi = vget<kL>(V_, Vc, i);
                         const float gap = (lead_x_old - P.length) - xi;
                         const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
@@ -1462,6 +1479,11 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                         last_x = xn;
                         last_v = vn;
                     }
+#if SIM_PASSC_UNROLL && SIM_PASSC_FENCE
+                    // (1024 threads: 128 VGPRs; an unfenced unroll hoists
+                    // later vehicles' reads and spills)
+                    if constexpr (kL) __builtin_amdgcn_sched_barrier(0);
+#endif
                 }
                 if (pop) {
 #pragma unroll

@@ -37,6 +37,10 @@ def main():
     subprocess.run(cmd, check=True)
     objs = [os.path.join(B.objdir(), os.path.basename(s) + ".o") for s in B._sources()
             if os.path.basename(s) != srcname] + [obj]
+    # the tree's source digest (dmdqn_source_digest): the variant is this tree
+    # plus switches, and loads only under DMDQN_ALLOW_FOREIGN_LIB=1 when swapped
+    # in (tools/ab_swap.sh) if its -D switches change the code
+    objs.append(B._digest_object("", B.tree_digest())[0])
     so = os.path.join(out, f"libdmdqn_hip_{name}.so")
     subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o", so] + objs,
                    check=True)
