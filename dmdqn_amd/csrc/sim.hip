@@ -1024,19 +1024,6 @@ __global__ void __launch_bounds__(256, 4) k_sim_step(dmdqn_sim S, dmdqn_idm Pa, 
 // Same passes, same IEEE operation order as the LDS path / oracle_sim.c
 // (bit-exact); the rings are written back compacted (head 0).
 constexpr int RCAP = 24;
-#ifndef SIM_STAGE_UNROLL
-#define SIM_STAGE_UNROLL 1  // 0: the round-5 staging / write-back loops (A/B)
-#endif
-#ifndef SIM_PASSC_UNROLL
-#define SIM_PASSC_UNROLL 1  // 0: pass C's rolled per-vehicle loop (A/B)
-#endif
-#ifndef SIM_PASSC_FENCE
-#define SIM_PASSC_FENCE 1  // a scheduling barrier per unrolled vehicle (1024-thread blocks)
-#endif
-#ifndef SIM_STAGE_CHUNK
-#define SIM_STAGE_CHUNK 8  // vehicles whose loads are in flight together
-#endif
-static_assert(RCAP % SIM_STAGE_CHUNK == 0, "whole staging chunks");
 
 __device__ __forceinline__ int wave_max_uniform(int x) {
 #pragma unroll
@@ -1184,40 +1171,6 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         DMDQN_DBG(h >= 0 && h < cap && n >= 0 && n <= RCAP && n <= cap, DBG_SIM_RING);
         const size_t base = (size_t)l * cap;
         const int nm = wave_max_uniform(n);
-#if SIM_STAGE_UNROLL
-        // in chunks of SIM_STAGE_CHUNK vehicles with constant register indices:
-        // every load of a chunk is in flight at once (a loop with a dynamic
-        // index waits for each load before its v_movreld: the wave's longest
-        // lane times a global round trip).  A chunk is skipped wave-uniformly
-        // past the wave's longest lane; a lane past its own count loads its
-        // ring's first slot (a valid address) and keeps nothing.
-#pragma unroll
-        for (int c = 0; c < RCAP; c += SIM_STAGE_CHUNK) {
-            if (c < nm) {
-                float xv[SIM_STAGE_CHUNK], vv[SIM_STAGE_CHUNK];
-                int dv[SIM_STAGE_CHUNK];
-#pragma unroll
-                for (int j = 0; j < SIM_STAGE_CHUNK; j++) {
-                    const int i = c + j;
-                    int sl = h + i;
-                    if (sl >= cap) sl -= cap;
-                    const size_t at = base + (i < n ? sl : 0);
-                    xv[j] = G.x[at];
-                    vv[j] = G.v[at];
-                    dv[j] = G.dst[at];
-                }
-#pragma unroll
-                for (int j = 0; j < SIM_STAGE_CHUNK; j++) {
-                    const int i = c + j;
-                    if (i < n) {
-                        X_[i] = xv[j];
-                        vset<kL>(V_, Vc, i, vv[j]);
-                        dset(D2_, i, dv[j]);
-                    }
-                }
-            }
-        }
-#else
         // loop counters are wave-uniform (bounded by the wave's longest lane):
         // the register arrays are then indexed with a scalar (s_set_gpr_idx)
         for (int i = 0; i < nm; i++) {
@@ -1229,7 +1182,6 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 dset(D2_, i, G.dst[base + sl]);
             }
         }
-#endif
         if (n > 0) {
             lx = G.x[base + (h + n - 1 < cap ? h + n - 1 : h + n - 1 - cap)];
             lv = G.v[base + (h + n - 1 < cap ? h + n - 1 : h + n - 1 - cap)];
@@ -1442,19 +1394,8 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 bool det = lead_x_new >= dp && lead_x_old0 < dpl;
                 float lead_x_old = lead_x_old0, lead_v_old = lead_v_old0;
                 float last_x = X_[0], last_v = vget<kL>(V_, Vc, 0);
-#if SIM_PASSC_UNROLL
-                // unrolled with constant register indices (no v_movrels /
-                // v_movreld per vehicle); the IDM terms of vehicle i + 1 do
-                // not depend on vehicle i's new position (only its clamp
-                // does), so the unrolled body overlaps them.  The loop leaves
-                // wave-uniformly past the wave's longest lane.
-#pragma unroll
-                for (int i = 1; i < RCAP; i++) {
-                    if (i < nm && i < n) {
-#else
                 for (int i = 1; i < nm; i++) {
                     if (i < n) {
-#endif
                         const float xi = X_[i], vi = vget<kL>(V_, Vc, i);
                         const float gap = (lead_x_old - P.length) - xi;
                         const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
@@ -1479,11 +1420,6 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                         last_x = xn;
                         last_v = vn;
                     }
-#if SIM_PASSC_UNROLL && SIM_PASSC_FENCE
-                    // (1024 threads: 128 VGPRs; an unfenced unroll hoists
-                    // later vehicles' reads and spills)
-                    if constexpr (kL) __builtin_amdgcn_sched_barrier(0);
-#endif
                 }
                 if (pop) {
 #pragma unroll
@@ -1589,18 +1525,6 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
             G.head[l] = 0;
             G.cnt[l] = n;
             const size_t base = (size_t)l * cap;
-#if SIM_STAGE_UNROLL
-            // constant register indices: no v_movrels per vehicle, the stores
-            // and the speed column's LDS reads issue back to back
-#pragma unroll
-            for (int i = 0; i < RCAP; i++) {
-                if (i < nm && i < n) {
-                    G.x[base + i] = X_[i];
-                    G.v[base + i] = vget<kL>(V_, Vc, i);
-                    G.dst[base + i] = dget(D2_, i);
-                }
-            }
-#else
             for (int i = 0; i < nm; i++) {
                 if (i < n) {
                     G.x[base + i] = X_[i];
@@ -1608,7 +1532,6 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                     G.dst[base + i] = dget(D2_, i);
                 }
             }
-#endif
         }
     }
     if (leader) G.qptr[tid] = qp;
