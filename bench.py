@@ -303,7 +303,7 @@ def auto_schedule(rows, cols, envs, shared, no_fuse, split_learn, cu_split, side
     return "env", cus, side_learn
 
 
-def make_streams(dev, cu_split=None, cu_stride=False, learn_priority=False):
+def make_streams(dev, cu_split=None, cu_stride=False, learn_priority=False, side_priority=False):
     """(learn stream, side stream or None) of bench.py: with cu_split, two
     CU-masked HIP streams (the side one on cu_split CUs: 0..k-1, or every
     n_cu/k-th CU with cu_stride; the learn stream on the rest), else one
@@ -313,8 +313,10 @@ def make_streams(dev, cu_split=None, cu_stride=False, learn_priority=False):
     then fill what the learn's dispatch leaves, its tail)."""
     import torch
     if not cu_split:
-        if learn_priority:
+        if learn_priority or side_priority:
             lo, hi = torch.cuda.Stream.priority_range()
+            if side_priority:  # the side stream's blocks take the CU slots the learn frees first
+                return torch.cuda.Stream(dev, priority=lo), torch.cuda.Stream(dev, priority=hi)
             return torch.cuda.Stream(dev, priority=hi), torch.cuda.Stream(dev, priority=lo)
         return torch.cuda.Stream(dev), None
     from dmdqn_amd._lib import cu_masked_stream
@@ -379,6 +381,9 @@ def main():
     ap.add_argument("--mark-every-learn", action="store_true",
                     help="overlap env: record the learn stream's ordering event behind every learn "
                          "(A/B; default every other one, which the ring's two spare slots allow)")
+    ap.add_argument("--side-priority", action="store_true",
+                    help="with --overlap sample/full/env/learn and no --cu-split: the side stream at "
+                         "the highest HIP stream priority, the learn stream at the lowest")
     ap.add_argument("--learn-priority", action="store_true",
                     help="with --overlap sample/full/env and no --cu-split: the learn stream at "
                          "the highest HIP stream priority, the side stream at the lowest")
@@ -423,9 +428,12 @@ def main():
             args.cu_split, args.side_learn)
     if args.side_learn is None:
         args.side_learn = 0
-    if args.learn_priority and args.cu_split:
-        ap.error("--learn-priority: CU-masked streams have no priority")
-    work, side = make_streams(dev, args.cu_split, args.cu_stride, args.learn_priority)
+    if (args.learn_priority or args.side_priority) and args.cu_split:
+        ap.error("--learn-priority / --side-priority: CU-masked streams have no priority")
+    if args.learn_priority and args.side_priority:
+        ap.error("--learn-priority and --side-priority exclude each other")
+    work, side = make_streams(dev, args.cu_split, args.cu_stride, args.learn_priority,
+                              args.side_priority)
     torch.cuda.set_stream(work)
     env_cfg = EnvConfig(rows=args.rows, cols=args.cols, num_envs=args.envs, seed=1000,
                         env_offset=rank * args.envs)
@@ -600,6 +608,7 @@ def main():
                             + (f"; side stream on {args.cu_split} CUs"
                                + (" (strided)" if args.cu_stride else "") if args.cu_split else "")
                             + ("; learn stream at high priority" if args.learn_priority else "")
+                            + ("; side stream at high priority" if args.side_priority else "")
                             + (f"; the learn of {args.side_learn} agents on the side stream"
                                if args.side_learn else ""),
             },
