@@ -373,6 +373,9 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
 // ---------------------------------------------------------------- pass 1: S'
 // LDS: both nets (2 x 58,896 B) + per wave: rewards f64 [128], ring slots
 // [128], transition word (a | done << 8) [128], z-scored rewards f32 [128].
+#ifndef SH_B4
+#define SH_B4 0  // 1: the barrier between an agent's dW1 and the next agent's L1 (round 5)
+#endif
 #ifndef NEXT_NT
 #define NEXT_NT 2  // 16-row tiles per weight read in k_shared_next
 #endif
@@ -970,7 +973,16 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
         yv = yn;
         avl = an;
         SH_STAMP(agent, 6, threadIdx.x);
+#if SH_B4
         __syncthreads();  // B4: the images are rewritten by the next agent
+#endif
+        // (round 6: no barrier here.  What the next agent's L1 writes, H1's
+        // own columns, every wave last read in dW2 -- before the pair barrier
+        // above; L1 reads the other X buffer, which RQ committed before B3.
+        // The later writes wait for B1: L2's H2 columns, which dW1 reads; RQ's
+        // X commit into this agent's buffer, dZ2 rows, DQ and loss partials.
+        // So waves that finish dW1 early start the next agent's L1 MFMAs
+        // beside the others' dW1.)
         SH_STAMP(agent, 7, threadIdx.x);
     }
     // partial sums of this workgroup, kernel layout (every index written once)
