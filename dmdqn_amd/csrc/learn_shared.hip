@@ -373,9 +373,6 @@ __device__ __forceinline__ void fwd_tiles(const Net &N, const half8 (&bx)[NT][3]
 // ---------------------------------------------------------------- pass 1: S'
 // LDS: both nets (2 x 58,896 B) + per wave: rewards f64 [128], ring slots
 // [128], transition word (a | done << 8) [128], z-scored rewards f32 [128].
-#ifndef SH_GRAD
-#define SH_GRAD 7  // 7: the half-agent software-pipelined gradient pass; 4: grad4 (A/B)
-#endif
 #ifndef SH_B4
 #define SH_B4 0  // 1: the barrier between an agent's dW1 and the next agent's L1 (round 5)
 #endif
@@ -547,7 +544,10 @@ __device__ __forceinline__ void row_loss(int kind, float diff, float &term, floa
 // template here until round 4; it lives on in git history -- rebuild it for a
 // same-box A/B with tools/build_rev.py 2d71bef <name> -DSH_GRAD=3.  Round 5's
 // one-wave-per-SIMD variant k_shared_grad6 (4 waves, two neuron tiles each;
-// slower): tools/build_rev.py 21344f7 <name> -DSH_GRAD=6.)
+// slower): tools/build_rev.py 21344f7 <name> -DSH_GRAD=6.  Round
+// 6's k_shared_grad7 (half-agent chunks, forward of chunk q beside the
+// backward of chunk q - 1, double-buffered images; bit-identical, 9 % slower):
+// tools/build_rev.py f08126b <name>.)
 namespace gx {
 constexpr int X_BYTES = B_ * DP * 2;             // [128][96] f16
 constexpr int IMG = B_ * H * 2;                  // [128][128] f16
@@ -1029,353 +1029,6 @@ __global__ void __launch_bounds__(512, 1) k_shared_grad4(dmdqn_learn_args a, con
 
 }  // namespace g4
 
-// ---------------------------------------------------------------- pass 2, v7
-// grad4's phases software-pipelined over HALF agents (round 6).  A 64-row
-// chunk is half an agent's batch; the images of two chunks (three X buffers)
-// fit where grad4 held one agent's, so every barrier-separated segment runs
-// the forward of chunk q beside the backward of chunk q - 1 -- two independent
-// streams of LDS reads and MFMAs per wave between barriers instead of one:
-//   S1  L1(q)  X -> H1 own columns        ||  dW2(q-1), dW3(q-1)
-//   S2  L2(q)  H1 -> H2 own columns       ||  dH1(q-1) -> dZ1 over H2(q-1) own
-//   S3  RQ(q)  rows of waves 4h..4h+3     ||  dW1(q-1) ; X(q+1) committed
-// Every gradient accumulator takes the same MFMA chain as grad4's (per agent
-// the 32-row K-steps 0..3 in order: chunk 0 gives steps 0-1, chunk 1 steps
-// 2-3), and the loss / Q statistics the same partials in the same order, so
-// the slabs are bit-identical to grad4's.  Chunk q of the workgroup's walk is
-// half q & 1 of agent blockIdx.x + (q >> 1) gridDim.x.
-namespace g7 {
-using gx::IMG;
-constexpr int CH = 64;                              // rows per chunk
-constexpr int XB = CH * DP * 2;                     // one X image [64][96] f16
-constexpr int HB = CH * H * 2;                      // one activation image [64][128] f16
-constexpr int OFF_X = 0;                            // three X buffers
-constexpr int OFF_H1 = 3 * XB;                      // two each of H1, H2 (then dZ1), Z2
-constexpr int OFF_H2 = OFF_H1 + 2 * HB;
-constexpr int OFF_Z2 = OFF_H2 + 2 * HB;
-constexpr int OFF_DQ = OFF_Z2 + 2 * HB;             // two [64][16]
-constexpr int W3LD = g4::W3LD, W3ROWS = g4::W3ROWS;
-constexpr int OFF_W3 = OFF_DQ + 2 * CH * 16 * 2;
-constexpr int OFF_SC = OFF_W3 + W3ROWS * W3LD * 2;  // sloss [8]
-constexpr int OFF_QS = OFF_SC + 32;                 // Q statistics [8][6]
-constexpr int LDS = OFF_QS + 8 * 6 * 4;
-static_assert(LDS <= 160 * 1024, "k_shared_grad7 LDS");
-static_assert(OFF_W3 % 16 == 0 && OFF_H1 % 16 == 0, "aligned images");
-
-// deque position of staging part `part` (2 parts per row, 128 parts per
-// chunk) of chunk q's rows, branch-free at a valid address (as gx::pos3)
-__device__ __forceinline__ int cpos(const dmdqn_learn_args &a, int q, int part) {
-    int ag = blockIdx.x + (q >> 1) * (int)gridDim.x;
-    ag = ag < a.NA ? ag : a.NA - 1;
-    return a.idx[(size_t)ag * B_ + CH * (q & 1) + ((part >> 1) & (CH - 1))];
-}
-
-__device__ __forceinline__ int chunk_agent(int q) { return blockIdx.x + (q >> 1) * (int)gridDim.x; }
-
-template <bool QSTATS>
-__global__ void __launch_bounds__(512, 1) k_shared_grad7(dmdqn_learn_args a, const float *y_in,
-                                                       const uint8_t *act_in, float *slab) {
-    constexpr int NTH = 512;
-    __shared__ __attribute__((aligned(16))) char smem[LDS];
-    h16 *W3I = reinterpret_cast<h16 *>(smem + OFF_W3);
-    float *sloss = reinterpret_cast<float *>(smem + OFF_SC);
-    float *sqs = reinterpret_cast<float *>(smem + OFF_QS);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    const h16 *WH = reinterpret_cast<const h16 *>(a.params_h);
-    g4::WSlice4 W;
-    g4::load_slice4(WH, w, W);
-    for (int k = threadIdx.x; k < W3ROWS * H; k += NTH)
-        W3I[(k / H) * W3LD + (k % H)] = WH[L::oW3T + (k & (NACT * H - 1))];
-    half8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; e++) ones[e] = (h16)1.0f;
-    f32x4 G1[6], G2[8], G3, GB1, GB2, GB3;
-    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < 6; f++) G1[f] = z4;
-#pragma unroll
-    for (int j = 0; j < 8; j++) G2[j] = z4;
-    G3 = GB1 = GB2 = GB3 = z4;
-    for (int k = threadIdx.x; k < 2 * CH * 16; k += NTH)
-        reinterpret_cast<h16 *>(smem + OFF_DQ)[k] = (h16)0.0f;
-    int wv = w;
-    asm volatile("" : "+v"(wv));
-    const int half_w = wv >> 2;           // the chunk half whose rows this wave takes in RQ
-    const int rt = wv & 3;                // its row tile within the chunk
-    const int bR = hoff(i, 8 * g), bX = hoff<DP>(i, 8 * g);
-    const int trH[2] = {hsplit(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    const int trX[2] = {hsplit<DP>(8 * (g & 1) + (i >> 2), 4 * (i & 3), g >> 1, 0),
-                        hsplit<DP>(8 * (g & 1) + (i >> 2), 16 + 4 * (i & 3), g >> 1, 0)};
-    const int c0 = 16 * wv;
-    const int bW = hoff(i, (c0 & 16) + 4 * g) + 256 * (c0 >> 5);
-    const int trO = hsplit(8 * (g & 1) + (i >> 2), (c0 & 16) + 4 * (i & 3), g >> 1, 0) + 256 * (c0 >> 5);
-    const int cP = 16 * (wv ^ 1), hh = wv & 1;
-    const int trP = hsplit(8 * (g & 1) + (i >> 2), (cP & 16) + 4 * (i & 3), g >> 1, 0) + 256 * (cP >> 5);
-    int hB[4], xB[3];
-#pragma unroll
-    for (int jj = 0; jj < 4; jj++) {
-        const int jt = 4 * hh + jj;
-        hB[jj] = (jj & 1 ? trH[1] : trH[0]) + 256 * (jt >> 1);
-    }
-#pragma unroll
-    for (int ff = 0; ff < 3; ff++) {
-        const int ft = 3 * hh + ff;
-        xB[ff] = (ft & 1 ? trX[1] : trX[0]) + 256 * (ft >> 1);
-    }
-    // chunks of this workgroup: two per agent it walks
-    const int nag = a.NA > (int)blockIdx.x ? (a.NA - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-    const int Q = 2 * nag;
-    const bool stager = threadIdx.x < 2 * CH;  // 128 parts of 48 B per chunk
-    const int part = threadIdx.x & (2 * CH - 1);
-    if (Q > 0) {
-        gx::XRows x0;
-        gx::xrows_issue<NTH>(a, chunk_agent(0), cpos(a, 0, part), part, x0);
-        if (stager) gx::xrows_commit(x0, reinterpret_cast<h16 *>(smem + OFF_X), part);
-    }
-    int npos = cpos(a, 1, part);  // the positions of the chunk staged next
-    // this wave's RQ row (agent-relative 16w + i): target and action, loaded
-    // one agent ahead
-    float yv = 0.0f;
-    int avl = 0;
-    if (Q > 0) {
-        const int ag = chunk_agent(0);
-        yv = y_in[(size_t)ag * B_ + 16 * wv + i];
-        avl = act_in[(size_t)ag * B_ + 16 * wv + i];
-    }
-    float yn = yv;
-    int an = avl;
-    __syncthreads();
-    for (int q = 0; q <= Q; q++) {
-        const bool fwd = q < Q, bwd = q > 0;
-        const int hb = q & 1, hp = hb ^ 1;                     // this / the previous chunk's images
-        const h16 *Xq = reinterpret_cast<const h16 *>(smem + OFF_X + (q % 3) * XB);
-        const h16 *Xp = reinterpret_cast<const h16 *>(smem + OFF_X + ((q + 2) % 3) * XB);
-        h16 *H1q = reinterpret_cast<h16 *>(smem + OFF_H1 + hb * HB);
-        h16 *H1p = reinterpret_cast<h16 *>(smem + OFF_H1 + hp * HB);
-        h16 *H2q = reinterpret_cast<h16 *>(smem + OFF_H2 + hb * HB);
-        h16 *H2p = reinterpret_cast<h16 *>(smem + OFF_H2 + hp * HB);
-        h16 *Z2q = reinterpret_cast<h16 *>(smem + OFF_Z2 + hb * HB);
-        h16 *Z2p = reinterpret_cast<h16 *>(smem + OFF_Z2 + hp * HB);
-        h16 *DQq = reinterpret_cast<h16 *>(smem + OFF_DQ + hb * CH * 16 * 2);
-        h16 *DQp = reinterpret_cast<h16 *>(smem + OFF_DQ + hp * CH * 16 * 2);
-        // look-ahead: chunk q + 1's X rows (committed in S3), the positions of
-        // chunk q + 2, and at an agent's first chunk the next agent's targets
-        gx::XRows xn;
-        gx::xrows_issue<NTH>(a, min(chunk_agent(q + 1), a.NA - 1), npos, part, xn);
-        npos = cpos(a, q + 2, part);
-        if ((q & 1) == 0) {
-            int ag = chunk_agent(q + 2);
-            ag = ag < a.NA ? ag : a.NA - 1;
-            yn = y_in[(size_t)ag * B_ + 16 * wv + i];
-            an = act_in[(size_t)ag * B_ + 16 * wv + i];
-        }
-        // ---- S1: L1(q) || dW2(q-1), dW3(q-1)
-        if (fwd) {
-            f32x4 c[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) c[r] = z4;
-#pragma unroll
-            for (int s = 0; s < 3; s++) {
-                half8 xb[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-                    xb[r] = *reinterpret_cast<const half8 *>(Xq + bX + 16 * DP * r + 256 * s);
-#pragma unroll
-                for (int r = 0; r < 4; r++) c[r] = mfma(W.w1[s], xb[r], c[r]);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-                *reinterpret_cast<half4v *>(H1q + bW + 16 * H * r) = gx::relu4(c[r], W.b1);
-        }
-        if (bwd) {
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const half8 dqf = frag_tr(DQp, 16, 32 * s, 0);
-                G3 = mfma(frag_tr_p(H2p + trO + 2 * 16 * H * s), dqf, G3);
-                if (w == 0) GB3 = mfma(ones, dqf, GB3);
-            }
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const half8 bqA = frag_tr_p(Z2p + trO + 2 * 16 * H * s);
-                const half8 bqB = frag_tr_p(Z2p + trP + 2 * 16 * H * s);
-                GB2 = mfma(ones, bqA, GB2);
-#pragma unroll
-                for (int jj = 0; jj < 4; jj++) {
-                    const half8 av = frag_tr_p(H1p + hB[jj] + 2 * 16 * H * s);
-                    G2[2 * jj] = mfma(av, bqA, G2[2 * jj]);
-                    G2[2 * jj + 1] = mfma(av, bqB, G2[2 * jj + 1]);
-                }
-            }
-        }
-        __syncthreads();  // H1(q) complete; Z2 / H1 / DQ(q-1) reads done
-        // ---- S2: L2(q) || dH1(q-1) -> dZ1 over H2(q-1) own columns
-        if (fwd) {
-            f32x4 c[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) c[r] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 hbv[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-                    hbv[r] = *reinterpret_cast<const half8 *>(H1q + bR + 16 * H * r + 256 * s);
-#pragma unroll
-                for (int r = 0; r < 4; r++) c[r] = mfma(W.w2[s], hbv[r], c[r]);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-                *reinterpret_cast<half4v *>(H2q + bW + 16 * H * r) = gx::relu4(c[r], W.b2);
-        }
-        if (bwd) {
-            f32x4 c[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) c[r] = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 zb[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-                    zb[r] = *reinterpret_cast<const half8 *>(Z2p + bR + 16 * H * r + 256 * s);
-#pragma unroll
-                for (int r = 0; r < 4; r++) c[r] = mfma(W.w2b[s], zb[r], c[r]);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                half4v o;
-                const half4v hv = *reinterpret_cast<const half4v *>(H1p + bW + 16 * H * r);
-#pragma unroll
-                for (int e = 0; e < 4; e++) o[e] = hv[e] > (h16)0.0f ? (h16)c[r][e] : (h16)0.0f;
-                *reinterpret_cast<half4v *>(H2p + bW + 16 * H * r) = o;
-            }
-        }
-        __syncthreads();  // H2(q) and dZ1(q-1) complete
-        // ---- S3: RQ(q) on waves 4h..4h+3 || dW1(q-1) ; X(q+1)
-        if (fwd && half_w == hb) {
-            half8 h2r[4];
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                h2r[s] = *reinterpret_cast<const half8 *>(H2q + bR + 16 * H * rt + 256 * s);
-            f32x4 cq = z4;
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                cq = mfma(*reinterpret_cast<const half8 *>(W3I + (i % W3ROWS) * W3LD + 32 * s + 8 * g),
-                          h2r[s], cq);
-            float qv[4];
-#pragma unroll
-            for (int e = 0; e < 4; e++) qv[e] = r16(r16(cq[e]) + (float)W.b3[e]);
-            const float qa = gx::pickf4(qv[0], qv[1], qv[2], qv[3], avl);
-            float term, dq;
-            row_loss(a.loss_kind, __fsub_rn(qa, yv), term, dq);
-            dq = r16(dq);
-            const int row = 16 * rt + i;  // chunk-relative
-            if (g == 0) {
-                half4v d;
-#pragma unroll
-                for (int e = 0; e < 4; e++) d[e] = e == avl ? (h16)dq : (h16)0.0f;
-                *reinterpret_cast<half4v *>(DQq + row * 16) = d;
-            }
-            if (QSTATS) {
-                const float s1 = g4::row16_sum((qv[0] + qv[1]) + (qv[2] + qv[3]));
-                const float s2 = g4::row16_sum((qv[0] * qv[0] + qv[1] * qv[1]) + (qv[2] * qv[2] + qv[3] * qv[3]));
-                if (l == 0) {
-                    sqs[w * 6 + 0] = s1;
-                    sqs[w * 6 + 1] = s2;
-                }
-#pragma unroll
-                for (int e = 0; e < NACT; e++) {
-                    const float cnt = (float)__popcll(__ballot(g == 0 && avl == e));
-                    if (l == 0) sqs[w * 6 + 2 + e] = cnt;
-                }
-            }
-            term = g4::row16_sum(term);
-            if (l == 0) sloss[w] = term;
-            half8 w3[4];
-#pragma unroll
-            for (int s = 0; s < 4; s++) w3[s] = *reinterpret_cast<const half8 *>(W3I + avl * W3LD + 32 * s + 8 * g);
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                half8 o;
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                    o[e] = h2r[s][e] > (h16)0.0f ? (h16)(dq * (float)w3[s][e]) : (h16)0.0f;
-                *reinterpret_cast<half8 *>(Z2q + bR + 16 * H * rt + 256 * s) = o;
-            }
-            // this wave's row is done for the agent: the next agent's target
-            yv = yn;
-            avl = an;
-        }
-        if (bwd) {
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const half8 bvA = frag_tr_p(H2p + trO + 2 * 16 * H * s);
-                const half8 bvB = frag_tr_p(H2p + trP + 2 * 16 * H * s);
-                GB1 = mfma(ones, bvA, GB1);
-#pragma unroll
-                for (int ff = 0; ff < 3; ff++) {
-                    const half8 xv = frag_tr_p(Xp + xB[ff] + 2 * 16 * DP * s);
-                    G1[2 * ff] = mfma(xv, bvA, G1[2 * ff]);
-                    G1[2 * ff + 1] = mfma(xv, bvB, G1[2 * ff + 1]);
-                }
-            }
-        }
-        if (q + 1 < Q && stager)
-            gx::xrows_commit(xn, reinterpret_cast<h16 *>(smem + OFF_X + ((q + 1) % 3) * XB), part);
-        __syncthreads();  // DQ, dZ2, loss partials of chunk q; X(q+1); dW1(q-1) reads done
-        if (fwd && hb == 1) {  // the agent's second half: its loss and Q statistics
-            const int agent = chunk_agent(q);
-            if (threadIdx.x == 0 && a.loss) {
-                float ls = sloss[0];
-                for (int v = 1; v < 8; v++) ls += sloss[v];
-                a.loss[agent] = ls / (float)B_;
-            }
-            if (QSTATS && threadIdx.x < 6) {
-                float t = sqs[threadIdx.x];
-                for (int v = 1; v < 8; v++) t += sqs[v * 6 + threadIdx.x];
-                a.qstats[(size_t)agent * 6 + threadIdx.x] += t;
-            }
-        }
-    }
-    // partial sums of this workgroup, kernel layout (as grad4)
-    float *G = slab + (size_t)blockIdx.x * L::P;
-    const int n0 = 16 * w, n = n0 + i;
-    if (i < NACT)
-        *reinterpret_cast<float4 *>(G + L::oW3T + i * H + n0 + 4 * g) =
-            make_float4(G3[0], G3[1], G3[2], G3[3]);
-    {
-        const int nB = 16 * (w ^ 1) + i;
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-            const int j0 = 16 * (4 * hh + jj) + 4 * g;
-            *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(n, j0, H)) =
-                make_float4(G2[2 * jj][0], G2[2 * jj][1], G2[2 * jj][2], G2[2 * jj][3]);
-            *reinterpret_cast<float4 *>(G + L::oW2T + qn_wt(nB, j0, H)) =
-                make_float4(G2[2 * jj + 1][0], G2[2 * jj + 1][1], G2[2 * jj + 1][2], G2[2 * jj + 1][3]);
-        }
-#pragma unroll
-        for (int ff = 0; ff < 3; ff++) {
-            const int ft = 3 * hh + ff;
-            if (ft < 5 || g < 2) {
-                *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(n, 16 * ft + 4 * g)) =
-                    make_float4(G1[2 * ff][0], G1[2 * ff][1], G1[2 * ff][2], G1[2 * ff][3]);
-                *reinterpret_cast<float4 *>(G + L::oW1T + qn_w1<H>(nB, 16 * ft + 4 * g)) =
-                    make_float4(G1[2 * ff + 1][0], G1[2 * ff + 1][1], G1[2 * ff + 1][2],
-                                G1[2 * ff + 1][3]);
-            }
-            if (ft == 5 && g == 2) {
-                G[L::oW1X + n] = G1[2 * ff][0];
-                G[L::oW1X + nB] = G1[2 * ff + 1][0];
-            }
-        }
-    }
-    if (g == 0) {
-        G[L::ob2 + n] = GB2[0];
-        G[L::ob1 + n] = GB1[0];
-    }
-    if (w == 0 && g == 0 && i < NACT) G[L::ob3 + i] = GB3[0];
-}
-
-}  // namespace g7
-
 
 
 
@@ -1393,11 +1046,7 @@ int launch_shared_v2(const dmdqn_learn_args *a, float *y, uint8_t *act, float *s
     const int next_blocks = next_wg < n_slabs ? next_wg : n_slabs;
     hipLaunchKernelGGL(k_shared_next, dim3(next_blocks), dim3(64 * NEXT_WAVES), 0, s, *a, y, act);
     DMDQN_LAUNCH_CHECK("k_shared_next");
-#if SH_GRAD == 7
-    auto k = a->qstats ? g7::k_shared_grad7<true> : g7::k_shared_grad7<false>;
-#else
     auto k = a->qstats ? g4::k_shared_grad4<true> : g4::k_shared_grad4<false>;
-#endif
     hipLaunchKernelGGL(k, dim3(n_slabs), dim3(512), 0, s, *a, y, act, slab);
     DMDQN_LAUNCH_CHECK("k_shared_grad");
     return DMDQN_OK;
