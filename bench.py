@@ -369,7 +369,7 @@ def main():
                          "and the learn stream on the rest (CU-masked HIP streams)")
     ap.add_argument("--cu-stride", action="store_true",
                     help="--cu-split picks every k-th CU instead of CUs 0..N-1")
-    ap.add_argument("--time-every", type=int, default=4,
+    ap.add_argument("--time-every", type=int, default=8,
                     help="bracket every k-th learn launch of the timed region with timing "
                          "events (the roofline's average launch duration; 1 = every launch)")
     ap.add_argument("--side-learn", type=int, default=None,
