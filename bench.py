@@ -174,6 +174,7 @@ def _sim_roofline(E, K, vbar, sim_ms, traffic, traffic_src, traffic_stale, in_ld
 
 
 SIM_PROBE_STEPS = 10  # untimed steps after the timed region that time the sim
+LEARN_PROBE_LAUNCHES = 6  # learns timed alone after the timed region
 STREAM_PROBE_BYTES = 4 << 30  # bytes copied per launch by the HBM streaming probe
 STREAM_PROBE_REPS = 5
 
@@ -369,9 +370,12 @@ def main():
                          "and the learn stream on the rest (CU-masked HIP streams)")
     ap.add_argument("--cu-stride", action="store_true",
                     help="--cu-split picks every k-th CU instead of CUs 0..N-1")
-    ap.add_argument("--time-every", type=int, default=8,
+    ap.add_argument("--time-every", type=int, default=7,
                     help="bracket every k-th learn launch of the timed region with timing "
-                         "events (the roofline's average launch duration; 1 = every launch)")
+                         "events (the roofline's average launch duration; 1 = every launch). "
+                         "Odd by default: under the env schedule the learn alternates between "
+                         "running alone and beside the side stream's env step (period 2), and "
+                         "an even stride would time only one kind")
     ap.add_argument("--side-learn", type=int, default=None,
                     help="overlap env: learn this many agents on the side stream behind its env "
                          "step (default with --overlap auto: one per side-stream CU; else 0)")
@@ -495,6 +499,22 @@ def main():
     D.barrier(args.dist_timeout)
     tr.agent.learn_hook = None
     n_learn = tr.agent.learn_launches - learn_before
+
+    # Learn-alone probe, after the timed region: LEARN_PROBE_LAUNCHES learns on
+    # the learn stream with nothing beside them (the side stream drained), each
+    # bracketed by timing events -- the kernel's own rate, beside the timed
+    # region's average under the schedule's overlap (roofline.avg_launch_ms)
+    tr.synchronize()
+    alone_ms = []
+    for _ in range(LEARN_PROBE_LAUNCHES):
+        if not tr.agent.learn_begin():
+            break
+        e0, e1 = TimingEvent(), TimingEvent()
+        e0.record(work)
+        tr.agent.learn_range(0, NA)
+        e1.record(work)
+        e1.synchronize()
+        alone_ms.append(e0.elapsed_time(e1))
 
     # Sim probe, after the timed region.  Timing (the envs advance without
     # being observed): SIM_PROBE_STEPS k_sim_step launches back to back between
@@ -648,6 +668,19 @@ def main():
             "bytes_per_launch": bpl,
             **timing,
         }
+        if alone_ms:
+            # the learn kernel alone (the learn-alone probe above): over every agent
+            bpl_alone = ((NA * 128 * REPLAY_ROW_BYTES + 28 * P) if args.shared
+                         else NA * learn_bytes_per_agent(P))
+            a_s = float(np.median(alone_ms)) / 1e3
+            hbm_roof["learn_alone"] = {
+                "avg_launch_ms": round(float(np.mean(alone_ms)), 4),
+                "median_launch_ms": round(a_s * 1e3, 4), "launches": len(alone_ms),
+                "bytes_per_launch": bpl_alone, "achieved": round(bpl_alone / a_s / 1e9, 1),
+                "frac": round(bpl_alone / a_s / 1e9 / HBM_PEAK_GBS, 4),
+                "note": "the same learn launched alone after the timed region (side stream "
+                        "drained); roofline.avg_launch_ms is the timed region's average under "
+                        "the schedule's overlap"}
         if probe and "skipped" in probe:
             hbm_roof["probe"] = probe
         elif probe:
@@ -680,6 +713,14 @@ def main():
             # by the matrix cores and its HBM figure is the secondary one
             out["roofline"] = {**mfma_roof, "traffic": traffic, "traffic_source": traffic_src,
                                "traffic_stale": traffic_stale, **timing}
+            if alone_ms:
+                a_s = float(np.median(alone_ms)) / 1e3
+                fl = NA * LEARN_FLOP_PER_AGENT
+                out["roofline"]["learn_alone"] = {
+                    "median_launch_ms": round(a_s * 1e3, 4), "launches": len(alone_ms),
+                    "achieved": round(fl / a_s / 1e12, 2),
+                    "frac": round(fl / a_s / 1e12 / MFMA_PEAK_TFLOPS[args.precision], 4),
+                    "note": "the shared learn launched alone after the timed region"}
             out["hbm"] = hbm_roof
         else:
             out["roofline"] = hbm_roof
