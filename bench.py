@@ -382,6 +382,10 @@ def main():
     ap.add_argument("--fenced-events", action="store_true",
                     help="overlap env: order the side stream after the learns with default "
                          "(system-scope) events instead of ordering-only ones (A/B)")
+    ap.add_argument("--ring-spare", type=int, default=2,
+                    help="replay-ring slots beyond replay_buffer_size (AgentConfig.ring_spare): "
+                         "under overlap env the side stream runs up to this many env steps ahead "
+                         "and the learn stream marks every this-many-th learn")
     ap.add_argument("--mark-every-learn", action="store_true",
                     help="overlap env: record the learn stream's ordering event behind every learn "
                          "(A/B; default every other one, which the ring's two spare slots allow)")
@@ -443,7 +447,7 @@ def main():
                         env_offset=rank * args.envs)
     # independent nets are seeded per rank; the shared net must start identical on every rank
     agent_cfg = AgentConfig(precision=args.precision, seed=1000 if args.shared else 1000 + rank,
-                            shared_params=args.shared)
+                            shared_params=args.shared, ring_spare=args.ring_spare)
     tr = Trainer(env_cfg, agent_cfg, device=dev, overlap=args.overlap, side_stream=side,
                  split_learn=args.split_learn, fused=not args.no_fuse,
                  war_events=not args.fenced_events, side_learn=args.side_learn,

@@ -240,6 +240,10 @@ class AgentConfig:
     # raise) | "f32" (any observation value, as dqn_agent.py:39-56 stores it;
     # the per-agent drop-in DQNAgent uses it)
     replay_rows: str = "int8"
+    # physical ring slots beyond replay_buffer_size (kernels.ReplayRing): with
+    # s spare slots the trainer's "env" schedule lets its side stream run up to
+    # s env steps ahead of the learn, which marks every s-th learn for it
+    ring_spare: int = 2
 
     @classmethod
     def from_dict(cls, d):
@@ -312,7 +316,8 @@ class BatchedDQN:
             raise ValueError("replay_rows must be 'int8' or 'f32'")
         if self.shared and cfg.replay_rows != "int8":
             raise ValueError("the shared-network learn reads int8 replay rows only")
-        self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev, row_format=cfg.replay_rows)
+        self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev, row_format=cfg.replay_rows,
+                                 spare=cfg.ring_spare)
         self._xs = self._xn = None  # float rows: the learn's pre-gathered batch
         if streams is not None:
             # shared (np_state, py_state) device streams, e.g. the process-global

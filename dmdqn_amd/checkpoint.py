@@ -26,7 +26,7 @@ import os
 import numpy as np
 import torch
 
-# 8: replay rings of cap + 2 slots (kernels.ReplayRing.SPARE); 7: cap + 1 slots,
+# 8: replay rings of cap + ring_spare slots (kernels.ReplayRing, default 2); 7: cap + 1 slots,
 # the written slots saved;
 # 6: + per-replica clocks and episode counters; 5: + the actuated-mode detector
 # times; 4: 128-B replay rows, unpadded W1T
@@ -41,12 +41,13 @@ _AGENT_TENSORS = ["params", "target", "adam_m", "adam_v", "np_state", "py_state"
 # different value would restore tensors that mean something else (or leave
 # derived state stale), so load() refuses it.
 _AGENT_FIXED = ["precision", "shared_params", "nn_layers", "replay_buffer_size", "batch_size",
-                "seed", "loss", "target_update_frequency", "count_env_steps", "replay_rows"]
+                "seed", "loss", "target_update_frequency", "count_env_steps", "replay_rows",
+                "ring_spare"]
 _ENV_FIXED = ["rows", "cols", "num_envs", "env_offset", "seed", "signal_features", "cap_lane",
               "end_ms", "period_ms", "step_duration", "max_sim_time", "action_stride", "scenario",
               "actuated"]
 # fields added after format 4 was introduced
-_DEFAULTS = {"loss": "mse", "actuated": False, "replay_rows": "int8"}
+_DEFAULTS = {"loss": "mse", "actuated": False, "replay_rows": "int8", "ring_spare": 2}
 
 
 def _written(total, ring):

@@ -100,13 +100,16 @@ class ReplayRing:
     per-agent drop-in surface): float32 rows of ROW_FLOATS, every value kept
     as the reference's buffer keeps it (dqn_agent.py:39-56)."""
 
-    SPARE = 2  # physical slots beyond the deque's maxlen (round 6; 1 before)
+    SPARE = 2  # default physical slots beyond the deque's maxlen (round 6; 1 before)
 
-    def __init__(self, NA, cap, device="cuda", row_format="int8"):
+    def __init__(self, NA, cap, device="cuda", row_format="int8", spare=None):
         if row_format not in ("int8", "f32"):
             raise ValueError("row_format must be 'int8' or 'f32'")
-        self.NA, self.cap, self.row_format = NA, cap, row_format
-        self.slots = S = cap + self.SPARE
+        spare = self.SPARE if spare is None else int(spare)
+        if spare < 1:
+            raise ValueError("a replay ring needs at least one spare slot")
+        self.NA, self.cap, self.row_format, self.spare = NA, cap, row_format, spare
+        self.slots = S = cap + spare
         z = dict(device=device)
         if row_format == "f32":
             self.s = torch.zeros((NA, S, ROW_FLOATS), dtype=torch.float32, **z)

@@ -139,17 +139,20 @@ class Trainer:
         # a learn's output): the learn -> side-stream wait only orders the store
         # of t+2 after learn t's ring reads, so it uses ordering-only events
         # (_lib.OrderEvent, no cache write-back between the learns) from a ring
-        self._war_ring = ([_lib.OrderEvent() for _ in range(4)]
+        # (more events than marks can be alive: a wait never meets a re-record)
+        self._war_ring = ([_lib.OrderEvent() for _ in range(max(4, self.agent.ring.spare + 2))]
                           if war_events and overlap == "env" else None)
         self._war_i = 0
         # overlap "env": (call index, event) of the learns the side stream may
         # wait for, newest last.  The store of call k overwrites the slot of
         # store k - slots, which the learns of calls up to k - 1 - spare read
-        # (kernels.ReplayRing.SPARE), so env step k waits for the newest marked
-        # learn of a call <= k - 2 -- never learn k - 1, beside which it runs.
-        # With 2 spare slots any learn of call k - 3 or k - 2 will do, so under
-        # ordering-only events the learn stream marks every other learn
-        # (a marker packet less per two steps between its kernels).
+        # (kernels.ReplayRing, spare = AgentConfig.ring_spare), so env step k
+        # waits for the newest marked learn of a call <= k - 2 -- never learn
+        # k - 1, beside which it runs.  Any learn of calls k - 1 - spare ..
+        # k - 2 will do, so under ordering-only events the learn stream marks
+        # every spare-th learn, and the side stream runs up to `spare` env
+        # steps ahead (C3 / C2 measured faster with 2 than with a mark per
+        # learn: profiles/r06/c3_marks, c2_marks).
         self._marks = []
         self._calls = 0
         self._first_learn = None  # the call of the first learn (always marked)
@@ -303,7 +306,7 @@ class Trainer:
                 ev.wait(side)
             else:
                 side.wait_event(ev)
-        self._marks = [m for m in self._marks if m[0] >= k - 3]
+        self._marks = [m for m in self._marks if m[0] >= k - 1 - spare]
         if agent.current_epsilon() < 1.0 and self._ev_learn is not None:
             # greedy act reads the updated weights (recorded as a full event:
             # an ordering-only one is used only while epsilon is fixed at 1)
@@ -332,11 +335,13 @@ class Trainer:
             loss = agent.learn_range(0, agent.NA - self.side_learn)
         war = (self._war_ring is not None and not agent.cfg.count_env_steps
                and agent.current_epsilon() >= 1.0)
-        if (learned and war and spare >= 2 and k % 2 and not self._mark_every
+        if (learned and war and spare >= 2 and not self._mark_every
                 and self._first_learn is not None
-                and self._first_learn != k):
-            # odd call under ordering-only events: no marker (the side stream's
-            # next waits are covered by the marks of calls k - 1 and k + 1)
+                and (k - self._first_learn) % spare):
+            # under ordering-only events only every spare-th learn is marked
+            # (from the first on): any `spare` consecutive calls hold a mark,
+            # so the newest mark of a call <= k' - 2 always covers call
+            # k' - 1 - spare (checked above)
             pass
         elif war:
             # epsilon cannot fall below 1 later (count_env_steps off): no act

@@ -1,6 +1,7 @@
 """Host-side agent logic (no GPU): parameter layout conversion, Keras Adam
 constants, epsilon schedule, config keys."""
 import numpy as np
+import pytest
 import yaml
 
 from conftest import ROOT
@@ -70,7 +71,8 @@ def test_config_keys_match_reference_yaml():
     assert cfg.nn_layers == y["nn_layers"]
 
 
-def test_replay_ring_spare_slot_arithmetic():
+@pytest.mark.parametrize("spare", [1, 2, 3])
+def test_replay_ring_spare_slot_arithmetic(spare):
     """ReplayRing keeps a deque of maxlen cap in cap + 2 slots: deque position
     p -> slot (start + p) % (cap + 2), the next stores go to the slots no
     position maps to, so the stores of steps t+1 and t+2 never touch the
@@ -78,22 +80,23 @@ def test_replay_ring_spare_slot_arithmetic():
     (it waits for learn t, or a later marked one)."""
     from dmdqn_amd.kernels import ReplayRing
     cap = 5
-    S = cap + ReplayRing.SPARE
-    assert ReplayRing.SPARE == 2
-    r = ReplayRing(2, cap, device="cpu")
+    S = cap + spare
+    assert ReplayRing.SPARE == 2  # the default
+    r = ReplayRing(2, cap, device="cpu", spare=spare)
     assert r.slots == S and tuple(r.a.shape) == (2, S)
     windows = []
     for t in range(40):
         window = {int(s) for s in r.slots_of(np.arange(len(r)))}
         assert len(window) == len(r) and r.next_slot not in window
-        # store t: `window` is what learn t-1 reads (stores 0..t-1), windows[-1]
-        # learn t-2's; neither holds its slot (two spare slots), so store t
-        # waits for neither -- learn t-3's window (windows[-2]) holds it once
-        # the ring is full, so store t waits for learn t-3 (or a later one)
-        if windows:
-            assert r.next_slot not in windows[-1]
-        if len(windows) >= 2 and len(windows[-2]) == cap:
-            assert r.next_slot in windows[-2]
+        # store t: `window` is what learn t-1 reads (stores 0..t-1), windows[-b]
+        # learn t-1-b's; with s spare slots none of learns t-1 .. t-s holds
+        # its slot, so store t waits for none of them -- learn t-1-s's window
+        # holds it once the ring is full, so store t waits for that learn
+        for b in range(1, spare):
+            if len(windows) >= b:
+                assert r.next_slot not in windows[-b]
+        if len(windows) >= spare and len(windows[-spare]) == cap:
+            assert r.next_slot in windows[-spare]
         windows.append(window)
         # deque semantics: position 0 is the oldest kept transition
         if t >= cap:

@@ -427,11 +427,11 @@ def test_c2_bench_schedule_steady_state_wrapped_rings():
 
 
 def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), precision="bf16",
-                  shared=False, marks=None):
+                  shared=False, marks=None, spare=2):
     R, C, E = grid
     tr = Trainer(EnvConfig(rows=R, cols=C, num_envs=E, seed=2),
                  AgentConfig(precision=precision, replay_buffer_size=cap, seed=2,
-                             shared_params=shared), **kw)
+                             shared_params=shared, ring_spare=spare), **kw)
     losses, stats, obs = [], [], []
     for t in range(steps):
         st = tr.step(collect_stats=t % stats_every == 0)
@@ -456,30 +456,33 @@ def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), preci
     return out
 
 
-@pytest.mark.parametrize("fenced", [False, True])
-def test_c2_bench_schedule_bit_identical_to_one_stream(fenced):
+@pytest.mark.parametrize("fenced,spare", [(False, 2), (True, 2), (False, 3), (False, 1)])
+def test_c2_bench_schedule_bit_identical_to_one_stream(fenced, spare):
     """C2 size, replay 300 (wrapped by step 300), 420
     steps: the bench's C2 schedule (masked streams, side learn of 64 agents,
     ordering-only learn events; fenced=True: default events, bench
     --fenced-events) gives losses, Q statistics (collect_stats every 7th
     step), observations, weights, Adam slots, target shadows,
-    random streams and rings bit-identical to the one-stream order."""
-    ref = _run_schedule({})
+    random streams and rings bit-identical to the one-stream order -- with
+    the ring's default two spare slots, and with three (the side stream up to
+    three env steps ahead, every third learn marked) and one (round 5's ring,
+    every learn marked)."""
+    ref = _run_schedule({}, spare=spare)
     work, kw = _bench_c2_schedule()
     kw["war_events"] = not fenced
     marks = []
     try:
         with torch.cuda.stream(work):
-            got = _run_schedule(kw, marks=marks)
+            got = _run_schedule(kw, marks=marks, spare=spare)
     finally:
         torch.cuda.synchronize()
-    # two spare ring slots: ordering-only events mark every other learn for
-    # the side stream (the first learn always); default events mark every one
+    # s spare ring slots: ordering-only events mark every s-th learn for the
+    # side stream (the first learn always); default events mark every one
     n_marks, n_learns = marks[0]
-    if fenced:
+    if fenced or spare == 1:
         assert n_marks == n_learns, (n_marks, n_learns)
     else:
-        assert abs(n_marks - n_learns / 2) <= 1.5, (n_marks, n_learns)
+        assert abs(n_marks - n_learns / spare) <= 1.5, (n_marks, n_learns)
     assert ref.keys() == got.keys()
     for k in ref:
         assert torch.equal(ref[k], got[k]), k
