@@ -382,7 +382,7 @@ def main():
     ap.add_argument("--fenced-events", action="store_true",
                     help="overlap env: order the side stream after the learns with default "
                          "(system-scope) events instead of ordering-only ones (A/B)")
-    ap.add_argument("--ring-spare", type=int, default=2,
+    ap.add_argument("--ring-spare", type=int, default=64,
                     help="replay-ring slots beyond replay_buffer_size (AgentConfig.ring_spare): "
                          "under overlap env the side stream runs up to this many env steps ahead "
                          "and the learn stream marks every this-many-th learn")

@@ -243,7 +243,7 @@ class AgentConfig:
     # physical ring slots beyond replay_buffer_size (kernels.ReplayRing): with
     # s spare slots the trainer's "env" schedule lets its side stream run up to
     # s env steps ahead of the learn, which marks every s-th learn for it
-    ring_spare: int = 2
+    ring_spare: int = 64
 
     @classmethod
     def from_dict(cls, d):

@@ -100,7 +100,11 @@ class ReplayRing:
     per-agent drop-in surface): float32 rows of ROW_FLOATS, every value kept
     as the reference's buffer keeps it (dqn_agent.py:39-56)."""
 
-    SPARE = 2  # default physical slots beyond the deque's maxlen (round 6; 1 before)
+    # default physical slots beyond the deque's maxlen (round 5: 1; round 6: 64
+    # -- the env schedule's side stream then runs up to 64 env steps ahead and
+    # the learn stream marks every 64th learn: C3 +2.3 %, C2 +1.8 % over 2
+    # slots, same box, profiles/r06/ring_spare)
+    SPARE = 64
 
     def __init__(self, NA, cap, device="cuda", row_format="int8", spare=None):
         if row_format not in ("int8", "f32"):

@@ -168,6 +168,13 @@ def _check_learn(tr, agents, pre, precision, shared, t32=None, stats=False):
         assert np.isfinite(p_now).all() and not np.array_equal(p_now, pre[0][0])
 
 
+# steps past the deque's maxlen in the steady-state tests: beyond the ring's
+# 64 spare slots (kernels.ReplayRing.SPARE), so the PHYSICAL ring wraps too
+# (the learns' slot arithmetic takes its wrap branch) -- as in bench.py's timed
+# region (10,000 prefill + 210 steps)
+PAST = 70
+
+
 def _run_config(rows, cols, envs, precision, steps, learn_checks, shared=False, sparse_until=0,
                 t32=None, shared_grad_checks=(), trainer_kw=None, stats_checks=()):
     """sparse_until: before this step, compare with the oracle only every 97th
@@ -234,7 +241,7 @@ def test_c3_steady_state_wrapped_rings():
     dqn_agent.py:29, 59-85) and the sampler runs CPython's set branch at
     n = 10,000.  Sampled replicas {0, 511, 1023} vs OracleLoop every 97th step
     and at every step after the wrap: actions, rewards, observations and replay
-    indices bit-exact; at learns 3 and 5 steps after the wrap, for 8 agents,
+    indices bit-exact; at the learns of steps PAST - 3 and PAST - 1 after the wrap, for 8 agents,
     the device z-score bit-exact and the loss vs the Keras mixed-precision
     checker (pinned to the reference's own learn; rtol 2e-3, as at step 128)
     and, as a sanity bound, the fp32 oracle "q-scaled" (_check_learn).  Under
@@ -244,11 +251,12 @@ def test_c3_steady_state_wrapped_rings():
     work, kw = _bench_c3_schedule()
     try:
         with torch.cuda.stream(work):
-            tr = _run_config(4, 4, 1024, "fp16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap,
+            tr = _run_config(4, 4, 1024, "fp16", cap + PAST, {cap + PAST - 3, cap + PAST - 1},
+                             sparse_until=cap,
                              trainer_kw=kw)
             assert tr.overlap == "env" and tr.side_learn == 0
             ring = tr.agent.ring
-            assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
+            assert len(ring) == cap and ring.total == cap + PAST and ring.start == PAST
             del tr
     finally:
         torch.cuda.synchronize()
@@ -272,13 +280,14 @@ def test_c2_steady_state_wrapped_rings():
     wrapped (start != 0) on int8 rows, the sampler in CPython's set branch at
     n = 10,000.  Sampled replicas {0, 128, 255} vs OracleLoop every 97th step
     and at every step after the wrap (actions, rewards, observations, replay
-    indices bit-exact); at learns 3 and 5 steps after the wrap the device
+    indices bit-exact); at the learns of steps PAST - 3 and PAST - 1 after the wrap the device
     z-score bit-exact and the loss vs oracle.learn_mixed (bf16, TOL16) for 8
     agents (dqn_agent.py:29, 59-85)."""
     cap = 10000
-    tr = _run_config(2, 2, 256, "bf16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap)
+    tr = _run_config(2, 2, 256, "bf16", cap + PAST, {cap + PAST - 3, cap + PAST - 1},
+                     sparse_until=cap)
     ring = tr.agent.ring
-    assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
+    assert len(ring) == cap and ring.total == cap + PAST and ring.start == PAST
     del tr
     torch.cuda.empty_cache()
 
@@ -287,17 +296,17 @@ def test_c5_steady_state_wrapped_rings():
     """C5 (8x8 x 256, ONE shared fp16 network, replay 10,000), the regime
     bench.py's C5 line times: past 10,000 steps, wrapped rings (start != 0,
     the wrap arithmetic of k_shared_next / k_shared_grad4) and the set-branch
-    sampler.  Sampled replicas vs OracleLoop as C2 / C3; at learns 3 and 5
-    after the wrap the device z-score bit-exact and 8 agents' losses vs
+    sampler.  Sampled replicas vs OracleLoop as C2 / C3; at the learns of
+    steps PAST - 3 and PAST - 1 after the wrap the device z-score bit-exact and 8 agents' losses vs
     oracle.learn_mixed; at both, Adam exact on the all-agent gradient and the
     gradient of the middle replica's 64 agents vs the mean of their
     oracle.learn_mixed gradients (_check_shared_grad)."""
     cap = 10000
-    checks = {cap + 3, cap + 5}
-    tr = _run_config(8, 8, 256, "fp16", cap + 6, checks, shared=True, sparse_until=cap,
+    checks = {cap + PAST - 3, cap + PAST - 1}
+    tr = _run_config(8, 8, 256, "fp16", cap + PAST, checks, shared=True, sparse_until=cap,
                      shared_grad_checks=checks)
     ring = tr.agent.ring
-    assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
+    assert len(ring) == cap and ring.total == cap + PAST and ring.start == PAST
     del tr
     torch.cuda.empty_cache()
 
@@ -406,7 +415,7 @@ def test_c2_bench_schedule_steady_state_wrapped_rings():
     steps (wrapped rings, the store in the spare slot, the set-branch
     sampler).  Sampled replicas {0, 128, 255} vs OracleLoop every 97th step
     and at every step after the wrap: actions, observations, rewards, replay
-    indices bit-exact.  At learns 3 and 5 after the wrap, agents of both
+    indices bit-exact.  At the learns of steps PAST - 3 and PAST - 1 after the wrap, agents of both
     launches (0, 3, 513, 515 on the learn stream; 1020..1023 on the side
     stream) are checked: device z-score bit-exact, loss vs
     oracle.learn_mixed (bf16, TOL16), gradient, and (learn 5) the Q
@@ -415,11 +424,12 @@ def test_c2_bench_schedule_steady_state_wrapped_rings():
     work, kw = _bench_c2_schedule()
     try:
         with torch.cuda.stream(work):
-            tr = _run_config(2, 2, 256, "bf16", cap + 6, {cap + 3, cap + 5}, sparse_until=cap,
-                             trainer_kw=kw, stats_checks={cap + 5})
+            tr = _run_config(2, 2, 256, "bf16", cap + PAST, {cap + PAST - 3, cap + PAST - 1},
+                             sparse_until=cap,
+                             trainer_kw=kw, stats_checks={cap + PAST - 1})
             assert tr.side_learn == 64 and tr.overlap == "env"
             ring = tr.agent.ring
-            assert len(ring) == cap and ring.total == cap + 6 and ring.start == 6
+            assert len(ring) == cap and ring.total == cap + PAST and ring.start == PAST
             del tr
     finally:
         torch.cuda.synchronize()
@@ -427,7 +437,7 @@ def test_c2_bench_schedule_steady_state_wrapped_rings():
 
 
 def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), precision="bf16",
-                  shared=False, marks=None, spare=2):
+                  shared=False, marks=None, spare=64):
     R, C, E = grid
     tr = Trainer(EnvConfig(rows=R, cols=C, num_envs=E, seed=2),
                  AgentConfig(precision=precision, replay_buffer_size=cap, seed=2,
@@ -456,7 +466,8 @@ def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), preci
     return out
 
 
-@pytest.mark.parametrize("fenced,spare", [(False, 2), (True, 2), (False, 3), (False, 1)])
+@pytest.mark.parametrize("fenced,spare", [(False, 64), (True, 64), (False, 2), (False, 3),
+                                          (False, 1)])
 def test_c2_bench_schedule_bit_identical_to_one_stream(fenced, spare):
     """C2 size, replay 300 (wrapped by step 300), 420
     steps: the bench's C2 schedule (masked streams, side learn of 64 agents,
@@ -464,9 +475,9 @@ def test_c2_bench_schedule_bit_identical_to_one_stream(fenced, spare):
     --fenced-events) gives losses, Q statistics (collect_stats every 7th
     step), observations, weights, Adam slots, target shadows,
     random streams and rings bit-identical to the one-stream order -- with
-    the ring's default two spare slots, and with three (the side stream up to
-    three env steps ahead, every third learn marked) and one (round 5's ring,
-    every learn marked)."""
+    the ring's default 64 spare slots (the side stream up to 64 env steps
+    ahead, every 64th learn marked), with two and three, and with one (round
+    5's ring, every learn marked)."""
     ref = _run_schedule({}, spare=spare)
     work, kw = _bench_c2_schedule()
     kw["war_events"] = not fenced
@@ -510,7 +521,8 @@ def test_c3_bench_schedule_bit_identical_to_one_stream():
     """The C3 schedule of bench.py (4x4 x 1024, fp16; the env step of t+1 and
     its draws beside learn t, ring stores in the two spare slots) vs the
     one-stream order in the sampler's set branch with the rings
-    wrapped: replay 1,100 (n >= 1,046 from step 1,046 on), 1,160 steps.
+    wrapped: replay 1,100 (n >= 1,046 from step 1,046 on), 1,200 steps (past the
+    ring's 1,164 physical slots).
     Losses of every learn, Q statistics (collect_stats every 50th step), the
     last observations, weights, Adam slots, target shadows, random streams and
     rings bit-identical (compared on the device)."""
@@ -518,7 +530,7 @@ def test_c3_bench_schedule_bit_identical_to_one_stream():
         tr = Trainer(EnvConfig(rows=4, cols=4, num_envs=1024, seed=2),
                      AgentConfig(precision="fp16", replay_buffer_size=1100, seed=2), **kw)
         losses, stats = [], []
-        for t in range(1160):
+        for t in range(1200):
             tr.step(collect_stats=t % 50 == 0)
             if tr.last_loss is not None:
                 losses.append(tr.last_loss.clone())
@@ -526,7 +538,7 @@ def test_c3_bench_schedule_bit_identical_to_one_stream():
                     stats.append(tr.agent.qstats.clone())
         torch.cuda.synchronize()
         ag = tr.agent
-        assert len(ag.ring) == 1100 and ag.ring.start == 60
+        assert len(ag.ring) == 1100 and ag.ring.start == 100 and ag.ring.total > ag.ring.slots
         out = dict(losses=torch.stack(losses), stats=torch.stack(stats), obs=tr.obs.clone(),
                    **{k: getattr(ag, k).clone() for k in ("params", "target", "adam_m", "adam_v",
                                                           "target_h", "np_state", "py_state")},

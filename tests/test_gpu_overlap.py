@@ -14,11 +14,12 @@ from dmdqn_amd.env import EnvConfig  # noqa: E402
 from dmdqn_amd.trainer import Trainer  # noqa: E402
 
 
-def _trainer(overlap, precision, shared, greedy, side_stream=None, cap=200, side_learn=0):
+def _trainer(overlap, precision, shared, greedy, side_stream=None, cap=200, side_learn=0,
+             spare=64):
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=8, seed=11, max_sim_time=500),
                  AgentConfig(replay_buffer_size=cap, target_update_frequency=9, seed=4,
                              precision=precision, shared_params=shared,
-                             count_env_steps=greedy),
+                             count_env_steps=greedy, ring_spare=spare),
                  overlap=overlap, side_stream=side_stream, side_learn=side_learn)
     if greedy:  # past the 8000-step epsilon floor (dqn_agent.py:258-261)
         tr.agent.global_step_count = 12000
@@ -85,24 +86,25 @@ def test_overlap_on_cu_masked_streams_matches_sequential():
     _compare(ref, ovl, a, b)
 
 
-@pytest.mark.parametrize("masked", [False, True])
-def test_env_beside_learn_on_a_wrapped_ring(masked):
-    """overlap "env": the fused env step of t+1 beside learn t, with the ring
-    wrapped (replay 150 < 170 steps, learns from step 128), so every store lands in the spare slot
-    the running learn cannot sample (kernels.ReplayRing) -- bit-identical to
-    the one-stream order, also with the two streams CU-masked (bench
-    --cu-split)."""
+@pytest.mark.parametrize("masked,spare", [(False, 2), (True, 2), (False, 64), (True, 64)])
+def test_env_beside_learn_on_a_wrapped_ring(masked, spare):
+    """overlap "env": the fused env step of t+1 beside learn t (the side
+    stream up to `spare` steps ahead), with the deque wrapped (replay 150 <
+    170 steps, learns from step 128) and, with 2 spare slots, the physical
+    ring too, so every store lands in a spare slot the running learns cannot
+    sample (kernels.ReplayRing) -- bit-identical to the one-stream order, also
+    with the two streams CU-masked (bench --cu-split)."""
     from dmdqn_amd._lib import cu_masked_stream
-    ref = _trainer("none", "bf16", False, False, cap=150)
+    ref = _trainer("none", "bf16", False, False, cap=150, spare=spare)
     a = _run(ref, 170)
     if masked:
         n_cu = torch.cuda.get_device_properties(0).multi_processor_count
         main, side = cu_masked_stream(range(64, n_cu)), cu_masked_stream(range(64))
         with torch.cuda.stream(main):
-            ovl = _trainer("env", "bf16", False, False, side_stream=side, cap=150)
+            ovl = _trainer("env", "bf16", False, False, side_stream=side, cap=150, spare=spare)
             b = _run(ovl, 170)
     else:
-        ovl = _trainer("env", "bf16", False, False, cap=150)
+        ovl = _trainer("env", "bf16", False, False, cap=150, spare=spare)
         b = _run(ovl, 170)
     assert ovl.agent.ring.start != 0 and ovl.agent.learn_launches == 170 - 127
     _compare(ref, ovl, a, b)
