@@ -38,9 +38,9 @@ tr = Trainer(EnvConfig(num_envs=4, scenario=sc), AgentConfig(precision="fp16"))
 for _ in range(240):
     tr.step()
 print("CLEAN")
-# negative control: positions >= cap
+# negative control: positions >= the ring's physical slot count
 ag = tr.agent
-ag.idx.fill_(ag.ring.cap + 3)
+ag.idx.fill_(ag.ring.slots + 3)  # past the physical slots
 torch.ops.dmdqn.learn_step(ag.ring.s, ag.ring.n, ag.ring.a, ag.ring.d, ag.ring.r, ag.idx,
                            ag.params, ag.adam_m, ag.adam_v, ag.target, ag.target_h, ag.loss,
                            ag.ring.start, 128, 1, False, 0.99, 1e-3, 0.1, 1e-3, 1e-7, 0,
