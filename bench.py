@@ -382,7 +382,7 @@ def main():
     ap.add_argument("--fenced-events", action="store_true",
                     help="overlap env: order the side stream after the learns with default "
                          "(system-scope) events instead of ordering-only ones (A/B)")
-    ap.add_argument("--ring-spare", type=int, default=64,
+    ap.add_argument("--ring-spare", type=int, default=16,
                     help="replay-ring slots beyond replay_buffer_size (AgentConfig.ring_spare): "
                          "under overlap env the side stream runs up to this many env steps ahead "
                          "and the learn stream marks every this-many-th learn")
@@ -533,6 +533,7 @@ def main():
     vsum = torch.zeros(E, dtype=torch.int64, device=dev)
     for _ in range(SIM_PROBE_STEPS):
         tr.step()
+        tr.quiesce()  # env state is the side stream's (it may run ahead under "env")
         vsum.add_(env.t_stats[:, 2])
     vbar = float(vsum.double().mean().item()) / SIM_PROBE_STEPS
     torch.cuda.synchronize(dev)

@@ -243,7 +243,7 @@ class AgentConfig:
     # physical ring slots beyond replay_buffer_size (kernels.ReplayRing): with
     # s spare slots the trainer's "env" schedule lets its side stream run up to
     # s env steps ahead of the learn, which marks every s-th learn for it
-    ring_spare: int = 64
+    ring_spare: int = 16
 
     @classmethod
     def from_dict(cls, d):
@@ -254,7 +254,12 @@ class AgentConfig:
 class BatchedDQN:
     """E*A independent DQN agents (agent index = env * A + junction)."""
 
-    OUT_BUFS = 3  # rotating per-step output buffers: loss, qstats, actions, idx (see __init__)
+    # rotating per-step output buffers (loss, qstats, actions, idx; see
+    # __init__): at least 3, and ring_spare + 2 -- under trainer overlap "env"
+    # the side stream runs up to ring_spare steps ahead of the learn stream, so
+    # it writes the buffers of step t + ring_spare + 1 while the learn of step
+    # t and then the caller's reads of step t's outputs may still be queued
+    OUT_BUFS = 3
 
     def __init__(self, num_envs, n_agents, cfg: AgentConfig = None, device="cuda",
                  env_seeds=None, init_weights=None, streams=None):
@@ -318,6 +323,7 @@ class BatchedDQN:
             raise ValueError("the shared-network learn reads int8 replay rows only")
         self.ring = K.ReplayRing(NA, cfg.replay_buffer_size, device=dev, row_format=cfg.replay_rows,
                                  spare=cfg.ring_spare)
+        self.OUT_BUFS = max(BatchedDQN.OUT_BUFS, self.ring.spare + 2)
         self._xs = self._xn = None  # float rows: the learn's pre-gathered batch
         if streams is not None:
             # shared (np_state, py_state) device streams, e.g. the process-global

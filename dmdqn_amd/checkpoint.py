@@ -26,7 +26,7 @@ import os
 import numpy as np
 import torch
 
-# 8: replay rings of cap + ring_spare slots (kernels.ReplayRing, default 64); 7: cap + 1 slots,
+# 8: replay rings of cap + ring_spare slots (kernels.ReplayRing, default 16); 7: cap + 1 slots,
 # the written slots saved;
 # 6: + per-replica clocks and episode counters; 5: + the actuated-mode detector
 # times; 4: 128-B replay rows, unpadded W1T

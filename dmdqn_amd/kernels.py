@@ -100,11 +100,12 @@ class ReplayRing:
     per-agent drop-in surface): float32 rows of ROW_FLOATS, every value kept
     as the reference's buffer keeps it (dqn_agent.py:39-56)."""
 
-    # default physical slots beyond the deque's maxlen (round 5: 1; round 6: 64
-    # -- the env schedule's side stream then runs up to 64 env steps ahead and
-    # the learn stream marks every 64th learn: C3 +2.3 %, C2 +1.8 % over 2
-    # slots, same box, profiles/r06/ring_spare)
-    SPARE = 64
+    # default physical slots beyond the deque's maxlen (round 5: 1; round 6: 16
+    # -- the env schedule's side stream then runs up to 16 env steps ahead and
+    # the learn stream marks every 16th learn: C3 +1.9 %, C2 +1.8 % over 2
+    # slots, same box, profiles/r06/ring_spare; the agent's output buffers
+    # rotate over ring_spare + 2, BatchedDQN.OUT_BUFS)
+    SPARE = 16
 
     def __init__(self, NA, cap, device="cuda", row_format="int8", spare=None):
         if row_format not in ("int8", "f32"):

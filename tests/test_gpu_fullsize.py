@@ -169,7 +169,7 @@ def _check_learn(tr, agents, pre, precision, shared, t32=None, stats=False):
 
 
 # steps past the deque's maxlen in the steady-state tests: beyond the ring's
-# 64 spare slots (kernels.ReplayRing.SPARE), so the PHYSICAL ring wraps too
+# spare slots (kernels.ReplayRing.SPARE, 16), so the PHYSICAL ring wraps too
 # (the learns' slot arithmetic takes its wrap branch) -- as in bench.py's timed
 # region (10,000 prefill + 210 steps)
 PAST = 70
@@ -437,7 +437,7 @@ def test_c2_bench_schedule_steady_state_wrapped_rings():
 
 
 def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), precision="bf16",
-                  shared=False, marks=None, spare=64):
+                  shared=False, marks=None, spare=16):
     R, C, E = grid
     tr = Trainer(EnvConfig(rows=R, cols=C, num_envs=E, seed=2),
                  AgentConfig(precision=precision, replay_buffer_size=cap, seed=2,
@@ -466,7 +466,7 @@ def _run_schedule(kw, steps=420, cap=300, stats_every=7, grid=(2, 2, 256), preci
     return out
 
 
-@pytest.mark.parametrize("fenced,spare", [(False, 64), (True, 64), (False, 2), (False, 3),
+@pytest.mark.parametrize("fenced,spare", [(False, 16), (True, 16), (False, 64), (False, 2),
                                           (False, 1)])
 def test_c2_bench_schedule_bit_identical_to_one_stream(fenced, spare):
     """C2 size, replay 300 (wrapped by step 300), 420
@@ -475,8 +475,8 @@ def test_c2_bench_schedule_bit_identical_to_one_stream(fenced, spare):
     --fenced-events) gives losses, Q statistics (collect_stats every 7th
     step), observations, weights, Adam slots, target shadows,
     random streams and rings bit-identical to the one-stream order -- with
-    the ring's default 64 spare slots (the side stream up to 64 env steps
-    ahead, every 64th learn marked), with two and three, and with one (round
+    the ring's default 16 spare slots (the side stream up to 16 env steps
+    ahead, every 16th learn marked), with 64 and two, and with one (round
     5's ring, every learn marked)."""
     ref = _run_schedule({}, spare=spare)
     work, kw = _bench_c2_schedule()

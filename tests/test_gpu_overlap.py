@@ -15,7 +15,7 @@ from dmdqn_amd.trainer import Trainer  # noqa: E402
 
 
 def _trainer(overlap, precision, shared, greedy, side_stream=None, cap=200, side_learn=0,
-             spare=64):
+             spare=16):
     tr = Trainer(EnvConfig(rows=2, cols=2, num_envs=8, seed=11, max_sim_time=500),
                  AgentConfig(replay_buffer_size=cap, target_update_frequency=9, seed=4,
                              precision=precision, shared_params=shared,
@@ -86,7 +86,7 @@ def test_overlap_on_cu_masked_streams_matches_sequential():
     _compare(ref, ovl, a, b)
 
 
-@pytest.mark.parametrize("masked,spare", [(False, 2), (True, 2), (False, 64), (True, 64)])
+@pytest.mark.parametrize("masked,spare", [(False, 2), (True, 2), (False, 16), (True, 16)])
 def test_env_beside_learn_on_a_wrapped_ring(masked, spare):
     """overlap "env": the fused env step of t+1 beside learn t (the side
     stream up to `spare` steps ahead), with the deque wrapped (replay 150 <
