@@ -444,38 +444,6 @@ __device__ __forceinline__ void adam_el(float &w, float &m, float &v, float g, f
     w = w - (m * alpha) / (sqrtf(v) + eps);
 }
 
-// Adam's m / v (read once and written once per learn) and the w stores with
-// the non-temporal hint (global_load / global_store ... nt): DMDQN_ADAM_NT
-// 1 = m, v loads and stores; 2 = also the w stores; 0 = plain (A/B switch).
-#ifndef DMDQN_ADAM_NT
-#define DMDQN_ADAM_NT 0
-#endif
-typedef float nt_f4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld_mv(const float *p) {
-#if DMDQN_ADAM_NT >= 1
-    const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4 *>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *reinterpret_cast<const float4 *>(p);
-#endif
-}
-__device__ __forceinline__ void st_mv(float *p, float4 x) {
-#if DMDQN_ADAM_NT >= 1
-    const nt_f4 v = {x.x, x.y, x.z, x.w};
-    __builtin_nontemporal_store(v, reinterpret_cast<nt_f4 *>(p));
-#else
-    *reinterpret_cast<float4 *>(p) = x;
-#endif
-}
-__device__ __forceinline__ void st_w(float *p, float4 x) {
-#if DMDQN_ADAM_NT >= 2
-    const nt_f4 v = {x.x, x.y, x.z, x.w};
-    __builtin_nontemporal_store(v, reinterpret_cast<nt_f4 *>(p));
-#else
-    *reinterpret_cast<float4 *>(p) = x;
-#endif
-}
-
 struct AdamC {
     float alpha, c1, c2, eps;
     bool sync;
@@ -501,8 +469,8 @@ __device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, c
 #pragma unroll
     for (int q = 0; q < NT; q++) {
         w[q] = *reinterpret_cast<const float4 *>(W + idx[q]);
-        m[q] = ld_mv(M + idx[q]);
-        v[q] = ld_mv(V + idx[q]);
+        m[q] = *reinterpret_cast<const float4 *>(M + idx[q]);
+        v[q] = *reinterpret_cast<const float4 *>(V + idx[q]);
     }
     // keep all 3*NT loads in flight together: under VGPR pressure the
     // scheduler would otherwise sink each load to its use (one round trip each)
@@ -516,9 +484,9 @@ __device__ __forceinline__ void adam4n(float *W, float *M, float *V, float *T, c
     }
 #pragma unroll
     for (int q = 0; q < NT; q++) {
-        st_w(W + idx[q], w[q]);
-        st_mv(M + idx[q], m[q]);
-        st_mv(V + idx[q], v[q]);
+        *reinterpret_cast<float4 *>(W + idx[q]) = w[q];
+        *reinterpret_cast<float4 *>(M + idx[q]) = m[q];
+        *reinterpret_cast<float4 *>(V + idx[q]) = v[q];
         if (k.sync) {
             *reinterpret_cast<float4 *>(T + idx[q]) = w[q];
             if (k.TH) {
@@ -585,8 +553,8 @@ __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T
         w[0][q] = m[0][q] = v[0][q] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (valid(q)) {
             w[0][q] = *reinterpret_cast<const float4 *>(W + i);
-            m[0][q] = ld_mv(M + i);
-            v[0][q] = ld_mv(V + i);
+            m[0][q] = *reinterpret_cast<const float4 *>(M + i);
+            v[0][q] = *reinterpret_cast<const float4 *>(V + i);
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -604,8 +572,8 @@ __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T
                 w[n][q] = m[n][q] = v[n][q] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (valid((h + 1) * NT + q)) {
                     w[n][q] = *reinterpret_cast<const float4 *>(W + i);
-                    m[n][q] = ld_mv(M + i);
-                    v[n][q] = ld_mv(V + i);
+                    m[n][q] = *reinterpret_cast<const float4 *>(M + i);
+                    v[n][q] = *reinterpret_cast<const float4 *>(V + i);
                 }
             }
         }
@@ -622,9 +590,9 @@ __device__ __forceinline__ void adam_pipe(float *W, float *M, float *V, float *T
         for (int q = 0; q < NT; q++) {
             const size_t i = ix(h * NT + q);
             if (!valid(h * NT + q)) continue;
-            st_w(W + i, w[c][q]);
-            st_mv(M + i, m[c][q]);
-            st_mv(V + i, v[c][q]);
+            *reinterpret_cast<float4 *>(W + i) = w[c][q];
+            *reinterpret_cast<float4 *>(M + i) = m[c][q];
+            *reinterpret_cast<float4 *>(V + i) = v[c][q];
             if (k.sync) {
                 *reinterpret_cast<float4 *>(T + i) = w[c][q];
                 if (k.TH) {
