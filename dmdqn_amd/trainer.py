@@ -35,14 +35,16 @@ sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
 
   "env"     the fused env step of step t+1 (act, sim, observe, remember) and
             the replay draws of learn t+1 run on a side stream beside learn t.
-            The ring has two spare slots (kernels.ReplayRing: cap + 2 slots
-            for a deque of maxlen cap), and the stores of steps t+1 and t+2 go
-            to slots learn t cannot sample; the store of step t+3 waits for
-            learn t (its slot is in learn t's window), or a later marked learn
-            (at fixed epsilon 1 the learn stream marks every other learn with
-            an ordering-only event).  A greedy act (epsilon < 1) waits for
-            learn t's weights.
-              side:  [wait learn t-2 or t-1] env_step_{t+1} sample_{t+1} (ev_env)
+            The ring has s = AgentConfig.ring_spare spare slots (16;
+            kernels.ReplayRing: cap + s slots for a deque of maxlen cap), and
+            the stores of steps t+1 .. t+s go to slots learn t cannot sample;
+            the store of step t+s+1 waits for learn t (its slot is in learn t's
+            window) or a later marked learn -- at fixed epsilon 1 the learn
+            stream marks every s-th learn with an ordering-only event, and the
+            side stream runs up to s steps ahead (the agent's per-step output
+            buffers rotate over s + 2 copies for it).  A greedy act (epsilon <
+            1) waits for learn t's weights.
+              side:  [wait the newest marked learn <= t-1] env_step_{t+1} sample_{t+1} (ev_env)
               main:  [wait ev_env of t] learn_t
             With a CU-masked side stream (bench --cu-split) the two split the
             chip.  side_learn=m runs the learn of the last m agents on the side
