@@ -1127,6 +1127,70 @@ __host__ __device__ inline size_t reg_vcol_off(int R, int C, bool fused, int ls)
     return (b + 15) & ~(size_t)15;
 }
 
+// Total LDS of the register path (what the launcher passes) and, in
+// *perm_off, where the lane order lives: the block's own arrays (and the fused
+// step's), the speed columns of a 1024-thread block, then the lane order
+// (u16 per thread) and its 32 bin counters.
+__host__ __device__ inline size_t reg_lds_total(int R, int C, bool fused, int ls, int nt,
+                                                size_t *perm_off) {
+    const int A = R * C;
+    size_t b = sim_reg_lds_bytes(R, C, ls);
+    if (fused) b = fuse_layout(b, 0, (size_t)ls * 9 * 4, A).bytes;
+    if (nt > 512) b = reg_vcol_off(R, C, fused, ls) + (size_t)RCAP * nt * 4;
+    const size_t p = (b + 15) & ~(size_t)15;
+    if (perm_off) *perm_off = p;
+    return p + (size_t)nt * 2 + 32 * 4;
+}
+
+// Which lane each thread owns for this launch: the lanes in DESCENDING order
+// of their vehicle counts at the launch's start (s_lane[tid] = lane).  Every
+// pass that walks a lane's vehicles runs to the longest lane of the wave
+// (wave-uniform loops over register arrays); with lanes in launch order the
+// 16 waves' longest lanes summed to ~5.7x the vehicles / 64 of an 8x8 replica
+// (oracle, steady state), sorted ~2.7x.  Per-lane results do not depend on
+// which thread computes them (lanes meet only through lane-indexed LDS
+// arrays and integer counters), so the order changes no bit.  Counting sort:
+// one ballot per wave and count (RCAP + 1 keys), one LDS atomic per wave and
+// key, ranks from the ballot's lane prefix.
+template <int NT>
+__device__ void lane_order(const int32_t *cnt, int NL, uint16_t *s_lane, int32_t *s_bin) {
+    const int tid = threadIdx.x, ln = tid & 63;
+    if (tid < 32) s_bin[tid] = 0;
+    __syncthreads();
+    int key = 31;  // threads without a lane take no rank
+    if (tid < NL) {
+        const int c = cnt[tid];
+        key = RCAP - (c < 0 ? 0 : c > RCAP ? RCAP : c);
+    }
+    for (int b = 0; b <= RCAP; b++) {
+        const uint64_t m = __ballot(key == b);
+        if (m && ln == 0) atomicAdd(&s_bin[b], (int)__popcll(m));
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int b = 0; b <= RCAP; b++) {
+            const int c = s_bin[b];
+            s_bin[b] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (int b = 0; b <= RCAP; b++) {
+        const uint64_t m = __ballot(key == b);
+        if (m) {  // wave-uniform
+            const int first = __ffsll((unsigned long long)m) - 1;
+            int base = 0;
+            if (ln == first) base = atomicAdd(&s_bin[b], (int)__popcll(m));
+            base = __shfl(base, first);
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (key == b) s_lane[base + below] = (uint16_t)tid;
+        }
+    }
+    __syncthreads();
+}
+
 template <int NT, bool kFuse>
 __global__ void __launch_bounds__(NT, NT <= 256 ? 2 : 1)
 k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, int t0_arg, int K,
@@ -1156,8 +1220,13 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                               P.len_outer);  // synced below
 
     // ---- this thread's lane (registers) and origin queue
+    // the lanes by descending vehicle count (lane_order): s_lane[tid] = lane
+    size_t perm_off = 0;
+    (void)reg_lds_total(S.R, S.C, kFuse, LS, NT, &perm_off);
+    uint16_t *const s_lane = reinterpret_cast<uint16_t *>(dyn + perm_off);
+    lane_order<NT>(G.cnt, NL, s_lane, reinterpret_cast<int32_t *>(dyn + perm_off + (size_t)NT * 2));
     const bool own = tid < NL;
-    const int l = tid;  // (e = l / 3 and kf = l % 3 are derived inside the substep loop)
+    const int l = own ? (int)s_lane[tid] : tid;  // (e = l / 3, kf = l % 3: inside the substep loop)
     constexpr bool kL = NT > 512;  // speeds in the LDS column (VColL)
     float X_[RCAP], V_[RCAP];
     VColL Vc{nullptr, 0, NT};
@@ -1284,7 +1353,8 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         // the lane ids again from an opaque thread id: expressions of them are
         // then computed in the loop instead of hoisted above it and held --
         // the 1024-thread fused kernel spilled 16 such invariants to scratch
-        const int l = opaque_tid(), e = l / 3, kf = l - 3 * (l / 3);
+        const int tq = opaque_tid();
+        const int l = tq < NL ? (int)s_lane[tq] : tq, e = l / 3, kf = l - 3 * (l / 3);
         const float len = LANE_LEN();
         TAKE_INSERT();
         // ---- A: the front vehicle decides (route, target lane, IDM, request)
@@ -1643,9 +1713,7 @@ static int launch_sim(const dmdqn_sim *sim, const dmdqn_idm *idm, const int32_t 
     if (use_reg) {
         const int nt = NL <= 256 ? 256 : NL <= 512 ? 512 : 1024;
         const int ls = SIM_LANE_STRIDE_NT ? nt : NL;  // the kernel's lane-array stride
-        size_t rlds = sim_reg_lds_bytes(sim->R, sim->C, ls);
-        if (F) rlds = fuse_layout(rlds, 0, (size_t)ls * 9 * 4, A).bytes;
-        if (nt > 512) rlds = reg_vcol_off(sim->R, sim->C, F != nullptr, ls) + (size_t)RCAP * nt * 4;
+        const size_t rlds = reg_lds_total(sim->R, sim->C, F != nullptr, ls, nt, nullptr);
         DMDQN_REQUIRE(rlds <= 160 * 1024, "dmdqn_sim_step: register path needs %zu bytes of LDS", rlds);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(sim->E), dim3(nt), rlds, as_stream(stream), *sim, *idm,
