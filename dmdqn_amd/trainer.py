@@ -157,8 +157,7 @@ class Trainer:
         # learn: profiles/r06/c3_marks, c2_marks).
         self._marks = []
         self._calls = 0
-        self._first_learn = None  # the call of the first learn (always marked)
-        self.n_marks = 0  # learns marked for the side stream (tests: every other one)
+        self.n_marks = 0  # marked calls that learned (tests: every spare-th learn)
         self._mark_every = bool(mark_every_learn)  # A/B: a marker behind every learn
         self.obs = self.env.reset()
         self.episode = 0
@@ -298,12 +297,15 @@ class Trainer:
         self._calls += 1
         spare = agent.ring.slots - agent.ring.cap
         marks = [m for m in self._marks if m[0] <= k - 2]
+        if k - 1 - spare >= 0 and not (marks and marks[-1][0] >= k - 1 - spare):
+            # (every call k' has a mark in [k' - 1 - spare, k' - 2]: see below)
+            raise RuntimeError(f"env schedule: no mark covers call {k - 1 - spare}")
         if marks:
             j, ev = marks[-1]
-            # every learn of a call <= k - 1 - spare must be covered (the main
-            # stream is in order: waiting for learn j covers every earlier one)
-            if j < k - 1 - spare and self._learned_at(k - 1 - spare, j):
-                raise RuntimeError(f"env schedule: no marked learn covers call {k - 1 - spare}")
+            # call k - 1 - spare must be covered -- its learn's ring reads and
+            # the caller's reads of its outputs, queued on main before the mark
+            # of any later call (the main stream is in order: the wait covers
+            # every earlier call too)
             if isinstance(ev, _lib.OrderEvent):
                 ev.wait(side)
             else:
@@ -337,12 +339,12 @@ class Trainer:
             loss = agent.learn_range(0, agent.NA - self.side_learn)
         war = (self._war_ring is not None and not agent.cfg.count_env_steps
                and agent.current_epsilon() >= 1.0)
-        if (learned and war and spare >= 2 and not self._mark_every
-                and self._first_learn is not None
-                and (k - self._first_learn) % spare):
-            # under ordering-only events only every spare-th learn is marked
-            # (from the first on): any `spare` consecutive calls hold a mark,
-            # so the newest mark of a call <= k' - 2 always covers call
+        if war and spare >= 2 and not self._mark_every and k % spare:
+            # under ordering-only events only every spare-th call is marked
+            # (whether or not it learned: the mark also orders the side
+            # stream's reuse of the per-step output buffers after the caller's
+            # reads of them): any `spare` consecutive calls hold a mark, so
+            # the newest mark of a call <= k' - 2 always covers call
             # k' - 1 - spare (checked above)
             pass
         elif war:
@@ -359,17 +361,13 @@ class Trainer:
             self._war_i = (self._war_i + 1) % len(self._war_ring)
             ev.record(main)
             self._ev_learn = ev
-            if learned:
-                self._marks.append((k, ev))
-                self.n_marks += 1
+            self._marks.append((k, ev))
+            self.n_marks += learned
         else:
             self._ev_learn = torch.cuda.Event()
             self._ev_learn.record(main)
-            if learned:
-                self._marks.append((k, self._ev_learn))
-                self.n_marks += 1
-        if learned and self._first_learn is None:
-            self._first_learn = k
+            self._marks.append((k, self._ev_learn))
+            self.n_marks += learned
         # the side learn's outputs (its agents' loss, stats and weights) for the
         # caller's stream.  The next learn needs no wait for them: the side
         # stream runs the next env step behind the side learn, and the next
@@ -403,11 +401,6 @@ class Trainer:
         weights read on it are complete.  A no-op otherwise."""
         if getattr(self, "_side_pending", None) is not None:
             torch.cuda.current_stream(self.env.device).wait_event(self._side_pending)
-
-    def _learned_at(self, call, newest_mark):
-        """Whether a learn ran at `call` that the mark of call `newest_mark`
-        does not cover (call > newest_mark and the learn had begun by then)."""
-        return self._first_learn is not None and newest_mark < call and self._first_learn <= call
 
     def _side_reads_nothing_from_main(self):
         """The "env" schedule's invariant for ordering-only learn events: no
