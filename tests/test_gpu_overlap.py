@@ -161,3 +161,28 @@ def test_fence_free_timing_and_ordering_events():
     torch.cuda.synchronize()
     t_sleep, t_after = start.elapsed_time(slept), start.elapsed_time(after)
     assert t_sleep > 0.1 and t_after >= t_sleep - 0.005, (t_after, t_sleep)
+
+
+@pytest.mark.parametrize("spare", [2, 4])
+def test_env_schedule_with_a_lagging_learn_stream(spare):
+    """overlap "env" with the learn stream held back (a GPU sleep queued on it
+    every step): the side stream then runs as far ahead as the schedule allows
+    (`spare` env steps past the newest marked call), before the first learn
+    too, while the caller's clones of each step's actions / observations /
+    rewards / losses are queued on the learn stream.  Every output and the
+    final state stay bit-identical to the one-stream order -- the marks order
+    both the ring slots' reuse and the output buffers' (OUT_BUFS = spare + 2)."""
+    ref = _trainer("none", "fp16", False, False, cap=150, spare=spare)
+    a = _run(ref, 170)
+    ovl = _trainer("env", "fp16", False, False, cap=150, spare=spare)
+    assert ovl.agent.OUT_BUFS == spare + 2
+    main = torch.cuda.current_stream()
+    out = []
+    for _ in range(170):
+        torch.cuda._sleep(200_000)  # ~0.1 ms of GPU time on the learn stream per step
+        st = ovl.step()
+        out.append((None if ovl.last_loss is None else ovl.last_loss.clone(), ovl.obs.clone(),
+                    ovl.last_reward.clone(), ovl.agent.actions.clone(), st.done))
+    assert torch.cuda.current_stream() == main
+    torch.cuda.synchronize()
+    _compare(ref, ovl, a, out)
