@@ -40,7 +40,7 @@ sequential order, so results are bit-identical (tests/test_gpu_overlap.py).
             the stores of steps t+1 .. t+s go to slots learn t cannot sample;
             the store of step t+s+1 waits for learn t (its slot is in learn t's
             window) or a later marked learn -- at fixed epsilon 1 the learn
-            stream marks every s-th learn with an ordering-only event, and the
+            stream marks every s-th call with an ordering-only event, and the
             side stream runs up to s steps ahead (the agent's per-step output
             buffers rotate over s + 2 copies for it).  A greedy act (epsilon <
             1) waits for learn t's weights.
