@@ -1240,20 +1240,41 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         DMDQN_DBG(h >= 0 && h < cap && n >= 0 && n <= RCAP && n <= cap, DBG_SIM_RING);
         const size_t base = (size_t)l * cap;
         const int nm = wave_max_uniform(n);
-        // loop counters are wave-uniform (bounded by the wave's longest lane):
-        // the register arrays are then indexed with a scalar (s_set_gpr_idx)
-        for (int i = 0; i < nm; i++) {
-            if (i < n) {
-                int sl = h + i;
-                if (sl >= cap) sl -= cap;
-                X_[i] = G.x[base + sl];
-                vset<kL>(V_, Vc, i, G.v[base + sl]);
-                dset(D2_, i, G.dst[base + sl]);
+        // Every load of the lane in flight at once: chunks of 8 vehicles
+        // (chunk count wave-uniform, bounded by the wave's longest lane) with
+        // constant register indices -- a rolled loop, indexing the arrays
+        // with a scalar (s_set_gpr_idx), waited out a memory round trip per
+        // vehicle.  Buffer loads: a vehicle past the lane's count gets an
+        // offset beyond the buffer's range, which makes no memory request
+        // and returns 0 (the array entries past the count are never read).
+        // The last vehicle (x, v) is picked from the loaded values.
+        const uint32_t nb = (uint32_t)NL * (uint32_t)cap * 4u;
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(G.x, 0, nb, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(G.v, 0, nb, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(G.dst, 0, nb, 0x00020000);
+#pragma unroll
+        for (int c = 0; c < RCAP / 8; c++) {
+            if (8 * c < nm) {
+                float tv[8];
+                uint32_t td[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int i = 8 * c + j;
+                    const int s0 = h + i, sl = s0 >= cap ? s0 - cap : s0;
+                    const uint32_t off = i < n ? (uint32_t)(base + sl) * 4u : 0x80000000u;
+                    X_[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, 0));
+                    tv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, off, 0, 0));
+                    td[j] = __builtin_amdgcn_raw_buffer_load_b32(rd, off, 0, 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int i = 8 * c + j;
+                    vset<kL>(V_, Vc, i, tv[j]);
+                    if (j & 1) D2_[i >> 1] = (td[j - 1] & 0xffffu) | (td[j] << 16);
+                    lx = i == n - 1 ? X_[i] : lx;
+                    lv = i == n - 1 ? tv[j] : lv;
+                }
             }
-        }
-        if (n > 0) {
-            lx = G.x[base + (h + n - 1 < cap ? h + n - 1 : h + n - 1 - cap)];
-            lv = G.v[base + (h + n - 1 < cap ? h + n - 1 : h + n - 1 - cap)];
         }
         s_cnt[l] = n;
         s_lx[l] = lx;
@@ -1464,25 +1485,44 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
                 bool det = lead_x_new >= dp && lead_x_old0 < dpl;
                 float lead_x_old = lead_x_old0, lead_v_old = lead_v_old0;
                 float last_x = X_[0], last_v = vget<kL>(V_, Vc, 0);
+                // (LDS speeds: vehicle i + 1's speed is read while vehicle i is
+                // computed -- the walk of the wave's longest lane otherwise
+                // waits out one LDS round trip per vehicle -- and its column
+                // slot is stepped from vehicle i's, which vehicle i's store
+                // then reuses; slot i + 1 <= RCAP stays in the column)
+                float vnx = 0.0f, *pn = nullptr;
+                int sn = 0;
+                if constexpr (kL) {
+                    sn = Vc.h + 1 == RCAP ? 0 : Vc.h + 1;
+                    pn = Vc.p + sn * NT;
+                    vnx = *pn;
+                }
                 for (int i = 1; i < nm; i++) {
                     if (i < n) {
-                        const float xi = X_[i], vi = vget<kL>(V_, Vc, i);
+                        const float xi = X_[i];
+                        float vi, *pc = pn;
+                        if constexpr (kL) {
+                            vi = vnx;
+                            sn = sn + 1 == RCAP ? 0 : sn + 1;
+                            pn = sn == 0 ? Vc.p : pn + NT;
+                            vnx = *pn;
+                        } else {
+                            vi = V_[i];
+                        }
                         const float gap = (lead_x_old - P.length) - xi;
                         const float acc = idm_acc(vi, gap, vi - lead_v_old, P);
                         float vn = clamp_speed(vi + acc, P);
                         float xn = xi + vn;
                         const float lim = lead_x_new - P.length;
-                        if (xn > lim) {
-                            if (lim < xi) {
-                                xn = xi;
-                                vn = 0.0f;
-                            } else {
-                                xn = lim;
-                                vn = lim - xi;
-                            }
-                        }
+                        // no overlap with the leader's new position: stop at
+                        // lim, or stand if lim is behind (selects, not branches)
+                        const bool over = xn > lim, stand = lim < xi;
+                        const float xc = stand ? xi : lim, vc = stand ? 0.0f : lim - xi;
+                        xn = over ? xc : xn;
+                        vn = over ? vc : vn;
                         X_[i] = xn;
-                        vset<kL>(V_, Vc, i, vn);
+                        if constexpr (kL) *pc = vn;
+                        else V_[i] = vn;
                         det = det || (xn >= dp && xi < dpl);
                         lead_x_old = xi;
                         lead_v_old = vi;
@@ -1564,14 +1604,43 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     const int t = t0 + K;
     // ---- outputs: halting counts, signals, running / pending, done
     int run = own ? n : 0, pend = leader ? qend - qp : 0;
+    // ... and the write-back of this lane's vehicles, compacted (head 0): as
+    // the staging, chunks of 8 with constant register indices (each chunk's
+    // LDS speed reads in flight together), buffer stores whose offset is out
+    // of range past the lane's count (dropped)
     {
         const int nm = wave_max_uniform(own ? n : 0);
-        if (own && l < 12 * A) {
+        if (own) {
+            const size_t base = (size_t)l * cap;
+            const uint32_t nb = (uint32_t)NL * (uint32_t)cap * 4u;
+            const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(G.x, 0, nb, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(G.v, 0, nb, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(G.dst, 0, nb, 0x00020000);
             int hc = 0;
-            for (int i = 0; i < nm; i++)
-                if (i < n) hc += vget<kL>(V_, Vc, i) < P.halt_speed ? 1 : 0;
-            halt[(size_t)blockIdx.x * 12 * A + l] = hc;
-            if constexpr (kFuse) s_halt[l] = hc;
+#pragma unroll
+            for (int c = 0; c < RCAP / 8; c++) {
+                if (8 * c < nm) {
+                    float tv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) tv[j] = vget<kL>(V_, Vc, 8 * c + j);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const int i = 8 * c + j;
+                        const bool in = i < n;
+                        const uint32_t off = in ? (uint32_t)(base + i) * 4u : 0x80000000u;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(X_[i]), rx, off, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(tv[j]), rv, off, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)dget(D2_, i), rd, off, 0, 0);
+                        hc += in && tv[j] < P.halt_speed ? 1 : 0;
+                    }
+                }
+            }
+            if (l < 12 * A) {
+                halt[(size_t)blockIdx.x * 12 * A + l] = hc;
+                if constexpr (kFuse) s_halt[l] = hc;
+            }
+            G.head[l] = 0;
+            G.cnt[l] = n;
         }
     }
     run = wave_sum(run);
@@ -1588,22 +1657,6 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     }
     if (S.actuated)
         for (int i = tid; i < 12 * A; i += NT) G.last_det[i] = s_ldet[i];
-    // ---- write-back: this lane's vehicles, compacted
-    {
-        const int nm = wave_max_uniform(own ? n : 0);
-        if (own) {
-            G.head[l] = 0;
-            G.cnt[l] = n;
-            const size_t base = (size_t)l * cap;
-            for (int i = 0; i < nm; i++) {
-                if (i < n) {
-                    G.x[base + i] = X_[i];
-                    G.v[base + i] = vget<kL>(V_, Vc, i);
-                    G.dst[base + i] = dget(D2_, i);
-                }
-            }
-        }
-    }
     if (leader) G.qptr[tid] = qp;
     __syncthreads();
     if (tid == 0) {

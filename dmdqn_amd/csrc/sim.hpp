@@ -248,9 +248,9 @@ __device__ __forceinline__ float idm_acc(float v, float s, float dv, const IdmK 
     float r2 = r * r;
     float r4 = r2 * r2;
     float ss = v * P.tau + (v * dv) * P.inv_two_sqrt_ab;
-    if (ss < 0.0f) ss = 0.0f;
+    ss = __builtin_fmaxf(ss, 0.0f);  // (clamps: see clamp_speed)
     float sstar = P.min_gap + ss;
-    if (s < 0.01f) s = 0.01f;
+    s = __builtin_fmaxf(s, 0.01f);
     float q = sstar / s;
     float t1 = 1.0f - r4;
     return P.accel * (t1 - q * q);
@@ -265,18 +265,23 @@ __device__ __forceinline__ float idm_sel(float v, float s, float dv, bool nofron
     float r2 = r * r;
     float r4 = r2 * r2;
     float ss = v * P.tau + (v * dv) * P.inv_two_sqrt_ab;
-    ss = ss < 0.0f ? 0.0f : ss;
+    ss = __builtin_fmaxf(ss, 0.0f);
     float sstar = P.min_gap + ss;
-    s = s < 0.01f ? 0.01f : s;
+    s = __builtin_fmaxf(s, 0.01f);
     float q = sstar / s;
     float t1 = 1.0f - r4;
     return P.accel * (t1 - (nofront ? 0.0f : q * q));
 }
 
+// v < 0 -> 0, v > vmax -> vmax, else v (oracle_sim.c's compares) as one
+// v_med3_f32; the IDM clamps above as v_max_f32.  The same bits for every
+// value these see: no NaN, and never -0.0 (speeds, gaps and the IDM terms are
+// sums of a +0 / positive speed term and products that round to +0 at worst,
+// x - x is +0 in round-to-nearest), where max / med3 could pick the other
+// zero.  Each select was a compare plus a cndmask in pass C's per-vehicle
+// chain, the longest lane's walk that bounds the pass.
 __device__ __forceinline__ float clamp_speed(float v, const IdmK &P) {
-    if (v < 0.0f) return 0.0f;
-    if (v > P.vmax) return P.vmax;
-    return v;
+    return __builtin_amdgcn_fmed3f(v, 0.0f, P.vmax);
 }
 
 }  // namespace dmdqn

@@ -40,6 +40,13 @@ def main():
 
     with cf.ThreadPoolExecutor(max_workers=8) as ex:
         objs = list(ex.map(compile_one, srcs))
+    # dmdqn_source_digest(), tagged with the revision: _lib.load() refuses it
+    # as stale unless DMDQN_ALLOW_FOREIGN_LIB=1 (tools/ab_swap.sh sets it)
+    dsrc = os.path.join(dst, "source_digest.cpp")
+    with open(dsrc, "w") as f:
+        f.write(f'extern "C" const char *dmdqn_source_digest(void) {{ return "rev-{rev}"; }}\n')
+    subprocess.run(["g++", "-c", "-fPIC", dsrc, "-o", dsrc + ".o"], check=True)
+    objs.append(dsrc + ".o")
     so = os.path.join(ROOT, "exp", f"libdmdqn_hip_{name}.so")
     subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o", so] + objs,
                    check=True)
