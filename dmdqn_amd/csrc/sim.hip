@@ -1149,45 +1149,41 @@ __host__ __device__ inline size_t reg_lds_total(int R, int C, bool fused, int ls
 // 16 waves' longest lanes summed to ~5.7x the vehicles / 64 of an 8x8 replica
 // (oracle, steady state), sorted ~2.7x.  Per-lane results do not depend on
 // which thread computes them (lanes meet only through lane-indexed LDS
-// arrays and integer counters), so the order changes no bit.  Counting sort:
-// one ballot per wave and count (RCAP + 1 keys), one LDS atomic per wave and
-// key, ranks from the ballot's lane prefix.
+// arrays and integer counters), so the order changes no bit -- nor does the
+// order of the lanes of equal count, which the LDS atomics below leave to
+// the hardware.  Counting sort: one LDS atomic per lane (its rank within its
+// count's bin), one wave's prefix scan over the RCAP + 1 bins, one store.
+// (Round 6's first form, a ballot and a wave-reduced atomic per wave and
+// key, took ~4.5 us of an 8x8 launch.)
+// Lane tid's count c and head h (loaded by the caller at the kernel's start)
+// are left in s_n / s_h (lane-indexed LDS) for the thread that takes the lane.
 template <int NT>
-__device__ void lane_order(const int32_t *cnt, int NL, uint16_t *s_lane, int32_t *s_bin) {
-    const int tid = threadIdx.x, ln = tid & 63;
+__device__ void lane_order(int c, int h, int NL, uint16_t *s_lane, int32_t *s_bin, int32_t *s_n,
+                           int32_t *s_h) {
+    const int tid = threadIdx.x;
     if (tid < 32) s_bin[tid] = 0;
-    __syncthreads();
-    int key = 31;  // threads without a lane take no rank
+    int key = 0;
     if (tid < NL) {
-        const int c = cnt[tid];
+        s_n[tid] = c;
+        s_h[tid] = h;
         key = RCAP - (c < 0 ? 0 : c > RCAP ? RCAP : c);
     }
-    for (int b = 0; b <= RCAP; b++) {
-        const uint64_t m = __ballot(key == b);
-        if (m && ln == 0) atomicAdd(&s_bin[b], (int)__popcll(m));
+    __syncthreads();
+    int r = 0;
+    if (tid < NL) r = atomicAdd(&s_bin[key], 1);
+    __syncthreads();
+    if (tid < 64) {  // exclusive prefix of the bins (wave 0)
+        const int v = tid <= RCAP ? s_bin[tid] : 0;
+        int x = v;
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) {
+            const int y = __shfl_up(x, off);
+            x += tid >= off ? y : 0;
+        }
+        if (tid <= RCAP) s_bin[tid] = x - v;
     }
     __syncthreads();
-    if (tid == 0) {
-        int acc = 0;
-        for (int b = 0; b <= RCAP; b++) {
-            const int c = s_bin[b];
-            s_bin[b] = acc;
-            acc += c;
-        }
-    }
-    __syncthreads();
-    for (int b = 0; b <= RCAP; b++) {
-        const uint64_t m = __ballot(key == b);
-        if (m) {  // wave-uniform
-            const int first = __ffsll((unsigned long long)m) - 1;
-            int base = 0;
-            if (ln == first) base = atomicAdd(&s_bin[b], (int)__popcll(m));
-            base = __shfl(base, first);
-            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (key == b) s_lane[base + below] = (uint16_t)tid;
-        }
-    }
+    if (tid < NL) s_lane[s_bin[key] + r] = (uint16_t)tid;
     __syncthreads();
 }
 
@@ -1205,6 +1201,22 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     EnvView G(S, blockIdx.x);
     const int A = G.A, NL = G.NL, cap = G.cap;
     const int tid = threadIdx.x;
+    // The prologue's loads are issued as early as their addresses allow, so
+    // that their memory round trips overlap (one wait covers several): this
+    // thread's origin queue position and end, and the counters (each wait
+    // below otherwise exposed one more round trip of the launch's start).
+    const bool leader = tid < 4 * A;  // origin queue q = tid
+    int qp = 0, qend = 0, qid = 0, qdst = 0;
+    if (leader) {
+        qp = G.qptr[tid];
+        qend = G.q_off[tid + 1];
+    }
+    const int st0 = tid < 2 ? G.stats[tid] : 0;
+    int cnt0 = 0, head0 = 0;  // lane tid's (lane_order)
+    if (tid < NL) {
+        cnt0 = G.cnt[tid];
+        head0 = G.head[tid];
+    }
     // ---- LDS: published per-lane values, signals, detector times, stats, topology
     // lane arrays LS entries apart (sim_reg_lds_bytes)
     constexpr int LS_ = SIM_LANE_STRIDE_NT ? NT : 0;
@@ -1216,15 +1228,36 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     int32_t *s_mdst = reinterpret_cast<int32_t *>(s_fv + LS), *s_ins = s_mdst + LS;
     int32_t *s_phase = s_ins + LS, *s_ts = s_phase + A, *s_ldet = s_ts + A;
     int32_t *s_stats = s_ldet + 12 * A;  // inserted, arrived, running, pending
+    // fused step: the MT stream past the block's own LDS; the halting counts
+    // later in the topology tables' place, the epilogue's scratch in the
+    // published-lane arrays (both dead by then).  The actions are drawn
+    // first: their two dependent loads (the stream position, then its words)
+    // overlap the topology's and the lanes' loads below.
+    const FuseLayout fl = fuse_layout(sim_reg_lds_bytes(S.R, S.C, LS), 0, (size_t)LS * 9 * 4, A);
+    int32_t *const s_halt = s_stats + 4;
+    int my_act = 0;
+    bool act_fast = false;
+    if constexpr (kFuse) my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off), act_fast);
     const Topo T = build_topo(s_stats + 4, S.R, S.C, S.exit_id, S.exit_ao, P.len_inner,
                               P.len_outer);  // synced below
 
     // ---- this thread's lane (registers) and origin queue
     // the lanes by descending vehicle count (lane_order): s_lane[tid] = lane
+#ifdef DMDQN_SIM_PROFILE
+    const uint64_t prof_topo = __builtin_amdgcn_s_memrealtime();  // after the act draw + topology
+#endif
     size_t perm_off = 0;
     (void)reg_lds_total(S.R, S.C, kFuse, LS, NT, &perm_off);
     uint16_t *const s_lane = reinterpret_cast<uint16_t *>(dyn + perm_off);
-    lane_order<NT>(G.cnt, NL, s_lane, reinterpret_cast<int32_t *>(dyn + perm_off + (size_t)NT * 2));
+    lane_order<NT>(cnt0, head0, NL, s_lane, reinterpret_cast<int32_t *>(dyn + perm_off + (size_t)NT * 2),
+                   s_cnt, s_gfrom);  // (s_gfrom: the heads until pass B)
+#ifdef DMDQN_SIM_PROFILE
+    const uint64_t prof_lo = __builtin_amdgcn_s_memrealtime();  // after lane_order
+#endif
+    if (leader && qp < qend) {  // in flight beside the vehicle staging
+        qid = G.q_ids[qp];
+        qdst = G.q_dst[qp];
+    }
     const bool own = tid < NL;
     const int l = own ? (int)s_lane[tid] : tid;  // (e = l / 3, kf = l % 3: inside the substep loop)
     constexpr bool kL = NT > 512;  // speeds in the LDS column (VColL)
@@ -1235,8 +1268,8 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     int n = 0;
     float lx = 0.0f, lv = 0.0f;
     if (own) {
-        const int h = G.head[l];
-        n = G.cnt[l];
+        const int h = s_gfrom[l];
+        n = s_cnt[l];
         DMDQN_DBG(h >= 0 && h < cap && n >= 0 && n <= RCAP && n <= cap, DBG_SIM_RING);
         const size_t base = (size_t)l * cap;
         const int nm = wave_max_uniform(n);
@@ -1284,23 +1317,11 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         const int nm = wave_max_uniform(0);
         (void)nm;
     }
-    const bool leader = tid < 4 * A;  // origin queue q = tid
-    int qp = 0, qend = 0, qid = 0, qdst = 0;
-    if (leader) {
-        qp = G.qptr[tid];
-        qend = G.q_off[tid + 1];
-        if (qp < qend) { qid = G.q_ids[qp]; qdst = G.q_dst[qp]; }
-    }
-    // fused step: the MT stream past the block's own LDS; the halting counts
-    // later in the topology tables' place, the epilogue's scratch in the
-    // published-lane arrays (both dead by then)
-    const FuseLayout fl = fuse_layout(sim_reg_lds_bytes(S.R, S.C, LS), 0, (size_t)LS * 9 * 4, A);
-    int32_t *const s_halt = s_stats + 4;
-    int my_act = 0;
-    bool act_fast = false;
+#ifdef DMDQN_SIM_PROFILE
+    const uint64_t prof_veh = __builtin_amdgcn_s_memrealtime();  // prologue to the staged vehicles
+#endif
     TailPre pre{};
     if constexpr (kFuse) {
-        my_act = fused_act(F, A, reinterpret_cast<uint32_t *>(dyn + fl.mt_off), act_fast);
         // (1024-thread blocks have no VGPRs to hold the prefetch across the substeps)
         if constexpr (!kL) pre = fused_prefetch(F, A);
         if (tid < A) {  // A <= NT (dmdqn_env_step)
@@ -1316,7 +1337,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     }
     if (S.actuated)
         for (int i = tid; i < 12 * A; i += NT) s_ldet[i] = G.last_det[i];
-    if (tid < 2) s_stats[tid] = G.stats[tid];
+    if (tid < 2) s_stats[tid] = st0;
     if (tid == 2 || tid == 3) s_stats[tid] = 0;
     __syncthreads();
     if constexpr (kFuse) {
@@ -1368,6 +1389,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
 #ifdef DMDQN_SIM_PROFILE
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memrealtime();
     prof[6] = prof_t - prof_t0;  // staging
+    prof[0] = prof_veh - prof_t0;  // (register path: slot 0 = the part up to the staged vehicles)
 #endif
     for (int k = 0; k < K; k++) {
         const int t = t0 + k;
@@ -1678,6 +1700,8 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     if (tid == 0) {
         prof[7] = __builtin_amdgcn_s_memrealtime() - prof_t;  // halting + write-back
         for (int i = 0; i < 8; i++) halt[(size_t)blockIdx.x * 12 * A + i] = (int32_t)prof[i];
+        halt[(size_t)blockIdx.x * 12 * A + 8] = (int32_t)(prof_topo - prof_t0);
+        halt[(size_t)blockIdx.x * 12 * A + 9] = (int32_t)(prof_lo - prof_t0);
     }
 #endif
 }

@@ -104,6 +104,32 @@ __device__ __forceinline__ Topo build_topo(int32_t *mem, int R, int C, const int
               nt = blockDim.x;
     int32_t *jrc = mem, *dinfo = jrc + A, *xid = dinfo + NE, *xao = xid + 4 * A;
     float *elen = reinterpret_cast<float *>(xao + 2 * X);
+    if (nt >= NE && nt >= 4 * A && nt >= 2 * X) {
+        // one entry of each table per thread: every load issued before the
+        // first store (one memory round trip; the loops below wait per table)
+        const int i = tid, ex = i - 4 * A;
+        const bool isx = ex >= 0 && i < NE;
+        const int vid = g_exit_id[i < 4 * A ? i : 0], vao = g_exit_ao[i < 2 * X ? i : 0];
+        const int xtj = g_exit_ao[isx ? 2 * ex : 0], xto = g_exit_ao[isx ? 2 * ex + 1 : 0];
+        if (i < A) jrc[i] = (i / C) * 16 + (i % C);
+        if (i < 4 * A) xid[i] = vid;
+        if (i < 2 * X) xao[i] = vao;
+        if (i < NE) {
+            int tj = xtj, to = xto;
+            bool inner = false;
+            if (!isx) {
+                const int b = i >> 2, db = i & 3, r = b / C, c = b % C;
+                tj = db == DIR_N ? (r > 0 ? b - C : -1) : db == DIR_S ? (r < R - 1 ? b + C : -1)
+                   : db == DIR_E ? (c < C - 1 ? b + 1 : -1) : (c > 0 ? b - 1 : -1);
+                inner = tj >= 0;
+                if (tj < 0) tj = 0;
+                to = opp(db);
+            }
+            dinfo[i] = tj * 4 + to;
+            elen[i] = inner ? len_inner : len_outer;
+        }
+        return Topo{R, C, A, jrc, dinfo, xid, xao, elen};
+    }
     for (int a = tid; a < A; a += nt) jrc[a] = (a / C) * 16 + (a % C);
     for (int i = tid; i < 4 * A; i += nt) xid[i] = g_exit_id[i];
     for (int i = tid; i < 2 * X; i += nt) xao[i] = g_exit_ao[i];
@@ -236,6 +262,25 @@ struct IdmK : dmdqn_idm {
         : dmdqn_idm(p), inv_vmax(1.0f / p.vmax), inv_two_sqrt_ab(1.0f / p.two_sqrt_ab) {}
 };
 
+// sstar / s rounded as IEEE f32 division: the compiler's expansion of `/`
+// (v_rcp_f32 refined by Newton-Raphson, then two residual corrections of the
+// quotient) without its v_div_scale / v_div_fmas scaling and v_div_fixup
+// special-case steps, which are the identity for the operands the IDM passes
+// -- finite and normal, the numerator in [min_gap, ~10^3], the denominator
+// clamped to >= 0.01 and below ~10^4: the same roundings in the same order,
+// so the same quotient bits, in 8 instructions instead of 12 (pass C's
+// per-vehicle chain; test_gpu_sim.py holds it to the oracle's `/`).
+__device__ __forceinline__ float idm_div(float a, float b) {
+    float y = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    float q = a * y;
+    const float r = __builtin_fmaf(-b, q, a);
+    q = __builtin_fmaf(r, y, q);
+    const float r2 = __builtin_fmaf(-b, q, a);
+    return __builtin_fmaf(r2, y, q);
+}
+
 __device__ __forceinline__ float idm_free(float v, const IdmK &P) {
     float r = v * P.inv_vmax;
     float r2 = r * r;
@@ -251,7 +296,7 @@ __device__ __forceinline__ float idm_acc(float v, float s, float dv, const IdmK 
     ss = __builtin_fmaxf(ss, 0.0f);  // (clamps: see clamp_speed)
     float sstar = P.min_gap + ss;
     s = __builtin_fmaxf(s, 0.01f);
-    float q = sstar / s;
+    float q = idm_div(sstar, s);
     float t1 = 1.0f - r4;
     return P.accel * (t1 - q * q);
 }
@@ -268,7 +313,7 @@ __device__ __forceinline__ float idm_sel(float v, float s, float dv, bool nofron
     ss = __builtin_fmaxf(ss, 0.0f);
     float sstar = P.min_gap + ss;
     s = __builtin_fmaxf(s, 0.01f);
-    float q = sstar / s;
+    float q = idm_div(sstar, s);
     float t1 = 1.0f - r4;
     return P.accel * (t1 - (nofront ? 0.0f : q * q));
 }

@@ -17,7 +17,7 @@ if fused:
     from dmdqn_amd.agent import AgentConfig, BatchedDQN  # noqa: E402
     ag = BatchedDQN(E, env.A, AgentConfig(replay_buffer_size=200), env_seeds=env.seeds)
 g = torch.Generator(device="cuda").manual_seed(0)
-acc = np.zeros(8)
+acc = np.zeros(10)
 n = 0
 for step in range(120):
     if fused:
@@ -28,8 +28,8 @@ for step in range(120):
         a = torch.randint(0, 4, (E, env.A), device="cuda", generator=g, dtype=torch.int32)
         env.step(a)
     if step >= 60:
-        acc += env.halt.reshape(E, -1)[:, :8].double().mean(0).cpu().numpy() / 100.0
+        acc += env.halt.reshape(E, -1)[:, :10].double().mean(0).cpu().numpy() / 100.0
         n += 1
-names = ["TL", "A front decide", "B grant", "C advance", "D append", "E insert", "staging",
-         "halt+writeback (+ fused epilogue)"]
+names = ["TL (reg path: prologue to staged vehicles, inside staging)", "A front decide", "B grant", "C advance", "D append", "E insert", "staging",
+         "halt+writeback (+ fused epilogue)", "(reg path) start to topology", "(reg path) start to lane order"]
 print({k: round(v / n, 2) for k, v in zip(names, acc)}, "us per launch (substep passes summed over K)")
