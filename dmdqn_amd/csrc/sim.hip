@@ -1274,8 +1274,9 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         const size_t base = (size_t)l * cap;
         const int nm = wave_max_uniform(n);
         // Every load of the lane in flight at once: chunks of 8 vehicles
-        // (chunk count wave-uniform, bounded by the wave's longest lane) with
-        // constant register indices -- a rolled loop, indexing the arrays
+        // (chunk count wave-uniform, bounded by the wave's longest lane; all
+        // chunks issued before the first is consumed) with constant register
+        // indices -- a rolled loop, indexing the arrays
         // with a scalar (s_set_gpr_idx), waited out a memory round trip per
         // vehicle.  Buffer loads: a vehicle past the lane's count gets an
         // offset beyond the buffer's range, which makes no memory request
@@ -1285,29 +1286,37 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(G.x, 0, nb, 0x00020000);
         const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(G.v, 0, nb, 0x00020000);
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(G.dst, 0, nb, 0x00020000);
+        float tv[RCAP] = {};
+        uint32_t td[RCAP] = {};
 #pragma unroll
         for (int c = 0; c < RCAP / 8; c++) {
             if (8 * c < nm) {
-                float tv[8];
-                uint32_t td[8];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
                     const int i = 8 * c + j;
                     const int s0 = h + i, sl = s0 >= cap ? s0 - cap : s0;
                     const uint32_t off = i < n ? (uint32_t)(base + sl) * 4u : 0x80000000u;
                     X_[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, 0));
-                    tv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, off, 0, 0));
-                    td[j] = __builtin_amdgcn_raw_buffer_load_b32(rd, off, 0, 0);
-                }
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const int i = 8 * c + j;
-                    vset<kL>(V_, Vc, i, tv[j]);
-                    if (j & 1) D2_[i >> 1] = (td[j - 1] & 0xffffu) | (td[j] << 16);
-                    lx = i == n - 1 ? X_[i] : lx;
-                    lv = i == n - 1 ? tv[j] : lv;
+                    tv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, off, 0, 0));
+                    td[i] = __builtin_amdgcn_raw_buffer_load_b32(rd, off, 0, 0);
                 }
             }
+        }
+        // (consumed unconditionally -- the same chunk conditions here let the
+        // compiler merge each chunk's loads with its consumption again, one
+        // wait per chunk; entries past the count are never read)
+#pragma unroll
+        for (int i = 0; i < RCAP; i++) {
+            vset<kL>(V_, Vc, i, tv[i]);
+            if (i & 1) {
+                // (an empty asm pins the packing here: hoisted into the chunk's
+                // load branch, it waited on each chunk's loads in turn)
+                uint32_t lo = td[i - 1], hi = td[i];
+                asm volatile("" : "+v"(lo), "+v"(hi));
+                D2_[i >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // lo.b0 lo.b1 hi.b0 hi.b1
+            }
+            lx = i == n - 1 ? X_[i] : lx;
+            lv = i == n - 1 ? tv[i] : lv;
         }
         s_cnt[l] = n;
         s_lx[l] = lx;
