@@ -1395,6 +1395,7 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
 
     tl_pass(t0);
     __syncthreads();
+    int rc_d0 = -1, rc_pk = 0;  // pass A's route cache (route words are >= 0)
 #ifdef DMDQN_SIM_PROFILE
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memrealtime();
     prof[6] = prof_t - prof_t0;  // staging
@@ -1409,50 +1410,59 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
         const int l = tq < NL ? (int)s_lane[tq] : tq, e = l / 3, kf = l - 3 * (l / 3);
         const float len = LANE_LEN();
         TAKE_INSERT();
-        // ---- A: the front vehicle decides (route, target lane, IDM, request)
+        // ---- A: the front vehicle decides (route, target lane, IDM, request).
+        // One IDM evaluation, its inputs chosen by selects (free road: no
+        // interaction term; green with a vehicle on the target lane: that
+        // vehicle; red / yellow: the stop line), as the LDS path's pass A --
+        // separate evaluations per branch ran every one a divergent wave
+        // took.  The route decisions of the front (its out-direction,
+        // movement, next edge and the movement it will take there) depend
+        // only on the lane and the front's route word: cached per thread
+        // (rc_d0; packed e2 | m << 12 | (mv2 + 1) << 16) and recomputed when
+        // the front changes.
         int rq = -1;
         float fx = 0.0f, fv = 0.0f;
         if (own && n > 0) {
             const float x0 = X_[0], v0 = vget<kL>(V_, Vc, 0);
             const int d0 = dget(D2_, 0);
-            float acc;
-            if (e >= 4 * A || on_final_edge(d0, e)) {  // exit edge or last edge: free road
-                acc = idm_free(v0, P);
-                fv = clamp_speed(v0 + acc, P);
-                fx = x0 + fv;
-                rq = kArrive;
-            } else {
+            const bool free_road = e >= 4 * A || on_final_edge(d0, e);
+            bool green = false, lead = false;
+            int tl = -1;
+            float xl = 0.0f, vl = 0.0f;
+            if (!free_road) {
                 const int aj = e >> 2, d = e & 3, h = opp(d);
-                const int o = out_dir(T, aj, h, d0);
-                const int m = movement(h, o);
-                DMDQN_DBG(T.nbr(aj, o) >= 0 || T.exit_id[aj * 4 + o] >= 0, DBG_SIM_EDGE);
-                const int e2 = next_edge(T, aj, o);
-                const int k2 = lane_for(T, e2, kf, route_advance(d0), s_cnt);
-                const int tl = e2 * 3 + k2;
-                const bool green = (green_mask(s_phase[aj]) >> (d * 4 + m)) & 1;
-                if (green) {
-                    if (s_cnt[tl] > 0) {
-                        const float xl = s_lx[tl], vl = s_lv[tl];
-                        const float gap = (len - x0) + (xl - P.length);
-                        acc = idm_acc(v0, gap, v0 - vl, P);
-                    } else {
-                        acc = idm_free(v0, P);
+                if (rc_d0 != d0) {
+                    const int o = out_dir(T, aj, h, d0);
+                    const int m = movement(h, o);
+                    DMDQN_DBG(T.nbr(aj, o) >= 0 || T.exit_id[aj * 4 + o] >= 0, DBG_SIM_EDGE);
+                    const int e2 = next_edge(T, aj, o);
+                    const int w2 = route_advance(d0);
+                    int mv2 = -1;
+                    if (!(e2 >= 4 * A || on_final_edge(w2, e2))) {
+                        const int h2 = opp(e2 & 3);
+                        mv2 = movement(h2, out_dir(T, e2 >> 2, h2, w2));
                     }
-                } else {
-                    const float gap = (len - x0) + P.min_gap;
-                    acc = idm_acc(v0, gap, v0, P);
+                    rc_pk = e2 | (m << 12) | ((mv2 + 1) << 16);
+                    rc_d0 = d0;
                 }
-                fv = clamp_speed(v0 + acc, P);
-                fx = x0 + fv;
-                if (fx > len) {
-                    if (green) {
-                        rq = tl;
-                    } else {
-                        fx = len;
-                        fv = 0.0f;
-                    }
-                }
+                const int e2 = rc_pk & 0xfff, m = (rc_pk >> 12) & 0xf, mv2 = (rc_pk >> 16) - 1;
+                const int k2 = mv2 < 0 ? kf : lane_for_move(mv2, e2, s_cnt);
+                tl = e2 * 3 + k2;
+                green = (green_mask(s_phase[aj]) >> (d * 4 + m)) & 1;
+                lead = green && s_cnt[tl] > 0;
+                xl = s_lx[tl];
+                vl = s_lv[tl];
             }
+            const bool nofront = free_road || (green && !lead);
+            const float gap = (len - x0) + (green ? (xl - P.length) : P.min_gap);
+            const float acc = idm_sel(v0, gap, v0 - (lead ? vl : 0.0f), nofront, P);
+            fv = clamp_speed(v0 + acc, P);
+            fx = x0 + fv;
+            const bool over = fx > len;
+            rq = free_road ? kArrive : (over && green ? tl : -1);
+            const bool stop = !free_road && over && !green;
+            fx = stop ? len : fx;
+            fv = stop ? 0.0f : fv;
             s_fx[l] = fx;
             s_fv[l] = fv;
         }
