@@ -1396,6 +1396,17 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
     tl_pass(t0);
     __syncthreads();
     int rc_d0 = -1, rc_pk = 0;  // pass A's route cache (route words are >= 0)
+    // Pass B's five feeder lanes of this thread's lane (static: computed once
+    // here, 10 bits each, bit 20 of fd_pk1 = the lane has feeders) instead of
+    // per substep
+    int fd_pk0 = 0, fd_pk1 = 0;
+    if (own) {
+        int as, o;
+        if (feed_src(T, l / 3, as, o)) {
+            fd_pk0 = feeder(as, o, 0) | (feeder(as, o, 1) << 10) | (feeder(as, o, 2) << 20);
+            fd_pk1 = feeder(as, o, 3) | (feeder(as, o, 4) << 10) | (1 << 20);
+        }
+    }
 #ifdef DMDQN_SIM_PROFILE
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memrealtime();
     prof[6] = prof_t - prof_t0;  // staging
@@ -1472,15 +1483,17 @@ k_sim_step_reg(dmdqn_sim S, dmdqn_idm Pa, const int32_t *actions, int stride, in
 
         // ---- B: this lane, as a target, grants one request if it has room
         if (own) {
-            int as, o, g = -1;
-            if (feed_src(T, e, as, o)) {
+            int g = -1;
+            if (fd_pk1 >> 20) {  // the lane has feeders (fd_pk0 / fd_pk1, above the loop)
                 int f[5];
+                f[0] = fd_pk0 & 1023;
+                f[1] = (fd_pk0 >> 10) & 1023;
+                f[2] = (fd_pk0 >> 20) & 1023;
+                f[3] = fd_pk1 & 1023;
+                f[4] = (fd_pk1 >> 10) & 1023;
                 uint32_t mask = 0;
 #pragma unroll
-                for (int i = 0; i < 5; i++) {
-                    f[i] = feeder(as, o, i);
-                    mask |= (s_req[f[i]] == l ? 1u : 0u) << i;
-                }
+                for (int i = 0; i < 5; i++) mask |= (s_req[f[i]] == l ? 1u : 0u) << i;
                 if (mask) {
                     const int start = t % 5;
                     const uint32_t rot = ((mask >> start) | (mask << (5 - start))) & 31u;
